@@ -1,0 +1,250 @@
+"""oracle/oracle.py -- TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of the CPU oracle (oracle/build/liboracle.so).  Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg import this module;
+the product (zkevm-prover_amd/) never does.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+P = 0xFFFFFFFF00000001
+
+_lib = None
+
+
+def build(force=False):
+    if force or not os.path.exists(_LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u64 = ctypes.c_uint64
+        ptr = ctypes.POINTER(ctypes.c_uint64)
+        sig = {
+            "oc_gl_mul": (u64, [u64, u64]),
+            "oc_gl_add": (u64, [u64, u64]),
+            "oc_gl_sub": (u64, [u64, u64]),
+            "oc_gl_inv": (u64, [u64]),
+            "oc_gl_pow": (u64, [u64, u64]),
+            "oc_gl_w": (u64, [ctypes.c_uint]),
+            "oc_gl3_mul": (None, [ptr, ptr, ptr]),
+            "oc_gl3_inv": (None, [ptr, ptr]),
+            "oc_ntt": (None, [ptr, ptr, u64, u64, ctypes.c_int]),
+            "oc_dft_naive": (None, [ptr, ptr, u64, u64, ctypes.c_int]),
+            "oc_extend_pol": (None, [ptr, ptr, u64, u64, u64]),
+            "oc_poseidon_full": (None, [ptr, ptr]),
+            "oc_poseidon_hash": (None, [ptr, ptr]),
+            "oc_linear_hash": (None, [ptr, ptr, u64]),
+            "oc_merkle_num_elements": (u64, [u64]),
+            "oc_merkletree": (None, [ptr, ptr, u64, u64]),
+            "oc_merkle_root": (None, [ptr, ptr, u64]),
+            "oc_merkle_proof_size": (u64, [u64]),
+            "oc_merkle_group_proof": (None, [ptr, ptr, ptr, u64, u64, u64]),
+            "oc_merkle_root_from_proof": (None, [ptr, ptr, u64, ptr, u64, u64]),
+            "oc_transcript_init": (None, [ctypes.c_void_p]),
+            "oc_transcript_put": (None, [ctypes.c_void_p, ptr, u64]),
+            "oc_transcript_get_fields1": (u64, [ctypes.c_void_p]),
+            "oc_transcript_get_field": (None, [ctypes.c_void_p, ptr]),
+            "oc_transcript_get_permutations": (None, [ctypes.c_void_p, ptr, u64, u64]),
+            "oc_fri_fold": (None, [ptr, ptr, u64, u64, ptr, u64]),
+            "oc_fri_fold_group": (None, [ptr, ptr, u64, u64, u64, ptr, u64]),
+            "oc_fri_get_transposed": (None, [ptr, ptr, u64, u64]),
+            "oc_batch_inverse3": (None, [ptr, ptr, u64]),
+            "oc_num_threads": (ctypes.c_int, []),
+            "oc_set_num_threads": (None, [ctypes.c_int]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    assert a.dtype == np.uint64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+
+
+def u64(x):
+    return np.ascontiguousarray(np.asarray(x, dtype=np.uint64))
+
+
+# ---------------------------------------------------------------- field
+def gl_mul(a, b): return lib().oc_gl_mul(a, b)
+def gl_add(a, b): return lib().oc_gl_add(a, b)
+def gl_sub(a, b): return lib().oc_gl_sub(a, b)
+def gl_inv(a): return lib().oc_gl_inv(a)
+def gl_pow(a, e): return lib().oc_gl_pow(a, e)
+def gl_w(n): return lib().oc_gl_w(n)
+
+
+def gl3_mul(a, b):
+    a, b = u64(a), u64(b)
+    o = np.zeros(3, np.uint64)
+    lib().oc_gl3_mul(_p(o), _p(a), _p(b))
+    return o
+
+
+def gl3_inv(a):
+    a = u64(a)
+    o = np.zeros(3, np.uint64)
+    lib().oc_gl3_inv(_p(o), _p(a))
+    return o
+
+
+# ---------------------------------------------------------------- NTT
+def ntt(x, inverse=False):
+    """x: (n, ncols) or (n,) uint64 row-major; returns the same shape."""
+    x = u64(x)
+    n = x.shape[0]
+    ncols = 1 if x.ndim == 1 else x.shape[1]
+    out = np.empty_like(x)
+    lib().oc_ntt(_p(out), _p(x), n, ncols, int(inverse))
+    return out
+
+
+def dft_naive(x, inverse=False):
+    x = u64(x)
+    n = x.shape[0]
+    ncols = 1 if x.ndim == 1 else x.shape[1]
+    out = np.empty_like(x)
+    lib().oc_dft_naive(_p(out), _p(x), n, ncols, int(inverse))
+    return out
+
+
+def extend_pol(x, n_ext):
+    x = u64(x)
+    n = x.shape[0]
+    ncols = 1 if x.ndim == 1 else x.shape[1]
+    shape = (n_ext,) if x.ndim == 1 else (n_ext, ncols)
+    out = np.empty(shape, np.uint64)
+    lib().oc_extend_pol(_p(out), _p(x), n_ext, n, ncols)
+    return out
+
+
+# ---------------------------------------------------------------- Poseidon
+def poseidon_full(x):
+    x = u64(x)
+    assert x.size == 12
+    o = np.zeros(12, np.uint64)
+    lib().oc_poseidon_full(_p(o), _p(x))
+    return o
+
+
+def poseidon_hash(x):
+    x = u64(x)
+    o = np.zeros(4, np.uint64)
+    lib().oc_poseidon_hash(_p(o), _p(x))
+    return o
+
+
+def linear_hash(x):
+    x = u64(x).reshape(-1)
+    o = np.zeros(4, np.uint64)
+    lib().oc_linear_hash(_p(o), _p(x) if x.size else _p(np.zeros(1, np.uint64)), x.size)
+    return o
+
+
+# ---------------------------------------------------------------- Merkle
+def merkletree(src):
+    """src: (nrows, ncols) row-major -> nodes array (getTreeNumElements)."""
+    src = u64(src)
+    nrows = src.shape[0]
+    ncols = src.shape[1] if src.ndim == 2 else 1
+    nodes = np.zeros(lib().oc_merkle_num_elements(nrows), np.uint64)
+    s = src if src.size else np.zeros(1, np.uint64)
+    lib().oc_merkletree(_p(nodes), _p(s), ncols, nrows)
+    return nodes
+
+
+def merkle_root(nodes):
+    return nodes[-4:].copy()
+
+
+def merkle_group_proof(nodes, src, idx):
+    src = u64(src)
+    nrows, ncols = src.shape[0], (src.shape[1] if src.ndim == 2 else 1)
+    nsib = lib().oc_merkle_proof_size(nrows)
+    proof = np.zeros(ncols + 4 * nsib, np.uint64)
+    s = src if src.size else np.zeros(1, np.uint64)
+    lib().oc_merkle_group_proof(_p(proof), _p(nodes), _p(s), ncols, nrows, idx)
+    return proof[:ncols], proof[ncols:].reshape(-1, 4)
+
+
+def merkle_root_from_proof(vals, siblings, idx):
+    vals = u64(vals).reshape(-1)
+    sib = u64(siblings).reshape(-1)
+    root = np.zeros(4, np.uint64)
+    v = vals if vals.size else np.zeros(1, np.uint64)
+    s = sib if sib.size else np.zeros(1, np.uint64)
+    lib().oc_merkle_root_from_proof(_p(root), _p(v), vals.size, _p(s), sib.size // 4, idx)
+    return root
+
+
+# ---------------------------------------------------------------- transcript
+class Transcript:
+    """Transcript (transcript.cpp:4-87) backed by the C oracle."""
+
+    def __init__(self):
+        self._buf = ctypes.create_string_buffer(8 * 24 + 8)
+        lib().oc_transcript_init(self._buf)
+
+    def put(self, vals):
+        v = u64(vals).reshape(-1)
+        if v.size:
+            lib().oc_transcript_put(self._buf, _p(v), v.size)
+
+    def get_fields1(self):
+        return lib().oc_transcript_get_fields1(self._buf)
+
+    def get_field(self):
+        o = np.zeros(3, np.uint64)
+        lib().oc_transcript_get_field(self._buf, _p(o))
+        return o
+
+    def get_permutations(self, n, nbits):
+        o = np.zeros(n, np.uint64)
+        lib().oc_transcript_get_permutations(self._buf, _p(o), n, nbits)
+        return o
+
+
+# ---------------------------------------------------------------- FRI
+def fri_fold(pol, pol_bits, out_bits, special_x, shift_inv):
+    pol = u64(pol).reshape(-1)
+    out = np.zeros(3 << out_bits, np.uint64)
+    sx = u64(special_x)
+    lib().oc_fri_fold(_p(out), _p(pol), pol_bits, out_bits, _p(sx), shift_inv)
+    return out
+
+
+def fri_fold_group(vals, g, pol_bits, special_x, shift_inv):
+    vals = u64(vals).reshape(-1)
+    out = np.zeros(3, np.uint64)
+    sx = u64(special_x)
+    lib().oc_fri_fold_group(_p(out), _p(vals), vals.size // 3, g, pol_bits, _p(sx), shift_inv)
+    return out
+
+
+def fri_get_transposed(pol, transpose_bits):
+    pol = u64(pol).reshape(-1)
+    aux = np.zeros_like(pol)
+    lib().oc_fri_get_transposed(_p(aux), _p(pol), pol.size // 3, transpose_bits)
+    return aux
+
+
+def batch_inverse3(x):
+    x = u64(x).reshape(-1)
+    o = np.zeros_like(x)
+    lib().oc_batch_inverse3(_p(o), _p(x), x.size // 3)
+    return o
