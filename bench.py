@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark of the MI355X STARK hot path.
+
+Workload (BASELINE.json configs[1]): the Goldilocks LDE of a 2^23-row trace to
+2^24 rows (blowup 2, coset shift 7), column-major in HBM, C = 100 committed
+columns per GPU -- NTT_Goldilocks::extendPol as called at starks.cpp:53.
+One "step" = one LDE of the whole per-GPU trace, inputs already resident in
+HBM.  Multi-GPU: columns are independent, so every rank extends its own 100
+columns with no data-path collective (weak scaling); the barrier + max over
+ranks of the timed region stay.
+
+value = LDE output elements produced by all ranks / second (Gelem/s).
+roofline = the dominant kernel (largest device time in the timed region),
+measured live with HIP events on the launch stream (zkgpu_prof_*), against
+8 TB/s; its algorithmic bytes per launch = every input element read once +
+every output element written once.
+cpu_baseline = the oracle's OpenMP LDE (oracle/ntt.c, a port of the
+reference algorithm) on a bounded sample (rank 0, N = 1 only).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--ncols C] [--log-n L]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "zkevm-prover_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "batch-proof STARK sec (2^23 trace) + Goldilocks NTT Gelem/s at 1/2/4/8 GPU"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--ncols", type=int, default=100)
+    ap.add_argument("--log-n", type=int, default=23)
+    ap.add_argument("--blowup-bits", type=int, default=1)
+    ap.add_argument("--cpu-sample-cols", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_COLS", "4")))
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(log_n, blow, ncols_sample):
+    """Oracle LDE (OpenMP) on a bounded sample: 2^log_n -> 2^(log_n+blow) x ncols_sample."""
+    import numpy as np
+    from oracle import oracle as oc
+    oc.lib()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    oc.lib().oc_set_num_threads(threads)
+    rng = np.random.default_rng(0x5EED)
+    x = rng.integers(0, 2**63, size=(1 << log_n, ncols_sample), dtype=np.uint64)
+    t0 = time.perf_counter()
+    oc.extend_pol(x, 1 << (log_n + blow))
+    dt = time.perf_counter() - t0
+    out_elems = (1 << (log_n + blow)) * ncols_sample
+    return {"value": out_elems / dt / 1e9, "unit": "Gelem/s", "cores": threads, "kind": "port",
+            "sample": "oracle extendPol 2^%d->2^%d x %d cols, %.1f s, %d threads (%s)"
+                      % (log_n, log_n + blow, ncols_sample, dt, threads, _cpu_model())}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import zkgpu
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    zkgpu.init(local)
+    stream = torch.cuda.current_stream()
+    zkgpu.set_stream(stream)
+
+    n = 1 << args.log_n
+    ne = n << args.blowup_bits
+    C = args.ncols
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED + rank)
+    # canonical Goldilocks values: uniform in [0, 2^63) < p
+    trace = torch.randint(0, 2**63 - 1, (C, n), dtype=torch.int64, device=dev, generator=g)
+    out = torch.empty((C, ne), dtype=torch.int64, device=dev)
+
+    def step():
+        zkgpu.extend_pol_dev(out, ne, trace, n, ne, n, C)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    zkgpu.prof_reset()
+    zkgpu.prof_enable(True)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    zkgpu.prof_enable(False)
+
+    # per-kernel live timings (HIP events on the launch stream)
+    kernels = {}
+    for k in zkgpu.prof_kernels():
+        launches, ms, by = zkgpu.prof_query(k)
+        kernels[k] = (launches, ms, by)
+    dom = max(kernels, key=lambda k: kernels[k][1])
+    launches, ms, by = kernels[dom]
+    avg_ms = ms / launches
+    achieved = (by / launches) / (avg_ms * 1e-3) / 1e9
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    if rank == 0:
+        total_elems = ne * C * world * args.steps
+        value = total_elems / elapsed / 1e9
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(args.log_n, args.blowup_bits, args.cpu_sample_cols)
+        lde_bytes = 8 * (n + ne) * C  # per step per GPU
+        res = {
+            "metric": METRIC,
+            "value": round(value, 4),
+            "unit": "Gelem/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64 (Goldilocks)",
+            "data": "synthetic (uniform canonical Goldilocks, torch generator seed 0x5EED+rank)",
+            "config": {
+                "workload": "LDE 2^%d -> 2^%d rows x %d cols per GPU (extendPol, starks.cpp:53), column-major in HBM"
+                            % (args.log_n, args.log_n + args.blowup_bits, C),
+                "log_n": args.log_n, "blowup_bits": args.blowup_bits, "ncols_per_gpu": C,
+                "parallelism": "column-sharded x%d (no data-path collective)" % world,
+            },
+            "roofline": {
+                "kernel": dom,
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "avg_launch_ms": round(avg_ms, 4),
+                "alg_bytes_per_launch": by / launches,
+                "lde_frac": round(lde_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+            },
+            "kernels": {k: {"launches": v[0], "avg_ms": round(v[1] / v[0], 4),
+                            "GB/s": round(v[2] / v[0] / (v[1] / v[0] * 1e-3) / 1e9, 1)} for k, v in kernels.items()},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,131 @@
+/*
+ * zkgpu.h -- C-ABI of libzkgpu, the MI355X (gfx950) STARK hot path for
+ * zkevm-prover.  Plain pointers and sizes only; every function returns
+ * ZKGPU_OK (0) or a negative error code, details in zkgpu_last_error().
+ *
+ * Two families:
+ *   - host-pointer drop-ins with the reference's row-major buffers
+ *     (stark_info.cpp:473-482 layout).  The library stages H2D, runs the HIP
+ *     kernels on its device copy (column-major "SoA" internally), and copies
+ *     the result back.  These are what the reference's C++ call sites bind to
+ *     (see INTEGRATION.md for the adapter classes).
+ *   - *_dev functions on device-resident column-major buffers (column c at
+ *     ptr + c*ld), for traces kept in HBM across stages.  No host copies.
+ *
+ * Element type: Goldilocks u64, p = 2^64 - 2^32 + 1; inputs may be
+ * non-canonical, outputs are canonical.  Extension elements are 3 u64.
+ *
+ * Threading: one calling host thread per process/device (the reference calls
+ * genProof from one thread, prover.cpp:182-255).  Kernels are enqueued on
+ * the stream given to zkgpu_set_stream (default: the null stream); host-
+ * pointer calls synchronise that stream before returning, *_dev calls do not.
+ */
+#ifndef ZKGPU_H
+#define ZKGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZKGPU_OK 0
+#define ZKGPU_ERR_HIP -1   /* HIP runtime error */
+#define ZKGPU_ERR_ARG -2   /* invalid argument / unsupported size */
+#define ZKGPU_ERR_INIT -3  /* zkgpu_init not called or failed */
+#define ZKGPU_ERR_OOM -4   /* device allocation failed */
+
+/* ---- lifecycle ------------------------------------------------------------
+ * Replaces the implicit setup of the Goldilocks submodule objects:
+ * NTT_Goldilocks(maxDomainSize, nThreads, extension) constructed at
+ * starks.hpp:81-82 and friProve.cpp:100 (twiddle tables), plus the Poseidon
+ * constant tables.  device = HIP device ordinal. */
+int zkgpu_init(int device);
+void zkgpu_release(void);
+const char *zkgpu_last_error(void);
+int zkgpu_set_stream(void *hip_stream);
+int zkgpu_synchronize(void);
+/* number of exported entry points (ABI self-check for tests) */
+int zkgpu_abi_version(void);
+
+/* ---- NTT ---------------------------------------------------------------
+ * NTT_Goldilocks::NTT / INTT(Element *dst, Element *src, uint64_t size,
+ * uint64_t ncols, Element *buffer, uint64_t nphase, uint64_t nblock)
+ * -- starks.cpp:262 (INTT NE x 3), :285 (NTT NE x 6), :326-327 (INTT N x 3),
+ * friProve.cpp:102.  Row-major n x ncols, natural order; INTT scales 1/n.
+ * dst may equal src.  n must be a power of two <= 2^28. */
+int zkgpu_gl_ntt(uint64_t *dst, const uint64_t *src, uint64_t n, uint64_t ncols, int inverse);
+
+/* NTT_Goldilocks::extendPol(Element *output, Element *input, uint64_t N_Extended,
+ * uint64_t N, uint64_t ncols, Element *buffer) -- starks.cpp:53,134,215.
+ * out[i][c] = P_c(7 * omega_{n_ext}^i), P_c interpolating in[.][c] on <omega_n>.
+ * Row-major in (n x ncols) and out (n_ext x ncols). */
+int zkgpu_gl_extend_pol(uint64_t *out, const uint64_t *in, uint64_t n_ext, uint64_t n, uint64_t ncols);
+
+/* device-resident, column-major variants */
+int zkgpu_gl_ntt_dev(uint64_t *dst, uint64_t ld_dst, const uint64_t *src, uint64_t ld_src, uint64_t n,
+                     uint64_t ncols, int inverse);
+int zkgpu_gl_extend_pol_dev(uint64_t *out, uint64_t ld_out, const uint64_t *in, uint64_t ld_in, uint64_t n_ext,
+                            uint64_t n, uint64_t ncols);
+/* row-major <-> column-major on device (boundary layout change) */
+int zkgpu_rows_to_cols_dev(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint64_t nrows, uint64_t ncols);
+int zkgpu_cols_to_rows_dev(uint64_t *rows, const uint64_t *cols, uint64_t ld, uint64_t nrows, uint64_t ncols);
+
+/* ---- Poseidon-GL --------------------------------------------------------
+ * PoseidonGoldilocks::hash_full_result(Element out[12], const Element in[12])
+ * -- transcript.cpp:23,46.  Computed on the GPU. */
+int zkgpu_gl_poseidon_full(uint64_t out[12], const uint64_t in[12]);
+/* PoseidonGoldilocks::hash(Element out[4], const Element in[12]) */
+int zkgpu_gl_poseidon_hash(uint64_t out[4], const uint64_t in[12]);
+/* PoseidonGoldilocks::linear_hash(Element *out, Element *in, uint64_t size)
+ * -- main_sm/fork_9/main_exec (utils.cpp:708).  One input row. */
+int zkgpu_gl_linear_hash(uint64_t out[4], const uint64_t *in, uint64_t size);
+/* batched permutation on device: in/out are n x 12 (full) or out n x 4 */
+int zkgpu_gl_poseidon_batch_dev(uint64_t *out, const uint64_t *in, uint64_t n, int full);
+
+/* ---- Merkle tree GL ----------------------------------------------------
+ * MerklehashGoldilocks::getTreeNumElements(nrows) (stark_info.hpp:332,
+ * build_const_tree.cpp:566-569): 4*nrows + 4*(nrows-1). */
+uint64_t zkgpu_gl_merkle_num_elements(uint64_t nrows);
+/* PoseidonGoldilocks::merkletree{,_avx,_avx512}(Element *tree, Element *input,
+ * uint64_t ncols, uint64_t nrows) -- merkleTreeGL.cpp:37-44,
+ * build_const_tree.cpp:582.  Row-major source; nrows a power of two. */
+int zkgpu_gl_merkletree(uint64_t *nodes, const uint64_t *src, uint64_t ncols, uint64_t nrows);
+/* device-resident: src column-major (ld), nodes on device */
+int zkgpu_gl_merkletree_dev(uint64_t *nodes, const uint64_t *src, uint64_t ld, uint64_t ncols, uint64_t nrows);
+/* device-resident, row-major source (FRI trees: friProve.cpp:117-121) */
+int zkgpu_gl_merkletree_rows_dev(uint64_t *nodes, const uint64_t *src, uint64_t ncols, uint64_t nrows);
+/* MerkleTreeGL::getGroupProof(Element *proof, uint64_t idx) for nq queries at
+ * once -- merkleTreeGL.cpp:12-35, friProve.cpp:195-232.
+ * vals_out: nq x ncols, sibs_out: nq x log2(nrows) x 4 (host pointers);
+ * src column-major on device (ld), nodes on device. */
+int zkgpu_gl_merkle_open_dev(uint64_t *vals_out, uint64_t *sibs_out, const uint64_t *nodes, const uint64_t *src,
+                             uint64_t ld, uint64_t ncols, uint64_t nrows, const uint64_t *idx, uint64_t nq);
+
+/* ---- FRI -----------------------------------------------------------------
+ * One fold step of FRIProve::prove (friProve.cpp:20-108), device-resident:
+ * pol has 2^pol_bits ext elements (interleaved, 3 u64 each), out 2^out_bits.
+ * special_x: host pointer to 3 u64; shift_inv: polShiftInv of this step. */
+int zkgpu_fri_fold_dev(uint64_t *out, const uint64_t *pol, uint32_t pol_bits, uint32_t out_bits,
+                       const uint64_t special_x[3], uint64_t shift_inv);
+/* FRIProve::getTransposed (friProve.cpp:252-270), ext elements, device */
+int zkgpu_fri_transpose_dev(uint64_t *aux, const uint64_t *pol, uint64_t degree, uint32_t transpose_bits);
+
+/* ---- live kernel profiling --------------------------------------------------
+ * With profiling on, every kernel launch is bracketed by HIP events recorded
+ * on the launch stream, tagged with the kernel name and its algorithmic bytes
+ * (each input element read once, each output element written once).
+ * zkgpu_prof_query synchronises the stream and returns, for one kernel name,
+ * the launch count, summed device time (ms) and summed algorithmic bytes.
+ * Replaces nothing in the reference (its TimerStart/TimerStopAndLog host
+ * timers, starks.cpp:49-403, are kept by the host adapter). */
+int zkgpu_prof_enable(int on);
+int zkgpu_prof_reset(void);
+int zkgpu_prof_query(const char *kernel, uint64_t *launches, double *total_ms, double *total_bytes);
+/* names of kernels seen since the last reset, '\n'-separated, into buf */
+int zkgpu_prof_kernels(char *buf, uint64_t buflen);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZKGPU_H */

@@ -1,0 +1,198 @@
+"""GPU parity: libzkgpu (HIP, via the C-ABI) vs the CPU oracle, bit-exact.
+
+Small and medium sizes compare against the oracle on the same seeded inputs;
+the full BASELINE sizes (2^23 -> 2^24) are checked in test_gpu_large.py
+through size-independent properties plus oracle spot checks.
+"""
+import numpy as np
+import pytest
+
+from golden_replay import check_proof
+
+pytestmark = pytest.mark.gpu
+
+P = 0xFFFFFFFF00000001
+
+
+def rand_gl(rng, shape, noncanon=False):
+    x = (rng.integers(0, 2**63, size=shape, dtype=np.uint64) * np.uint64(2) +
+         rng.integers(0, 2, size=shape, dtype=np.uint64))
+    if not noncanon:
+        x %= np.uint64(P)
+    return x
+
+
+# ------------------------------------------------------------------ NTT
+@pytest.mark.parametrize("logn,ncols", [(0, 1), (1, 2), (4, 3), (8, 1), (10, 5), (12, 2), (13, 1), (14, 3),
+                                        (16, 4), (17, 1), (19, 2)])
+def test_ntt_vs_oracle(oracle, zkgpu, logn, ncols):
+    rng = np.random.default_rng(100 + logn)
+    x = rand_gl(rng, (1 << logn, ncols))
+    for inv in (False, True):
+        assert np.array_equal(zkgpu.ntt(x, inv), oracle.ntt(x, inv)), (logn, ncols, inv)
+
+
+def test_ntt_noncanonical(oracle, zkgpu):
+    rng = np.random.default_rng(5)
+    x = rand_gl(rng, (1 << 14, 2), noncanon=True)
+    assert np.array_equal(zkgpu.ntt(x), oracle.ntt(x))
+
+
+@pytest.mark.parametrize("logn,blow,ncols", [(0, 1, 1), (3, 1, 2), (10, 1, 3), (12, 1, 4), (13, 1, 2),
+                                             (14, 2, 3), (16, 1, 8), (18, 1, 2)])
+def test_extend_pol_vs_oracle(oracle, zkgpu, logn, blow, ncols):
+    rng = np.random.default_rng(200 + logn)
+    x = rand_gl(rng, (1 << logn, ncols))
+    ne = 1 << (logn + blow)
+    assert np.array_equal(zkgpu.extend_pol(x, ne), oracle.extend_pol(x, ne))
+
+
+def test_extend_pol_dev_column_major(oracle, zkgpu):
+    """Device-resident SoA path with padded leading dimensions."""
+    import torch
+    rng = np.random.default_rng(9)
+    logn, ncols = 15, 5
+    n, ne = 1 << logn, 1 << (logn + 1)
+    x = rand_gl(rng, (n, ncols))
+    ld_in, ld_out = n + 64, ne + 128
+    cols = np.zeros((ncols, ld_in), np.uint64)
+    cols[:, :n] = x.T
+    din = zkgpu.to_device(cols)
+    dout = torch.zeros((ncols, ld_out), dtype=torch.int64, device="cuda:0")
+    zkgpu.set_stream(torch.cuda.current_stream())
+    zkgpu.extend_pol_dev(dout, ld_out, din, ld_in, ne, n, ncols)
+    torch.cuda.synchronize()
+    got = zkgpu.from_device(dout)[:, :ne].T
+    assert np.array_equal(got, oracle.extend_pol(x, ne))
+
+
+# ------------------------------------------------------------------ Poseidon
+def test_poseidon_vs_oracle(oracle, zkgpu):
+    rng = np.random.default_rng(11)
+    for i in range(20):
+        x = rand_gl(rng, 12, noncanon=(i % 3 == 0))
+        assert np.array_equal(zkgpu.poseidon_full(x), oracle.poseidon_full(x))
+        assert np.array_equal(zkgpu.poseidon_hash(x), oracle.poseidon_hash(x))
+    for x in (np.zeros(12, np.uint64), np.full(12, P - 1, np.uint64)):
+        assert np.array_equal(zkgpu.poseidon_full(x), oracle.poseidon_full(x))
+
+
+def test_poseidon_batch_dev(oracle, zkgpu):
+    import torch
+    rng = np.random.default_rng(12)
+    n = 10000
+    x = rand_gl(rng, (n, 12))
+    din = zkgpu.to_device(x)
+    dout = torch.zeros((n, 12), dtype=torch.int64, device="cuda:0")
+    zkgpu.poseidon_batch_dev(dout, din, n, True)
+    torch.cuda.synchronize()
+    got = zkgpu.from_device(dout)
+    for i in (0, 1, 4097, n - 1):
+        assert np.array_equal(got[i], oracle.poseidon_full(x[i]))
+
+
+@pytest.mark.parametrize("size", [0, 1, 3, 4, 5, 8, 9, 16, 17, 52, 100])
+def test_linear_hash_vs_oracle(oracle, zkgpu, size):
+    rng = np.random.default_rng(300 + size)
+    x = rand_gl(rng, size)
+    assert np.array_equal(zkgpu.linear_hash(x), oracle.linear_hash(x))
+
+
+# ------------------------------------------------------------------ Merkle
+@pytest.mark.parametrize("nrows,ncols", [(1, 5), (2, 3), (256, 0), (1024, 13), (4096, 100), (2048, 4), (8192, 9)])
+def test_merkletree_vs_oracle(oracle, zkgpu, nrows, ncols):
+    rng = np.random.default_rng(nrows + ncols)
+    src = rand_gl(rng, (nrows, ncols))
+    assert np.array_equal(zkgpu.merkletree(src), oracle.merkletree(src))
+
+
+def test_merkletree_dev_and_openings(oracle, zkgpu):
+    import torch
+    rng = np.random.default_rng(21)
+    nrows, ncols = 1 << 12, 21
+    src = rand_gl(rng, (nrows, ncols))
+    dsrc = zkgpu.to_device(np.ascontiguousarray(src.T))
+    nodes = torch.zeros(zkgpu.merkle_num_elements(nrows), dtype=torch.int64, device="cuda:0")
+    zkgpu.merkletree_dev(nodes, dsrc, nrows, ncols, nrows)
+    torch.cuda.synchronize()
+    ref_nodes = oracle.merkletree(src)
+    assert np.array_equal(zkgpu.from_device(nodes), ref_nodes)
+    idx = np.array([0, 1, 7, 2048, nrows - 1], np.uint64)
+    vals, sibs = zkgpu.merkle_open_dev(nodes, dsrc, nrows, ncols, nrows, idx)
+    for q, i in enumerate(idx):
+        v, s = oracle.merkle_group_proof(ref_nodes, src, int(i))
+        assert np.array_equal(vals[q], v)
+        assert np.array_equal(sibs[q], s)
+
+
+def test_merkletree_rows_dev(oracle, zkgpu):
+    import torch
+    rng = np.random.default_rng(22)
+    nrows, ncols = 1 << 10, 48
+    src = rand_gl(rng, (nrows, ncols))
+    nodes = torch.zeros(zkgpu.merkle_num_elements(nrows), dtype=torch.int64, device="cuda:0")
+    zkgpu.merkletree_rows_dev(nodes, zkgpu.to_device(src), ncols, nrows)
+    torch.cuda.synchronize()
+    assert np.array_equal(zkgpu.from_device(nodes), oracle.merkletree(src))
+
+
+# ------------------------------------------------------------------ FRI
+@pytest.mark.parametrize("pol_bits,out_bits", [(6, 2), (10, 6), (12, 9), (16, 12), (20, 16), (11, 11), (13, 8)])
+def test_fri_fold_vs_oracle(oracle, zkgpu, pol_bits, out_bits):
+    import torch
+    rng = np.random.default_rng(pol_bits * 31 + out_bits)
+    pol = rand_gl(rng, 3 << pol_bits)
+    sx = rand_gl(rng, 3)
+    sinv = oracle.gl_pow(oracle.gl_inv(7), 1 << (pol_bits % 5))
+    dpol = zkgpu.to_device(pol)
+    dout = torch.zeros(3 << out_bits, dtype=torch.int64, device="cuda:0")
+    zkgpu.fri_fold_dev(dout, dpol, pol_bits, out_bits, sx, sinv)
+    torch.cuda.synchronize()
+    assert np.array_equal(zkgpu.from_device(dout), oracle.fri_fold(pol, pol_bits, out_bits, sx, sinv))
+
+
+def test_fri_transpose(oracle, zkgpu):
+    import torch
+    rng = np.random.default_rng(23)
+    pol = rand_gl(rng, 3 << 12)
+    daux = torch.zeros(3 << 12, dtype=torch.int64, device="cuda:0")
+    zkgpu.fri_transpose_dev(daux, zkgpu.to_device(pol), 1 << 12, 8)
+    torch.cuda.synchronize()
+    assert np.array_equal(zkgpu.from_device(daux), oracle.fri_get_transposed(pol, 8))
+
+
+# ------------------------------------------------------------------ golden, through the GPU
+@pytest.mark.parametrize("name", ["recursive1.zkin.proof_0.json", "recursive2.zkin.proof_01.json"])
+def test_golden_replay_on_gpu(oracle, zkgpu, name):
+    """The reference's own proofs re-derived with GPU Poseidon/linear-hash and
+    the GPU fold kernel (transcript order and query indices from the oracle)."""
+    import torch
+
+    def root_from_proof(vals, sibs, idx):
+        cur = zkgpu.linear_hash(vals)
+        for s in np.asarray(sibs, np.uint64).reshape(-1, 4):
+            pair = np.concatenate([s, cur]) if idx & 1 else np.concatenate([cur, s])
+            cur = zkgpu.poseidon_hash(np.concatenate([pair, np.zeros(4, np.uint64)]))
+            idx >>= 1
+        return cur
+
+    cache = {}
+
+    def fold_group(vals, g, pol_bits, sx, sinv):
+        nx = vals.size // 3
+        out_bits = pol_bits - (nx.bit_length() - 1)
+        key = (pol_bits, out_bits)
+        if key not in cache:
+            cache[key] = (torch.zeros(3 << pol_bits, dtype=torch.int64, device="cuda:0"),
+                          torch.zeros(3 << out_bits, dtype=torch.int64, device="cuda:0"))
+        dpol, dout = cache[key]
+        dpol.zero_()
+        v = torch.from_numpy(np.ascontiguousarray(vals, np.uint64).view(np.int64)).to("cuda:0")
+        idx = torch.tensor([(j << out_bits) + g for j in range(nx)], device="cuda:0")
+        dpol.view(-1, 3)[idx] = v.view(-1, 3)
+        zkgpu.fri_fold_dev(dout, dpol, pol_bits, out_bits, sx, sinv)
+        torch.cuda.synchronize()
+        return zkgpu.from_device(dout[3 * g:3 * g + 3])
+
+    bad, _ = check_proof(oracle, name, root_from_proof=root_from_proof, fold_group=fold_group)
+    assert bad["s0"] == 0 and bad["fri_tree"] == 0 and bad["fold"] == 0 and bad["final"] == 0

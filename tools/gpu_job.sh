@@ -1,0 +1,73 @@
+#!/bin/bash
+# GPU job runner for gpurun: each GPU step has its own time limit; the job
+# stops at the first fault / abort / segfault / timeout (exit >= 124 or
+# signal), but continues past an ordinary test failure (exit 1).
+# Usage: tools/gpu_job.sh <step>...   steps: tests smoke bench prof pmc large
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+ok_or_stop() {
+    local rc=$1 what=$2
+    echo "[gpu_job] $what exit=$rc" | tee -a gpurun_out/job.log
+    if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then
+        echo "[gpu_job] stopping after $what (rc=$rc)" | tee -a gpurun_out/job.log
+        exit "$rc"
+    fi
+}
+for step in "$@"; do
+    case "$step" in
+    tests)
+        timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider --deselect tests/test_gpu_large.py \
+            > gpurun_out/pytest_gpu.log 2>&1
+        ok_or_stop $? "pytest -m gpu"
+        tail -5 gpurun_out/pytest_gpu.log
+        ;;
+    large)
+        timeout -k 10 900 python -m pytest tests/test_gpu_large.py -x -q -p no:cacheprovider \
+            > gpurun_out/pytest_gpu_large.log 2>&1
+        ok_or_stop $? "pytest large"
+        tail -5 gpurun_out/pytest_gpu_large.log
+        ;;
+    smoke)
+        timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+        ok_or_stop $? "smoke"
+        tail -3 gpurun_out/smoke.log
+        ;;
+    bench)
+        timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+        ok_or_stop $? "bench"
+        cat gpurun_out/bench.json
+        ;;
+    prof)
+        cd /tmp
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run \
+            --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu \
+            > "$GRAFT_REPO_ROOT/gpurun_out/prof_bench.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/prof.err"
+        rc=$?
+        cd "$GRAFT_REPO_ROOT"
+        ok_or_stop $rc "rocprofv3 kernel-trace"
+        find gpurun_out/prof -name "*stats*" | head
+        ;;
+    pmc)
+        cd /tmp
+        timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_fetch" -o run \
+            --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu --steps 2 --warmup 1 \
+            > /dev/null 2> "$GRAFT_REPO_ROOT/gpurun_out/pmc_fetch.err"
+        rc=$?
+        cd "$GRAFT_REPO_ROOT"
+        ok_or_stop $rc "rocprofv3 pmc FETCH_SIZE"
+        cd /tmp
+        timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_write" -o run \
+            --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu --steps 2 --warmup 1 \
+            > /dev/null 2> "$GRAFT_REPO_ROOT/gpurun_out/pmc_write.err"
+        rc=$?
+        cd "$GRAFT_REPO_ROOT"
+        ok_or_stop $rc "rocprofv3 pmc WRITE_SIZE"
+        ;;
+    *)
+        echo "unknown step $step"
+        ;;
+    esac
+done
+echo "[gpu_job] done" | tee -a gpurun_out/job.log

@@ -1,0 +1,546 @@
+// libzkgpu C-ABI (include/zkgpu.h): context, tables, host-pointer drop-ins
+// and device-resident entry points.  All bulk arithmetic runs in the HIP
+// kernels of ntt.hip / poseidon.hip / fri.hip; the host only stages buffers
+// and computes a handful of scalar constants (roots, inverses).
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "gl_device.hpp"
+#include "zkgpu_internal.hpp"
+
+namespace zk {
+
+int upload_poseidon_constants(Ctx &c);
+
+static Ctx g_ctx;
+static thread_local char g_err[512] = "";
+
+Ctx &ctx() { return g_ctx; }
+
+int set_error(int code, const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int check_hip(hipError_t e, const char *what)
+{
+    if (e != hipSuccess) return set_error(ZKGPU_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    return ZKGPU_OK;
+}
+
+int check_launch(const char *what) { return check_hip(hipGetLastError(), what); }
+
+uint64_t *workspace(int i, size_t bytes)
+{
+    Workspace &w = g_ctx.ws[i];
+    if (w.bytes >= bytes) return (uint64_t *)w.ptr;
+    if (w.ptr) {
+        (void)hipStreamSynchronize(g_ctx.stream);
+        (void)hipFree(w.ptr);
+        w.ptr = nullptr;
+        w.bytes = 0;
+    }
+    if (hipMalloc(&w.ptr, bytes) != hipSuccess) {
+        w.ptr = nullptr;
+        set_error(ZKGPU_ERR_OOM, "workspace %d: hipMalloc(%zu) failed", i, bytes);
+        return nullptr;
+    }
+    w.bytes = bytes;
+    return (uint64_t *)w.ptr;
+}
+
+// ---- host scalar field (setup constants only)
+static const uint64_t HP = 0xFFFFFFFF00000001ULL;
+uint64_t h_mul(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) % HP); }
+uint64_t h_pow(uint64_t a, uint64_t e)
+{
+    uint64_t r = 1;
+    a %= HP;
+    while (e) {
+        if (e & 1) r = h_mul(r, a);
+        a = h_mul(a, a);
+        e >>= 1;
+    }
+    return r;
+}
+uint64_t h_inv(uint64_t a) { return h_pow(a, HP - 2); }
+uint64_t h_w(uint32_t n)
+{
+    uint64_t w = 7277203076849721926ULL;  // W[32]
+    for (uint32_t i = n; i < 32; i++) w = h_mul(w, w);
+    return w;
+}
+
+static int alloc_dev(uint64_t **p, size_t n)
+{
+    if (hipMalloc((void **)p, n * sizeof(uint64_t)) != hipSuccess)
+        return set_error(ZKGPU_ERR_OOM, "hipMalloc(%zu) failed", n * sizeof(uint64_t));
+    return 0;
+}
+
+// LDE post-scale tables: factor(k) = 1/n * 7^k = lo[k & 4095] * hi[k >> 12]
+static int ensure_post_tables(uint32_t logn)
+{
+    Ctx &c = g_ctx;
+    if (c.post_lo && c.post_logn == logn) return 0;
+    if (c.post_lo) {
+        (void)hipStreamSynchronize(c.stream);
+        (void)hipFree(c.post_lo);
+        (void)hipFree(c.post_hi);
+        c.post_lo = c.post_hi = nullptr;
+    }
+    uint64_t n = 1ULL << logn;
+    uint64_t nlo = 1ULL << POST_BITS;
+    uint64_t nhi = n > nlo ? n >> POST_BITS : 1;
+    int rc;
+    if ((rc = alloc_dev(&c.post_lo, nlo)) || (rc = alloc_dev(&c.post_hi, nhi))) return rc;
+    fill_powers(c.post_lo, 7, 1, 1, nlo, c.stream);
+    fill_powers(c.post_hi, 7, nlo, h_inv(n), nhi, c.stream);
+    c.post_logn = logn;
+    return check_launch("post tables");
+}
+
+static int require_init()
+{
+    if (!g_ctx.ready) return set_error(ZKGPU_ERR_INIT, "zkgpu_init() not called");
+    return 0;
+}
+
+static bool is_pow2(uint64_t n) { return n && !(n & (n - 1)); }
+static uint32_t log2u(uint64_t n)
+{
+    uint32_t l = 0;
+    while ((1ULL << l) < n) l++;
+    return l;
+}
+
+// device LDE on column-major buffers
+static int extend_pol_dev(uint64_t *out, uint64_t ld_out, const uint64_t *in, uint64_t ld_in, uint64_t n_ext,
+                          uint64_t n, uint64_t ncols)
+{
+    if (!ncols || !n) return 0;
+    if (!is_pow2(n) || !is_pow2(n_ext) || n_ext < n)
+        return set_error(ZKGPU_ERR_ARG, "extend_pol: sizes must be powers of two with n_ext >= n");
+    uint32_t logn = log2u(n), loge = log2u(n_ext);
+    if (loge > TW_MAX_LOG) return set_error(ZKGPU_ERR_ARG, "extend_pol: n_ext > 2^%u", TW_MAX_LOG);
+    int rc;
+    if ((rc = ensure_post_tables(logn))) return rc;
+    Ctx &c = g_ctx;
+    // column batching bounds the scratch and keeps a batch's passes cache-resident
+    uint64_t batch = ncols;
+    const char *env = getenv("ZKGPU_LDE_BATCH_COLS");
+    if (env && atoll(env) > 0) batch = (uint64_t)atoll(env);
+    if (batch > ncols) batch = ncols;
+    uint64_t *coef = workspace(0, batch * n * sizeof(uint64_t));
+    uint64_t *tmp = workspace(1, batch * n_ext * sizeof(uint64_t));
+    if (!coef || !tmp) return ZKGPU_ERR_OOM;
+    uint32_t post_bits = logn < POST_BITS ? logn : POST_BITS;
+    for (uint64_t c0 = 0; c0 < ncols; c0 += batch) {
+        uint64_t nc = ncols - c0 < batch ? ncols - c0 : batch;
+        // coefficients * 7^k / n
+        if ((rc = ntt_columns(c, coef, n, in + c0 * ld_in, ld_in, n, tmp, n, logn, nc, 1, c.post_lo, c.post_hi,
+                              post_bits, 1, c.stream)))
+            return rc;
+        // evaluations on the extended domain (zero padding = predicated loads)
+        if ((rc = ntt_columns(c, out + c0 * ld_out, ld_out, coef, n, n, tmp, n_ext, loge, nc, 0, nullptr, nullptr, 0,
+                              1, c.stream)))
+            return rc;
+    }
+    return 0;
+}
+
+static int ntt_dev(uint64_t *dst, uint64_t ld_dst, const uint64_t *src, uint64_t ld_src, uint64_t n, uint64_t ncols,
+                   int inverse)
+{
+    if (!ncols || !n) return 0;
+    if (!is_pow2(n)) return set_error(ZKGPU_ERR_ARG, "ntt: n must be a power of two");
+    uint32_t logn = log2u(n);
+    if (logn > TW_MAX_LOG) return set_error(ZKGPU_ERR_ARG, "ntt: n > 2^%u", TW_MAX_LOG);
+    Ctx &c = g_ctx;
+    uint64_t *tmp = nullptr;
+    if (logn > 12) {
+        tmp = workspace(1, ncols * n * sizeof(uint64_t));
+        if (!tmp) return ZKGPU_ERR_OOM;
+    }
+    uint64_t scale = inverse ? h_inv(n) : 1;
+    return ntt_columns(c, dst, ld_dst, src, ld_src, n, tmp, n, logn, ncols, inverse, nullptr, nullptr, 0, scale,
+                       c.stream);
+}
+
+}  // namespace zk
+
+using namespace zk;
+
+extern "C" {
+
+int zkgpu_abi_version(void) { return 1; }
+
+const char *zkgpu_last_error(void) { return g_err; }
+
+int zkgpu_init(int device)
+{
+    Ctx &c = g_ctx;
+    if (c.ready && c.device == device) return 0;
+    int rc;
+    if ((rc = check_hip(hipSetDevice(device), "hipSetDevice"))) return rc;
+    c.device = device;
+    for (int d = 0; d < 2; d++) {
+        if ((rc = alloc_dev(&c.rt_small[d], 2048)) || (rc = alloc_dev(&c.tw_lo[d], TW_LEVEL_SIZE)) ||
+            (rc = alloc_dev(&c.tw_hi[d], TW_LEVEL_SIZE)))
+            return rc;
+        uint64_t w12 = h_w(12), w28 = h_w(TW_MAX_LOG);
+        if (d) {
+            w12 = h_inv(w12);
+            w28 = h_inv(w28);
+        }
+        fill_powers(c.rt_small[d], w12, 1, 1, 2048, c.stream);
+        fill_powers(c.tw_lo[d], w28, 1, 1, TW_LEVEL_SIZE, c.stream);
+        fill_powers(c.tw_hi[d], w28, TW_LEVEL_SIZE, 1, TW_LEVEL_SIZE, c.stream);
+    }
+    if ((rc = upload_poseidon_constants(c))) return rc;
+    if ((rc = check_launch("init tables"))) return rc;
+    if ((rc = check_hip(hipStreamSynchronize(c.stream), "init sync"))) return rc;
+    c.ready = true;
+    return 0;
+}
+
+void zkgpu_release(void)
+{
+    Ctx &c = g_ctx;
+    if (!c.ready) return;
+    (void)hipDeviceSynchronize();
+    for (int d = 0; d < 2; d++) {
+        (void)hipFree(c.rt_small[d]);
+        (void)hipFree(c.tw_lo[d]);
+        (void)hipFree(c.tw_hi[d]);
+    }
+    if (c.post_lo) (void)hipFree(c.post_lo);
+    if (c.post_hi) (void)hipFree(c.post_hi);
+    for (auto &w : c.ws)
+        if (w.ptr) (void)hipFree(w.ptr);
+    c = Ctx();
+}
+
+int zkgpu_set_stream(void *s)
+{
+    g_ctx.stream = (hipStream_t)s;
+    return 0;
+}
+
+int zkgpu_synchronize(void) { return check_hip(hipStreamSynchronize(g_ctx.stream), "synchronize"); }
+
+// ---------------------------------------------------------------- NTT
+int zkgpu_gl_ntt_dev(uint64_t *dst, uint64_t ld_dst, const uint64_t *src, uint64_t ld_src, uint64_t n, uint64_t ncols,
+                     int inverse)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    return ntt_dev(dst, ld_dst, src, ld_src, n, ncols, inverse);
+}
+
+int zkgpu_gl_extend_pol_dev(uint64_t *out, uint64_t ld_out, const uint64_t *in, uint64_t ld_in, uint64_t n_ext,
+                            uint64_t n, uint64_t ncols)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    return extend_pol_dev(out, ld_out, in, ld_in, n_ext, n, ncols);
+}
+
+int zkgpu_rows_to_cols_dev(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint64_t nrows, uint64_t ncols)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    rows_to_cols(rows, cols, nrows, ncols, ld, g_ctx.stream);
+    return check_launch("rows_to_cols");
+}
+
+int zkgpu_cols_to_rows_dev(uint64_t *rows, const uint64_t *cols, uint64_t ld, uint64_t nrows, uint64_t ncols)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    cols_to_rows(cols, rows, nrows, ncols, ld, g_ctx.stream);
+    return check_launch("cols_to_rows");
+}
+
+// host-pointer drop-ins: H2D row-major -> column-major on device -> kernels
+// -> row-major -> D2H.  Staging buffers: ws[2] (input cols), ws[3] (output).
+int zkgpu_gl_ntt(uint64_t *dst, const uint64_t *src, uint64_t n, uint64_t ncols, int inverse)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!n || !ncols) return 0;
+    Ctx &c = g_ctx;
+    size_t bytes = n * ncols * sizeof(uint64_t);
+    uint64_t *rows = workspace(2, bytes);
+    uint64_t *cols = workspace(3, bytes);
+    if (!rows || !cols) return ZKGPU_ERR_OOM;
+    if ((rc = check_hip(hipMemcpyAsync(rows, src, bytes, hipMemcpyHostToDevice, c.stream), "H2D"))) return rc;
+    rows_to_cols(rows, cols, n, ncols, n, c.stream);
+    if ((rc = ntt_dev(cols, n, cols, n, n, ncols, inverse))) return rc;
+    cols_to_rows(cols, rows, n, ncols, n, c.stream);
+    if ((rc = check_hip(hipMemcpyAsync(dst, rows, bytes, hipMemcpyDeviceToHost, c.stream), "D2H"))) return rc;
+    return check_hip(hipStreamSynchronize(c.stream), "ntt sync");
+}
+
+int zkgpu_gl_extend_pol(uint64_t *out, const uint64_t *in, uint64_t n_ext, uint64_t n, uint64_t ncols)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!n || !ncols) return 0;
+    if (n_ext < n) return set_error(ZKGPU_ERR_ARG, "extend_pol: n_ext < n");
+    Ctx &c = g_ctx;
+    size_t in_bytes = n * ncols * sizeof(uint64_t), out_bytes = n_ext * ncols * sizeof(uint64_t);
+    uint64_t *rows = workspace(2, out_bytes);
+    uint64_t *cols = workspace(3, out_bytes + in_bytes);
+    if (!rows || !cols) return ZKGPU_ERR_OOM;
+    uint64_t *cin = cols + n_ext * ncols;
+    if ((rc = check_hip(hipMemcpyAsync(rows, in, in_bytes, hipMemcpyHostToDevice, c.stream), "H2D"))) return rc;
+    rows_to_cols(rows, cin, n, ncols, n, c.stream);
+    if ((rc = extend_pol_dev(cols, n_ext, cin, n, n_ext, n, ncols))) return rc;
+    cols_to_rows(cols, rows, n_ext, ncols, n_ext, c.stream);
+    if ((rc = check_hip(hipMemcpyAsync(out, rows, out_bytes, hipMemcpyDeviceToHost, c.stream), "D2H"))) return rc;
+    return check_hip(hipStreamSynchronize(c.stream), "extend_pol sync");
+}
+
+// ---------------------------------------------------------------- Poseidon
+static int poseidon_one(uint64_t *out, const uint64_t *in, int full)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    Ctx &c = g_ctx;
+    uint64_t *d = workspace(2, 24 * sizeof(uint64_t));
+    if (!d) return ZKGPU_ERR_OOM;
+    if ((rc = check_hip(hipMemcpyAsync(d, in, 12 * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream), "H2D")))
+        return rc;
+    if ((rc = poseidon_batch(d + 12, d, 1, full, c.stream))) return rc;
+    if ((rc = check_hip(hipMemcpyAsync(out, d + 12, (full ? 12 : 4) * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                       c.stream),
+                        "D2H")))
+        return rc;
+    return check_hip(hipStreamSynchronize(c.stream), "poseidon sync");
+}
+
+int zkgpu_gl_poseidon_full(uint64_t out[12], const uint64_t in[12]) { return poseidon_one(out, in, 1); }
+int zkgpu_gl_poseidon_hash(uint64_t out[4], const uint64_t in[12]) { return poseidon_one(out, in, 0); }
+
+int zkgpu_gl_poseidon_batch_dev(uint64_t *out, const uint64_t *in, uint64_t n, int full)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    return poseidon_batch(out, in, n, full, g_ctx.stream);
+}
+
+int zkgpu_gl_linear_hash(uint64_t out[4], const uint64_t *in, uint64_t size)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    Ctx &c = g_ctx;
+    uint64_t *d = workspace(2, (size + 4) * sizeof(uint64_t));
+    if (!d) return ZKGPU_ERR_OOM;
+    if (size && (rc = check_hip(hipMemcpyAsync(d + 4, in, size * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream),
+                                "H2D")))
+        return rc;
+    // one row of `size` columns, column-major with ld = 1
+    if ((rc = merkle_leaves_cols(d, d + 4, size, 1, 1, c.stream))) return rc;
+    if ((rc = check_hip(hipMemcpyAsync(out, d, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream), "D2H")))
+        return rc;
+    return check_hip(hipStreamSynchronize(c.stream), "linear_hash sync");
+}
+
+// ---------------------------------------------------------------- Merkle
+uint64_t zkgpu_gl_merkle_num_elements(uint64_t nrows) { return nrows ? 4 * nrows + 4 * (nrows - 1) : 0; }
+
+int zkgpu_gl_merkletree_dev(uint64_t *nodes, const uint64_t *src, uint64_t ld, uint64_t ncols, uint64_t nrows)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!nrows) return 0;
+    if (!is_pow2(nrows)) return set_error(ZKGPU_ERR_ARG, "merkletree: nrows must be a power of two");
+    if ((rc = merkle_leaves_cols(nodes, src, ncols, nrows, ld, g_ctx.stream))) return rc;
+    return merkle_levels(nodes, nrows, g_ctx.stream);
+}
+
+int zkgpu_gl_merkletree_rows_dev(uint64_t *nodes, const uint64_t *src, uint64_t ncols, uint64_t nrows)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!nrows) return 0;
+    if (!is_pow2(nrows)) return set_error(ZKGPU_ERR_ARG, "merkletree: nrows must be a power of two");
+    if ((rc = merkle_leaves_rows(nodes, src, ncols, nrows, g_ctx.stream))) return rc;
+    return merkle_levels(nodes, nrows, g_ctx.stream);
+}
+
+int zkgpu_gl_merkletree(uint64_t *nodes, const uint64_t *src, uint64_t ncols, uint64_t nrows)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!nrows) return 0;
+    if (!is_pow2(nrows)) return set_error(ZKGPU_ERR_ARG, "merkletree: nrows must be a power of two");
+    Ctx &c = g_ctx;
+    size_t src_bytes = nrows * ncols * sizeof(uint64_t);
+    size_t nodes_bytes = zkgpu_gl_merkle_num_elements(nrows) * sizeof(uint64_t);
+    uint64_t *rows = workspace(2, src_bytes + 8);
+    uint64_t *dn = workspace(3, nodes_bytes + src_bytes + 8);
+    if (!rows || !dn) return ZKGPU_ERR_OOM;
+    uint64_t *cols = dn + zkgpu_gl_merkle_num_elements(nrows);
+    if (src_bytes &&
+        (rc = check_hip(hipMemcpyAsync(rows, src, src_bytes, hipMemcpyHostToDevice, c.stream), "H2D")))
+        return rc;
+    rows_to_cols(rows, cols, nrows, ncols, nrows, c.stream);
+    if ((rc = merkle_leaves_cols(dn, cols, ncols, nrows, nrows, c.stream))) return rc;
+    if ((rc = merkle_levels(dn, nrows, c.stream))) return rc;
+    if ((rc = check_hip(hipMemcpyAsync(nodes, dn, nodes_bytes, hipMemcpyDeviceToHost, c.stream), "D2H"))) return rc;
+    return check_hip(hipStreamSynchronize(c.stream), "merkletree sync");
+}
+
+int zkgpu_gl_merkle_open_dev(uint64_t *vals_out, uint64_t *sibs_out, const uint64_t *nodes, const uint64_t *src,
+                             uint64_t ld, uint64_t ncols, uint64_t nrows, const uint64_t *idx, uint64_t nq)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!nq) return 0;
+    Ctx &c = g_ctx;
+    uint32_t nlev = log2u(nrows);
+    for (uint64_t q = 0; q < nq; q++)
+        if (idx[q] >= nrows) return set_error(ZKGPU_ERR_ARG, "merkle_open: index %llu >= nrows", (unsigned long long)idx[q]);
+    size_t nv = nq * ncols, ns = nq * nlev * 4;
+    uint64_t *d = workspace(2, (nq + nv + ns + 1) * sizeof(uint64_t));
+    if (!d) return ZKGPU_ERR_OOM;
+    uint64_t *didx = d, *dv = d + nq, *ds = d + nq + nv;
+    if ((rc = check_hip(hipMemcpyAsync(didx, idx, nq * sizeof(uint64_t), hipMemcpyHostToDevice, c.stream), "H2D")))
+        return rc;
+    if ((rc = merkle_open_cols(dv, ds, nodes, src, ncols, nrows, ld, didx, nq, c.stream))) return rc;
+    if (nv && (rc = check_hip(hipMemcpyAsync(vals_out, dv, nv * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream),
+                              "D2H")))
+        return rc;
+    if (ns && (rc = check_hip(hipMemcpyAsync(sibs_out, ds, ns * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream),
+                              "D2H")))
+        return rc;
+    return check_hip(hipStreamSynchronize(c.stream), "merkle_open sync");
+}
+
+// ---------------------------------------------------------------- FRI
+int zkgpu_fri_fold_dev(uint64_t *out, const uint64_t *pol, uint32_t pol_bits, uint32_t out_bits,
+                       const uint64_t special_x[3], uint64_t shift_inv)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    return fri_fold(out, pol, pol_bits, out_bits, special_x, shift_inv, g_ctx.stream);
+}
+
+int zkgpu_fri_transpose_dev(uint64_t *aux, const uint64_t *pol, uint64_t degree, uint32_t transpose_bits)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    return fri_transpose(aux, pol, degree, transpose_bits, g_ctx.stream);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- profiling
+#include <string>
+#include <vector>
+
+namespace zk {
+struct ProfRec {
+    std::string name;
+    hipEvent_t start, stop;
+    double bytes;
+};
+static bool g_prof = false;
+static std::vector<ProfRec> g_prof_recs;
+static std::vector<hipEvent_t> g_event_pool;
+static hipEvent_t g_pending_start = nullptr;
+
+static hipEvent_t get_event()
+{
+    if (!g_event_pool.empty()) {
+        hipEvent_t e = g_event_pool.back();
+        g_event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+bool prof_on() { return g_prof; }
+
+void prof_begin(hipStream_t s)
+{
+    if (!g_prof) return;
+    g_pending_start = get_event();
+    (void)hipEventRecord(g_pending_start, s);
+}
+
+void prof_end(const char *kernel, double bytes, hipStream_t s)
+{
+    if (!g_prof || !g_pending_start) return;
+    hipEvent_t stop = get_event();
+    (void)hipEventRecord(stop, s);
+    g_prof_recs.push_back(ProfRec{kernel, g_pending_start, stop, bytes});
+    g_pending_start = nullptr;
+}
+}  // namespace zk
+
+extern "C" {
+int zkgpu_prof_enable(int on)
+{
+    zk::g_prof = on != 0;
+    return 0;
+}
+
+int zkgpu_prof_reset(void)
+{
+    (void)hipStreamSynchronize(zk::g_ctx.stream);
+    for (auto &r : zk::g_prof_recs) {
+        zk::g_event_pool.push_back(r.start);
+        zk::g_event_pool.push_back(r.stop);
+    }
+    zk::g_prof_recs.clear();
+    return 0;
+}
+
+int zkgpu_prof_query(const char *kernel, uint64_t *launches, double *total_ms, double *total_bytes)
+{
+    int rc;
+    if ((rc = zk::check_hip(hipStreamSynchronize(zk::g_ctx.stream), "prof sync"))) return rc;
+    uint64_t n = 0;
+    double ms = 0, bytes = 0;
+    for (auto &r : zk::g_prof_recs) {
+        if (r.name != kernel) continue;
+        float t = 0;
+        if ((rc = zk::check_hip(hipEventSynchronize(r.stop), "prof event"))) return rc;
+        if ((rc = zk::check_hip(hipEventElapsedTime(&t, r.start, r.stop), "prof elapsed"))) return rc;
+        n++;
+        ms += t;
+        bytes += r.bytes;
+    }
+    *launches = n;
+    *total_ms = ms;
+    *total_bytes = bytes;
+    return 0;
+}
+
+int zkgpu_prof_kernels(char *buf, uint64_t buflen)
+{
+    std::vector<std::string> seen;
+    for (auto &r : zk::g_prof_recs) {
+        bool dup = false;
+        for (auto &s : seen) dup |= (s == r.name);
+        if (!dup) seen.push_back(r.name);
+    }
+    std::string out;
+    for (auto &s : seen) out += s + "\n";
+    if (buflen == 0) return 0;
+    size_t n = out.size() < buflen - 1 ? out.size() : buflen - 1;
+    memcpy(buf, out.data(), n);
+    buf[n] = 0;
+    return 0;
+}
+}  // extern "C"

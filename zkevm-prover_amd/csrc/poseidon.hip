@@ -1,0 +1,256 @@
+// Poseidon-GL permutation, linear hash and Merkle tree kernels for gfx950.
+//
+// Replaces PoseidonGoldilocks::{hash_full_result, hash, linear_hash,
+// merkletree_avx} (submodule, absent; call sites merkleTreeGL.cpp:37-44,
+// transcript.cpp:23,46, build_const_tree.cpp:582) and MerkleTreeGL's
+// getGroupProof (merkleTreeGL.cpp:12-35).
+//
+// Permutation: t = 12, 4 + 22 + 4 rounds, S-box x^7, MDS = circ(17,15,41,16,
+// 2,28,13,13,39,18,34,20) + diag(8,0,...) -- the reference's own form at
+// poseidon_g_executor.cpp:201-231 / .hpp:29-51.  Integer VALU-bound: one
+// thread per permutation, the 12-lane state in VGPRs, round constants in
+// constant memory (wave-uniform -> scalar loads), the MDS as 32x32->64
+// multiply-adds on the 32-bit halves of each lane (the MDS entries are < 64).
+//
+// Leaves: one thread per row; a column-major (SoA) source makes each of the
+// ceil(ncols/8) absorption steps a fully coalesced 8-column read.
+#include "gl_device.hpp"
+#include "poseidon_gl_constants.h"
+#include "zkgpu_internal.hpp"
+
+namespace zk {
+
+__constant__ uint64_t c_rc[360];
+
+__device__ __forceinline__ uint64_t pow7(uint64_t x)
+{
+    uint64_t x2 = gl_mul(x, x);
+    uint64_t x3 = gl_mul(x2, x);
+    uint64_t x4 = gl_mul(x2, x2);
+    return gl_mul(x3, x4);
+}
+
+// state' = M * state ; M[x][y] = MCIRC[(y - x) mod 12] + (x == y) * MDIAG[x]
+__device__ __forceinline__ void mds(uint64_t st[12])
+{
+    constexpr uint32_t MC[12] = {17, 15, 41, 16, 2, 28, 13, 13, 39, 18, 34, 20};
+    uint32_t lo[12], hi[12];
+#pragma unroll
+    for (int y = 0; y < 12; y++) {
+        lo[y] = (uint32_t)st[y];
+        hi[y] = (uint32_t)(st[y] >> 32);
+    }
+    uint64_t out[12];
+#pragma unroll
+    for (int x = 0; x < 12; x++) {
+        uint64_t sl = 0, sh = 0;
+#pragma unroll
+        for (int y = 0; y < 12; y++) {
+            uint32_t m = MC[(y - x + 12) % 12] + (x == y && x == 0 ? 8u : 0u);
+            sl += (uint64_t)lo[y] * m;
+            sh += (uint64_t)hi[y] * m;
+        }
+        // value = sl + sh * 2^32  (< 2^75)
+        uint64_t l = sl + (sh << 32);
+        uint64_t c = (l < sl) ? 1ULL : 0ULL;
+        uint64_t h = (sh >> 32) + c;
+        out[x] = gl_reduce128(l, h);
+    }
+#pragma unroll
+    for (int x = 0; x < 12; x++) st[x] = out[x];
+}
+
+__device__ __forceinline__ void full_round(uint64_t st[12], int r)
+{
+#pragma unroll
+    for (int s = 0; s < 12; s++) st[s] = pow7(gl_add(st[s], c_rc[r * 12 + s]));
+    mds(st);
+}
+
+__device__ __forceinline__ void partial_round(uint64_t st[12], int r)
+{
+#pragma unroll
+    for (int s = 0; s < 12; s++) st[s] = gl_add(st[s], c_rc[r * 12 + s]);
+    st[0] = pow7(st[0]);
+    mds(st);
+}
+
+__device__ void poseidon_perm(uint64_t st[12])
+{
+#pragma unroll 1
+    for (int r = 0; r < 4; r++) full_round(st, r);
+#pragma unroll 1
+    for (int r = 4; r < 26; r++) partial_round(st, r);
+#pragma unroll 1
+    for (int r = 26; r < 30; r++) full_round(st, r);
+}
+
+// ---------------------------------------------------------------- kernels
+__global__ void k_poseidon_batch(uint64_t *out, const uint64_t *in, uint64_t n, int full)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t st[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) st[k] = gl_canon(in[i * 12 + k]);
+    poseidon_perm(st);
+    const int w = full ? 12 : 4;
+    for (int k = 0; k < w; k++) out[i * w + k] = st[k];
+}
+
+// leaf digests from a column-major source (column c at src + c*ld)
+__global__ void __launch_bounds__(256) k_leaves_cols(uint64_t *digests, const uint64_t *__restrict__ src,
+                                                    uint64_t ncols, uint64_t nrows, uint64_t ld)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nrows) return;
+    uint64_t st[12];
+    if (ncols <= 4) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) st[k] = (uint64_t)k < ncols ? src[k * ld + i] : 0;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 12; k++) st[k] = 0;
+        for (uint64_t c0 = 0; c0 < ncols; c0 += 8) {
+            uint64_t nk = ncols - c0 < 8 ? ncols - c0 : 8;
+            if (c0) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) st[8 + k] = st[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) st[k] = (uint64_t)k < nk ? gl_canon(src[(c0 + k) * ld + i]) : 0;
+            poseidon_perm(st);
+        }
+    }
+    uint64_t *d = digests + 4 * i;
+#pragma unroll
+    for (int k = 0; k < 4; k++) d[k] = st[k];
+}
+
+// leaf digests from a row-major source (row i at src + i*ncols)
+__global__ void __launch_bounds__(256) k_leaves_rows(uint64_t *digests, const uint64_t *__restrict__ src,
+                                                    uint64_t ncols, uint64_t nrows)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nrows) return;
+    const uint64_t *row = src + i * ncols;
+    uint64_t st[12];
+    if (ncols <= 4) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) st[k] = (uint64_t)k < ncols ? row[k] : 0;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 12; k++) st[k] = 0;
+        for (uint64_t c0 = 0; c0 < ncols; c0 += 8) {
+            uint64_t nk = ncols - c0 < 8 ? ncols - c0 : 8;
+            if (c0) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) st[8 + k] = st[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) st[k] = (uint64_t)k < nk ? gl_canon(row[c0 + k]) : 0;
+            poseidon_perm(st);
+        }
+    }
+    uint64_t *d = digests + 4 * i;
+#pragma unroll
+    for (int k = 0; k < 4; k++) d[k] = st[k];
+}
+
+// one tree level: dst[i] = hash(lvl[2i] || lvl[2i+1] || 0000)
+__global__ void __launch_bounds__(256) k_merkle_level(uint64_t *dst, const uint64_t *lvl, uint64_t next)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= next) return;
+    uint64_t st[12];
+#pragma unroll
+    for (int k = 0; k < 8; k++) st[k] = lvl[8 * i + k];
+#pragma unroll
+    for (int k = 8; k < 12; k++) st[k] = 0;
+    poseidon_perm(st);
+#pragma unroll
+    for (int k = 0; k < 4; k++) dst[4 * i + k] = st[k];
+}
+
+// openings: vals[q*ncols + c] = src[c*ld + idx[q]]; sibs[q][l][0..3]
+__global__ void k_merkle_open(uint64_t *vals, uint64_t *sibs, const uint64_t *nodes, const uint64_t *src,
+                              uint64_t ncols, uint64_t nrows, uint64_t ld, const uint64_t *idx, uint64_t nq,
+                              uint32_t nlevels)
+{
+    uint64_t q = blockIdx.x;
+    if (q >= nq) return;
+    uint64_t row = idx[q];
+    for (uint64_t c = threadIdx.x; c < ncols; c += blockDim.x) vals[q * ncols + c] = src[c * ld + row];
+    if (threadIdx.x == 0) {
+        uint64_t off = 0, pending = nrows, id = row;
+        for (uint32_t l = 0; l < nlevels; l++) {
+            for (int k = 0; k < 4; k++) sibs[(q * nlevels + l) * 4 + k] = nodes[off + 4 * (id ^ 1) + k];
+            off += 4 * pending;
+            pending >>= 1;
+            id >>= 1;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- host side
+static inline uint32_t blocks_for(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
+
+int upload_poseidon_constants(Ctx &c)
+{
+    (void)c;
+    return check_hip(hipMemcpyToSymbol(HIP_SYMBOL(c_rc), ZKGPU_POSEIDON_RC, sizeof(uint64_t) * 360), "poseidon rc");
+}
+
+int poseidon_batch(uint64_t *out, const uint64_t *in, uint64_t n, int full, hipStream_t s)
+{
+    if (!n) return 0;
+    hipLaunchKernelGGL(k_poseidon_batch, dim3(blocks_for(n, 256)), dim3(256), 0, s, out, in, n, full);
+    return check_launch("k_poseidon_batch");
+}
+
+int merkle_leaves_cols(uint64_t *digests, const uint64_t *src, uint64_t ncols, uint64_t nrows, uint64_t ld,
+                       hipStream_t s)
+{
+    if (!nrows) return 0;
+    prof_begin(s);
+    hipLaunchKernelGGL(k_leaves_cols, dim3(blocks_for(nrows, 256)), dim3(256), 0, s, digests, src, ncols, nrows, ld);
+    prof_end("k_leaves_cols", 8.0 * (double)nrows * (double)ncols + 32.0 * (double)nrows, s);
+    return check_launch("k_leaves_cols");
+}
+
+int merkle_leaves_rows(uint64_t *digests, const uint64_t *src, uint64_t ncols, uint64_t nrows, hipStream_t s)
+{
+    if (!nrows) return 0;
+    prof_begin(s);
+    hipLaunchKernelGGL(k_leaves_rows, dim3(blocks_for(nrows, 256)), dim3(256), 0, s, digests, src, ncols, nrows);
+    prof_end("k_leaves_rows", 8.0 * (double)nrows * (double)ncols + 32.0 * (double)nrows, s);
+    return check_launch("k_leaves_rows");
+}
+
+int merkle_levels(uint64_t *nodes, uint64_t nrows, hipStream_t s)
+{
+    uint64_t off = 0, pending = nrows;
+    while (pending > 1) {
+        uint64_t next = pending / 2;
+        prof_begin(s);
+        hipLaunchKernelGGL(k_merkle_level, dim3(blocks_for(next, 256)), dim3(256), 0, s, nodes + off + 4 * pending,
+                           nodes + off, next);
+        prof_end("k_merkle_level", 96.0 * (double)next, s);
+        off += 4 * pending;
+        pending = next;
+    }
+    return check_launch("k_merkle_level");
+}
+
+int merkle_open_cols(uint64_t *vals, uint64_t *sibs, const uint64_t *nodes, const uint64_t *src, uint64_t ncols,
+                     uint64_t nrows, uint64_t ld, const uint64_t *idx, uint64_t nq, hipStream_t s)
+{
+    if (!nq) return 0;
+    uint32_t nlevels = 0;
+    while ((1ULL << nlevels) < nrows) nlevels++;
+    hipLaunchKernelGGL(k_merkle_open, dim3((uint32_t)nq), dim3(64), 0, s, vals, sibs, nodes, src, ncols, nrows, ld,
+                       idx, nq, nlevels);
+    return check_launch("k_merkle_open");
+}
+
+}  // namespace zk

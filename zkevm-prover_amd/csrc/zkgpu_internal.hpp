@@ -1,0 +1,81 @@
+// Internal state of libzkgpu (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/zkgpu.h"
+
+namespace zk {
+
+constexpr uint32_t NTT_MAX_PASSES = 4;  // log2 n <= 32 at radix <= 2^8
+constexpr uint32_t TW_MAX_LOG = 28;     // big-twiddle base omega_{2^28}
+constexpr uint32_t TW_LEVEL_BITS = 14;
+constexpr uint64_t TW_LEVEL_SIZE = 1ULL << TW_LEVEL_BITS;
+constexpr uint32_t POST_BITS = 12;  // LDE shift-power tables: lo 4096 entries
+
+struct Workspace {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+
+struct Ctx {
+    int device = -1;
+    bool ready = false;
+    hipStream_t stream = nullptr;  // launches go here (zkgpu_set_stream)
+    // direction 0 = forward, 1 = inverse
+    uint64_t *rt_small[2] = {nullptr, nullptr};  // omega_4096^k, k < 2048
+    uint64_t *tw_lo[2] = {nullptr, nullptr};     // omega_{2^28}^i, i < 2^14
+    uint64_t *tw_hi[2] = {nullptr, nullptr};     // omega_{2^28}^(2^14 i)
+    // LDE post-scale tables (1/n * 7^k), cached per log n
+    uint32_t post_logn = 0;
+    uint64_t *post_lo = nullptr;
+    uint64_t *post_hi = nullptr;
+    // scratch workspaces
+    Workspace ws[4];
+    // Poseidon constants on device
+    uint64_t *poseidon_rc = nullptr;
+};
+
+Ctx &ctx();
+int set_error(int code, const char *fmt, ...);
+int check_launch(const char *what);
+int check_hip(hipError_t e, const char *what);
+// grow-only scratch buffer i
+uint64_t *workspace(int i, size_t bytes);
+
+// host-side scalar Goldilocks (setup values only; all bulk math is on the GPU)
+uint64_t h_mul(uint64_t a, uint64_t b);
+uint64_t h_pow(uint64_t a, uint64_t e);
+uint64_t h_inv(uint64_t a);
+uint64_t h_w(uint32_t n);
+
+// ---- live kernel profiling (HIP events on the launch stream; zkgpu_prof_*)
+// prof_begin/prof_end bracket one kernel launch; bytes = algorithmic bytes
+// (each input element read once + each output element written once).
+bool prof_on();
+void prof_begin(hipStream_t s);
+void prof_end(const char *kernel, double bytes, hipStream_t s);
+
+// ---- ntt.hip
+int ntt_columns(Ctx &c, uint64_t *dst, uint64_t dst_ld, const uint64_t *src, uint64_t src_ld, uint64_t src_valid,
+                uint64_t *tmp, uint64_t tmp_ld, uint32_t logn, uint64_t ncols, int inverse, const uint64_t *post_lo,
+                const uint64_t *post_hi, uint32_t post_bits, uint64_t post_scale, hipStream_t s);
+void rows_to_cols(const uint64_t *in, uint64_t *out, uint64_t nrows, uint64_t ncols, uint64_t ld, hipStream_t s);
+void cols_to_rows(const uint64_t *in, uint64_t *out, uint64_t nrows, uint64_t ncols, uint64_t ld, hipStream_t s);
+void fill_powers(uint64_t *out, uint64_t base, uint64_t step, uint64_t scale, uint64_t count, hipStream_t s);
+
+// ---- poseidon.hip
+int poseidon_batch(uint64_t *out, const uint64_t *in, uint64_t n, int full, hipStream_t s);
+int merkle_leaves_cols(uint64_t *digests, const uint64_t *src, uint64_t ncols, uint64_t nrows, uint64_t ld,
+                       hipStream_t s);
+int merkle_leaves_rows(uint64_t *digests, const uint64_t *src, uint64_t ncols, uint64_t nrows, hipStream_t s);
+int merkle_levels(uint64_t *nodes, uint64_t nrows, hipStream_t s);
+int merkle_open_cols(uint64_t *vals, uint64_t *sibs, const uint64_t *nodes, const uint64_t *src, uint64_t ncols,
+                     uint64_t nrows, uint64_t ld, const uint64_t *idx, uint64_t nq, hipStream_t s);
+
+// ---- fri.hip
+int fri_fold(uint64_t *out, const uint64_t *pol, uint32_t pol_bits, uint32_t out_bits, const uint64_t sx[3],
+             uint64_t shift_inv, hipStream_t s);
+int fri_transpose(uint64_t *aux, const uint64_t *pol, uint64_t degree, uint32_t tbits, hipStream_t s);
+
+}  // namespace zk

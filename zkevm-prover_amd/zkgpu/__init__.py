@@ -1,0 +1,276 @@
+"""zkgpu -- Python binding of libzkgpu (the MI355X HIP STARK hot path).
+
+Thin ctypes layer over the C-ABI declared in include/zkgpu.h.  Host-pointer
+calls take numpy uint64 arrays (row-major, like the reference); *_dev calls
+take device addresses (ints) or torch tensors (int64/uint64 storage,
+column-major: column c at base + c*ld elements).
+
+There is no CPU fallback: if lib/libzkgpu.so is missing or no GPU is
+present, calls raise ZkgpuError.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libzkgpu.so")
+HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "zkgpu.h")
+
+P = 0xFFFFFFFF00000001
+
+
+class ZkgpuError(RuntimeError):
+    pass
+
+
+_lib = None
+
+u64 = ctypes.c_uint64
+u32 = ctypes.c_uint32
+vp = ctypes.c_void_p
+pu64 = ctypes.POINTER(ctypes.c_uint64)
+
+_SIGS = {
+    "zkgpu_init": (ctypes.c_int, [ctypes.c_int]),
+    "zkgpu_release": (None, []),
+    "zkgpu_last_error": (ctypes.c_char_p, []),
+    "zkgpu_set_stream": (ctypes.c_int, [vp]),
+    "zkgpu_synchronize": (ctypes.c_int, []),
+    "zkgpu_abi_version": (ctypes.c_int, []),
+    "zkgpu_gl_ntt": (ctypes.c_int, [vp, vp, u64, u64, ctypes.c_int]),
+    "zkgpu_gl_extend_pol": (ctypes.c_int, [vp, vp, u64, u64, u64]),
+    "zkgpu_gl_ntt_dev": (ctypes.c_int, [vp, u64, vp, u64, u64, u64, ctypes.c_int]),
+    "zkgpu_gl_extend_pol_dev": (ctypes.c_int, [vp, u64, vp, u64, u64, u64, u64]),
+    "zkgpu_rows_to_cols_dev": (ctypes.c_int, [vp, u64, vp, u64, u64]),
+    "zkgpu_cols_to_rows_dev": (ctypes.c_int, [vp, vp, u64, u64, u64]),
+    "zkgpu_gl_poseidon_full": (ctypes.c_int, [vp, vp]),
+    "zkgpu_gl_poseidon_hash": (ctypes.c_int, [vp, vp]),
+    "zkgpu_gl_linear_hash": (ctypes.c_int, [vp, vp, u64]),
+    "zkgpu_gl_poseidon_batch_dev": (ctypes.c_int, [vp, vp, u64, ctypes.c_int]),
+    "zkgpu_gl_merkle_num_elements": (u64, [u64]),
+    "zkgpu_gl_merkletree": (ctypes.c_int, [vp, vp, u64, u64]),
+    "zkgpu_gl_merkletree_dev": (ctypes.c_int, [vp, vp, u64, u64, u64]),
+    "zkgpu_gl_merkletree_rows_dev": (ctypes.c_int, [vp, vp, u64, u64]),
+    "zkgpu_gl_merkle_open_dev": (ctypes.c_int, [vp, vp, vp, vp, u64, u64, u64, vp, u64]),
+    "zkgpu_fri_fold_dev": (ctypes.c_int, [vp, vp, u32, u32, vp, u64]),
+    "zkgpu_fri_transpose_dev": (ctypes.c_int, [vp, vp, u64, u32]),
+    "zkgpu_prof_enable": (ctypes.c_int, [ctypes.c_int]),
+    "zkgpu_prof_reset": (ctypes.c_int, []),
+    "zkgpu_prof_query": (ctypes.c_int, [ctypes.c_char_p, pu64, ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_double)]),
+    "zkgpu_prof_kernels": (ctypes.c_int, [ctypes.c_char_p, u64]),
+}
+
+
+def build():
+    """Compile libzkgpu for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    subprocess.check_call(["make", "-s", "-C", PKG_ROOT, "-j8"])
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ZkgpuError("libzkgpu.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def _check(rc, what):
+    if rc != 0:
+        msg = lib().zkgpu_last_error().decode(errors="replace")
+        raise ZkgpuError("%s failed (%d): %s" % (what, rc, msg))
+
+
+def init(device=0):
+    _check(lib().zkgpu_init(device), "zkgpu_init")
+
+
+def release():
+    lib().zkgpu_release()
+
+
+def set_stream(stream):
+    """stream: a torch.cuda.Stream, an int handle, or None (null stream)."""
+    h = 0
+    if stream is not None:
+        h = getattr(stream, "cuda_stream", stream)
+    _check(lib().zkgpu_set_stream(h or None), "zkgpu_set_stream")
+
+
+def synchronize():
+    _check(lib().zkgpu_synchronize(), "zkgpu_synchronize")
+
+
+def _np(a):
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    return a
+
+
+def _addr(x):
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    raise TypeError(type(x))
+
+
+# ---------------------------------------------------------------- host-pointer
+def ntt(x, inverse=False):
+    x = _np(x)
+    n = x.shape[0]
+    ncols = 1 if x.ndim == 1 else x.shape[1]
+    out = np.empty_like(x)
+    _check(lib().zkgpu_gl_ntt(out.ctypes.data, x.ctypes.data, n, ncols, int(inverse)), "zkgpu_gl_ntt")
+    return out
+
+
+def extend_pol(x, n_ext):
+    x = _np(x)
+    n = x.shape[0]
+    ncols = 1 if x.ndim == 1 else x.shape[1]
+    out = np.empty((n_ext,) if x.ndim == 1 else (n_ext, ncols), np.uint64)
+    _check(lib().zkgpu_gl_extend_pol(out.ctypes.data, x.ctypes.data, n_ext, n, ncols), "zkgpu_gl_extend_pol")
+    return out
+
+
+def poseidon_full(x):
+    x = _np(x)
+    out = np.zeros(12, np.uint64)
+    _check(lib().zkgpu_gl_poseidon_full(out.ctypes.data, x.ctypes.data), "zkgpu_gl_poseidon_full")
+    return out
+
+
+def poseidon_hash(x):
+    x = _np(x)
+    out = np.zeros(4, np.uint64)
+    _check(lib().zkgpu_gl_poseidon_hash(out.ctypes.data, x.ctypes.data), "zkgpu_gl_poseidon_hash")
+    return out
+
+
+def linear_hash(x):
+    x = _np(x).reshape(-1)
+    out = np.zeros(4, np.uint64)
+    buf = x if x.size else np.zeros(1, np.uint64)
+    _check(lib().zkgpu_gl_linear_hash(out.ctypes.data, buf.ctypes.data, x.size), "zkgpu_gl_linear_hash")
+    return out
+
+
+def merkle_num_elements(nrows):
+    return lib().zkgpu_gl_merkle_num_elements(nrows)
+
+
+def merkletree(src):
+    src = _np(src)
+    nrows = src.shape[0]
+    ncols = src.shape[1] if src.ndim == 2 else 1
+    nodes = np.zeros(merkle_num_elements(nrows), np.uint64)
+    buf = src if src.size else np.zeros(1, np.uint64)
+    _check(lib().zkgpu_gl_merkletree(nodes.ctypes.data, buf.ctypes.data, ncols, nrows), "zkgpu_gl_merkletree")
+    return nodes
+
+
+# ---------------------------------------------------------------- device
+def ntt_dev(dst, ld_dst, src, ld_src, n, ncols, inverse=False):
+    _check(lib().zkgpu_gl_ntt_dev(_addr(dst), ld_dst, _addr(src), ld_src, n, ncols, int(inverse)), "zkgpu_gl_ntt_dev")
+
+
+def extend_pol_dev(out, ld_out, src, ld_in, n_ext, n, ncols):
+    _check(lib().zkgpu_gl_extend_pol_dev(_addr(out), ld_out, _addr(src), ld_in, n_ext, n, ncols),
+           "zkgpu_gl_extend_pol_dev")
+
+
+def rows_to_cols_dev(cols, ld, rows, nrows, ncols):
+    _check(lib().zkgpu_rows_to_cols_dev(_addr(cols), ld, _addr(rows), nrows, ncols), "zkgpu_rows_to_cols_dev")
+
+
+def cols_to_rows_dev(rows, cols, ld, nrows, ncols):
+    _check(lib().zkgpu_cols_to_rows_dev(_addr(rows), _addr(cols), ld, nrows, ncols), "zkgpu_cols_to_rows_dev")
+
+
+def poseidon_batch_dev(out, src, n, full=True):
+    _check(lib().zkgpu_gl_poseidon_batch_dev(_addr(out), _addr(src), n, int(full)), "zkgpu_gl_poseidon_batch_dev")
+
+
+def merkletree_dev(nodes, src, ld, ncols, nrows):
+    _check(lib().zkgpu_gl_merkletree_dev(_addr(nodes), _addr(src), ld, ncols, nrows), "zkgpu_gl_merkletree_dev")
+
+
+def merkletree_rows_dev(nodes, src, ncols, nrows):
+    _check(lib().zkgpu_gl_merkletree_rows_dev(_addr(nodes), _addr(src), ncols, nrows),
+           "zkgpu_gl_merkletree_rows_dev")
+
+
+def merkle_open_dev(nodes, src, ld, ncols, nrows, idx):
+    idx = _np(idx).reshape(-1)
+    nq = idx.size
+    nlev = max(0, int(nrows).bit_length() - 1)
+    vals = np.zeros((nq, ncols), np.uint64)
+    sibs = np.zeros((nq, nlev, 4), np.uint64)
+    _check(lib().zkgpu_gl_merkle_open_dev(vals.ctypes.data, sibs.ctypes.data, _addr(nodes), _addr(src), ld, ncols,
+                                          nrows, idx.ctypes.data, nq), "zkgpu_gl_merkle_open_dev")
+    return vals, sibs
+
+
+def fri_fold_dev(out, pol, pol_bits, out_bits, special_x, shift_inv):
+    sx = _np(special_x)
+    _check(lib().zkgpu_fri_fold_dev(_addr(out), _addr(pol), pol_bits, out_bits, sx.ctypes.data, shift_inv),
+           "zkgpu_fri_fold_dev")
+
+
+def fri_transpose_dev(aux, pol, degree, transpose_bits):
+    _check(lib().zkgpu_fri_transpose_dev(_addr(aux), _addr(pol), degree, transpose_bits), "zkgpu_fri_transpose_dev")
+
+
+# ---------------------------------------------------------------- profiling
+def prof_enable(on=True):
+    _check(lib().zkgpu_prof_enable(int(on)), "zkgpu_prof_enable")
+
+
+def prof_reset():
+    _check(lib().zkgpu_prof_reset(), "zkgpu_prof_reset")
+
+
+def prof_query(kernel):
+    """-> (launches, total_ms, total_algorithmic_bytes) since the last reset."""
+    n = ctypes.c_uint64(0)
+    ms = ctypes.c_double(0)
+    by = ctypes.c_double(0)
+    _check(lib().zkgpu_prof_query(kernel.encode(), ctypes.byref(n), ctypes.byref(ms), ctypes.byref(by)),
+           "zkgpu_prof_query")
+    return n.value, ms.value, by.value
+
+
+def prof_kernels():
+    buf = ctypes.create_string_buffer(4096)
+    _check(lib().zkgpu_prof_kernels(buf, len(buf)), "zkgpu_prof_kernels")
+    return [k for k in buf.value.decode().split("\n") if k]
+
+
+# ---------------------------------------------------------------- torch helpers
+def to_device(a, device="cuda:0"):
+    """numpy uint64 -> torch int64 tensor on the GPU (bit-identical storage)."""
+    import torch
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    return torch.from_numpy(a.view(np.int64)).to(device)
+
+
+def from_device(t):
+    return t.detach().cpu().numpy().view(np.uint64)
