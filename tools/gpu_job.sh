@@ -39,6 +39,13 @@ for step in "$@"; do
         ok_or_stop $? "bench"
         cat gpurun_out/bench.json
         ;;
+    sweep)
+        for b in 1 2 4 10 100; do
+            ZKGPU_LDE_BATCH_COLS=$b timeout -k 10 300 python bench.py --no-cpu > gpurun_out/sweep_b$b.json 2>> gpurun_out/sweep.err
+            ok_or_stop $? "bench batch=$b"
+            echo "batch=$b $(python -c "import json;d=json.load(open('gpurun_out/sweep_b$b.json'));print(d['ms_per_step'],'ms',d['value'],'Gelem/s',d['kernels'])")"
+        done
+        ;;
     prof)
         cd /tmp
         timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run \

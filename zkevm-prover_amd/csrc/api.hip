@@ -144,11 +144,11 @@ static int extend_pol_dev(uint64_t *out, uint64_t ld_out, const uint64_t *in, ui
         uint64_t nc = ncols - c0 < batch ? ncols - c0 : batch;
         // coefficients * 7^k / n
         if ((rc = ntt_columns(c, coef, n, in + c0 * ld_in, ld_in, n, tmp, n, logn, nc, 1, c.post_lo, c.post_hi,
-                              post_bits, 1, c.stream)))
+                              post_bits, 7, 1, c.stream)))
             return rc;
         // evaluations on the extended domain (zero padding = predicated loads)
         if ((rc = ntt_columns(c, out + c0 * ld_out, ld_out, coef, n, n, tmp, n_ext, loge, nc, 0, nullptr, nullptr, 0,
-                              1, c.stream)))
+                              1, 1, c.stream)))
             return rc;
     }
     return 0;
@@ -168,7 +168,7 @@ static int ntt_dev(uint64_t *dst, uint64_t ld_dst, const uint64_t *src, uint64_t
         if (!tmp) return ZKGPU_ERR_OOM;
     }
     uint64_t scale = inverse ? h_inv(n) : 1;
-    return ntt_columns(c, dst, ld_dst, src, ld_src, n, tmp, n, logn, ncols, inverse, nullptr, nullptr, 0, scale,
+    return ntt_columns(c, dst, ld_dst, src, ld_src, n, tmp, n, logn, ncols, inverse, nullptr, nullptr, 0, 1, scale,
                        c.stream);
 }
 

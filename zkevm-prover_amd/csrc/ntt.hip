@@ -17,6 +17,8 @@
 //   Zero padding (LDE) is a predicated load in the first NTT pass; the
 //   1/n * shift^k factor of the LDE is fused into the last INTT pass.
 //   n <= 4096 uses a single-workgroup-per-column LDS kernel.
+#include <utility>
+
 #include "gl_device.hpp"
 #include "zkgpu_internal.hpp"
 
@@ -50,104 +52,168 @@ struct PassArgs {
     uint64_t src_valid;  // rows >= src_valid are zero (LDE padding)
     uint64_t *dst;
     uint64_t dst_ld;
-    const uint64_t *rt_small;  // omega_4096^k, k < 2048, for this direction
-    const uint64_t *tw_lo;     // big twiddles, this direction
+    const uint64_t *tw_lo;  // big twiddles omega_{2^28}, this direction
     const uint64_t *tw_hi;
-    const uint64_t *post_lo;  // post-scale (last pass), may be null
+    const uint64_t *post_lo;  // post-scale tables (last pass), may be null
     const uint64_t *post_hi;
+    uint64_t post_step;   // post factor ratio between consecutive k2 (last pass)
     uint64_t post_scale;  // applied when post_lo == null and != 1
     uint32_t post_bits;
     uint32_t logn;
-    uint32_t logm;      // block size before this pass (first pass: logn)
-    uint32_t last;      // 1 = last pass (digit-reversed scatter)
+    uint32_t logm;  // block size before this pass (first pass: logn)
+    uint32_t last;  // 1 = last pass (digit-reversed scatter)
     uint32_t npass;
     uint32_t rbits[NTT_MAX_PASSES];
-    uint32_t pass_idx;  // index of this pass
 };
 
-constexpr int PASS_THREADS = 256;
 constexpr int GROUPS = 16;
 
-// DIF radix-2 over LDS: 16 groups x R elements, element (j, g) at lds[j*16+g].
-template <int LOGR>
-__device__ __forceinline__ void dif_lds(uint64_t *lds, const uint64_t *tw)
+// x * 2^E mod p for a compile-time E in [0, 192) (2^96 = -1 mod p): the
+// twiddles of every DFT of size <= 64 are such powers (omega_R = 2^(192/R)).
+template <int E>
+__device__ __forceinline__ uint64_t mul2e(uint64_t x)
 {
-    constexpr int R = 1 << LOGR;
-    constexpr int NB = GROUPS * R / 2;
-#pragma unroll
-    for (int lh = LOGR - 1; lh >= 0; lh--) {
-        const int h = 1 << lh;
-        __syncthreads();
-        for (int bi = threadIdx.x; bi < NB; bi += PASS_THREADS) {
-            int g = bi & 15;
-            int b = bi >> 4;
-            int pos = b & (h - 1);
-            int i0 = ((b >> lh) << (lh + 1)) + pos;
-            int i1 = i0 + h;
-            uint64_t a = lds[i0 * 16 + g];
-            uint64_t c = lds[i1 * 16 + g];
-            lds[i0 * 16 + g] = gl_add(a, c);
-            uint64_t d = gl_sub(a, c);
-            lds[i1 * 16 + g] = (pos == 0) ? d : gl_mul(d, tw[pos << (LOGR - 1 - lh)]);
-        }
+    if constexpr (E == 0) {
+        return x;
+    } else if constexpr (E >= 96) {
+        return gl_neg(mul2e<E - 96>(x));
+    } else if constexpr (E < 64) {
+        return gl_reduce128(x << E, x >> (64 - E));
+    } else {
+        return mul2e<E - 48>(mul2e<48>(x));
     }
-    __syncthreads();
 }
 
-template <int LOGR>
-__global__ void __launch_bounds__(PASS_THREADS) k_ntt_pass(PassArgs a)
+// radix-2 DIF network on R = 2^LOG registers; afterwards v[r] = X[bitrev(r)].
+// twiddle omega_{2h}^i = 2^(96 i / h) (forward), 2^(192 - 96 i / h) (inverse).
+template <int LOG, bool INV, int H, int I>
+__device__ __forceinline__ uint64_t dif_tw(uint64_t d)
 {
-    constexpr int R = 1 << LOGR;
-    __shared__ uint64_t lds[GROUPS * R];
-    __shared__ uint64_t tw[R / 2];
+    constexpr int e = (96 * I) / H;
+    if constexpr (e == 0) return d;
+    else return mul2e<INV ? (192 - e) % 192 : e>(d);
+}
+
+template <int LOG, bool INV, int H = (1 << LOG) / 2>
+__device__ __forceinline__ void dft_regs(uint64_t *v)
+{
+    if constexpr (H >= 1) {
+        constexpr int R = 1 << LOG;
+        [&]<int... Bs>(std::integer_sequence<int, Bs...>) {
+            (
+                [&]<int B>() {
+                    [&]<int... Is>(std::integer_sequence<int, Is...>) {
+                        (
+                            [&]<int I>() {
+                                uint64_t a = v[B * 2 * H + I];
+                                uint64_t c = v[B * 2 * H + I + H];
+                                v[B * 2 * H + I] = gl_add(a, c);
+                                v[B * 2 * H + I + H] = dif_tw<LOG, INV, H, I>(gl_sub(a, c));
+                            }.template operator()<Is>(),
+                            ...);
+                    }(std::make_integer_sequence<int, H>{});
+                }.template operator()<Bs>(),
+                ...);
+        }(std::make_integer_sequence<int, R / (2 * H)>{});
+        dft_regs<LOG, INV, H / 2>(v);
+    }
+}
+
+__host__ __device__ constexpr int brev_c(int x, int bits)
+{
+    int r = 0;
+    for (int i = 0; i < bits; i++) r |= ((x >> i) & 1) << (bits - 1 - i);
+    return r;
+}
+
+// One pass of radix R = 2^(L1+L2) over 16 independent sub-DFTs per workgroup.
+//   step 1: thread (g, j2) loads x[R2*j1 + j2] (j1 < R1), R1-point DFT in
+//           registers, times omega_R^(j2*k1), to LDS
+//   step 2: thread (g, k1) reads y[j2][k1] (j2 < R2), R2-point DFT in
+//           registers -> X[k1 + R1*k2], outer twiddle / post-scale, store.
+// LDS image (k1*R2 + j2)*17 + g: conflict-free for both access patterns.
+template <int L1, int L2, bool INV>
+__global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
+{
+    constexpr int R1 = 1 << L1, R2 = 1 << L2, LOGR = L1 + L2, R = 1 << LOGR;
+    constexpr int T = GROUPS * R2;
+    __shared__ uint64_t lds[R * 17];
+    __shared__ uint64_t twR[R];  // omega_R^i
     const uint32_t col = blockIdx.y;
     const uint64_t *src = a.src + (uint64_t)col * a.src_ld;
     uint64_t *dst = a.dst + (uint64_t)col * a.dst_ld;
     const int tid = threadIdx.x;
-
-    for (int k = tid; k < R / 2; k += PASS_THREADS) tw[k] = a.rt_small[k << (12 - LOGR)];
-
     const uint64_t u = blockIdx.x;
+
+    // omega_R^i = omega_{2^28}^(i << (28 - LOGR))
+    for (int i = tid; i < R; i += T) twR[i] = tw_big(a.tw_lo, a.tw_hi, (uint64_t)i << (TW_MAX_LOG - LOGR));
+
+    uint64_t v[R2 > R1 ? R2 : R1];
+    // ------------------------------------------------ step 1 (load + R1-DFT)
+    int g, j2;
+    uint64_t base = 0, k1g = 0, rest = 0;
+    uint32_t logmp = 0, logS = 0;
     if (!a.last) {
-        // ---- first / middle pass: in-place layout
-        const uint32_t logmp = a.logm - LOGR;  // log2 m'
-        const uint64_t mp = 1ULL << logmp;
-        const uint64_t groups_per_blk = mp >> 4;
-        const uint64_t blk = u / groups_per_blk;
-        const uint64_t j0 = (u % groups_per_blk) << 4;
-        const uint64_t base = (blk << a.logm) + j0;
-        const int g = tid & 15;
+        g = tid & 15;
+        j2 = tid >> 4;
+        logmp = a.logm - LOGR;
+        const uint64_t groups_per_blk = 1ULL << (logmp - 4);
+        const uint64_t blk = u >> (logmp - 4);
+        const uint64_t j0 = (u & (groups_per_blk - 1)) << 4;
+        base = (blk << a.logm) + j0;
 #pragma unroll
-        for (int it = 0; it < R / 16; it++) {
-            int j = (tid >> 4) + 16 * it;
-            uint64_t pos = base + ((uint64_t)j << logmp) + g;
-            uint64_t v = pos < a.src_valid ? gl_canon(src[pos]) : 0;
-            lds[j * 16 + g] = v;
-        }
-        dif_lds<LOGR>(lds, tw);
-        const uint32_t tshift = TW_MAX_LOG - a.logm;
-        const uint64_t jp = j0 + g;
-#pragma unroll
-        for (int it = 0; it < R / 16; it++) {
-            int k = (tid >> 4) + 16 * it;
-            uint64_t v = lds[bitrev_u32(k, LOGR) * 16 + g];
-            uint64_t e = (jp * (uint64_t)k) << tshift;
-            if (e) v = gl_mul(v, tw_big(a.tw_lo, a.tw_hi, e));
-            dst[base + ((uint64_t)k << logmp) + g] = v;
+        for (int j1 = 0; j1 < R1; j1++) {
+            uint64_t pos = base + ((uint64_t)(R2 * j1 + j2) << logmp) + g;
+            v[j1] = pos < a.src_valid ? gl_canon(src[pos]) : 0;
         }
     } else {
-        // ---- last pass: 16 blocks with consecutive leading digit k_1
-        // blk = k_1 * S + rest, S = n / (r_1 * R)
-        const uint32_t r1b = a.rbits[0];
-        const uint32_t logS = a.logn - r1b - LOGR;
-        const uint64_t S = 1ULL << logS;
-        const uint64_t rest = u & (S - 1);
-        const uint64_t k1g = u >> logS;
-        // reversed digits of rest (radices rbits[1..npass-2])
+        j2 = tid & (R2 - 1);
+        g = tid >> L2;
+        logS = a.logn - a.rbits[0] - LOGR;
+        rest = u & ((1ULL << logS) - 1);
+        k1g = u >> logS;
+        const uint64_t blk = ((k1g * 16 + g) << logS) + rest;
+#pragma unroll
+        for (int j1 = 0; j1 < R1; j1++) {
+            uint64_t pos = (blk << LOGR) + R2 * j1 + j2;
+            v[j1] = pos < a.src_valid ? gl_canon(src[pos]) : 0;
+        }
+    }
+    dft_regs<L1, INV>(v);
+    __syncthreads();  // twR ready
+#pragma unroll
+    for (int r = 0; r < R1; r++) {
+        const int k1 = brev_c(r, L1);
+        uint64_t y = v[r];
+        if (k1) y = gl_mul(y, twR[(j2 * k1) & (R - 1)]);
+        lds[(k1 * R2 + j2) * 17 + g] = y;
+    }
+    __syncthreads();
+    // ------------------------------------------------ step 2 (R2-DFT + store)
+    if (tid >= GROUPS * R1) return;
+    g = tid & 15;
+    const int k1 = tid >> 4;
+#pragma unroll
+    for (int jj = 0; jj < R2; jj++) v[jj] = lds[(k1 * R2 + jj) * 17 + g];
+    dft_regs<L2, INV>(v);
+    if (!a.last) {
+        // X[k] * omega_m^(j' k), k = k1 + R1*k2, j' = j0 + g
+        const uint32_t tshift = TW_MAX_LOG - a.logm;
+        const uint64_t jp = (base & ((1ULL << logmp) - 1)) + g;
+        uint64_t t = tw_big(a.tw_lo, a.tw_hi, (jp * k1) << tshift);
+        const uint64_t step = tw_big(a.tw_lo, a.tw_hi, (jp * R1) << tshift);
+#pragma unroll
+        for (int k2 = 0; k2 < R2; k2++) {
+            const int r = brev_c(k2, L2);
+            uint64_t x = v[r];
+            if (k1 | k2) x = gl_mul(x, t);
+            dst[base + ((uint64_t)(k1 + R1 * k2) << logmp) + g] = x;
+            t = gl_mul(t, step);
+        }
+    } else {
         uint64_t rrev = 0;
         {
-            // rest = sum_{i=1..npass-2} k_i * prod_{l>i} r_l (k_1 of rest most significant);
-            // rrev = sum_i k_i * prod_{1<=l<i} r_l  (mixed-radix digit reversal)
+            // rest = sum_{i=1..npass-2} k_i * prod_{l>i} r_l; rrev = mixed-radix reversal
             uint32_t rev_pos[NTT_MAX_PASSES];
             uint32_t acc = 0;
             for (uint32_t i = 1; i + 1 < a.npass; i++) {
@@ -161,37 +227,28 @@ __global__ void __launch_bounds__(PASS_THREADS) k_ntt_pass(PassArgs a)
                 rrev |= d << rev_pos[i];
             }
         }
-        // load 16 blocks x R contiguous elements
-        for (int e = tid; e < GROUPS * R; e += PASS_THREADS) {
-            int g = e >> LOGR;
-            int t = e & (R - 1);
-            uint64_t blk = ((k1g * 16 + g) << logS) + rest;
-            uint64_t pos = (blk << LOGR) + t;
-            uint64_t v = pos < a.src_valid ? gl_canon(src[pos]) : 0;
-            lds[t * 16 + g] = v;
-        }
-        dif_lds<LOGR>(lds, tw);
-        const int g = tid & 15;
-        const uint64_t xbase = (k1g * 16 + g) + (rrev << r1b);
         const uint32_t lognr = a.logn - LOGR;
+        const uint64_t x0 = (k1g * 16 + g) + (rrev << a.rbits[0]) + ((uint64_t)k1 << lognr);
+        uint64_t f = 1;
+        if (a.post_lo)
+            f = gl_mul(a.post_lo[x0 & ((1ULL << a.post_bits) - 1)], a.post_hi[x0 >> a.post_bits]);
+        else
+            f = a.post_scale;
 #pragma unroll
-        for (int it = 0; it < R / 16; it++) {
-            int k = (tid >> 4) + 16 * it;
-            uint64_t v = lds[bitrev_u32(k, LOGR) * 16 + g];
-            uint64_t x = xbase + ((uint64_t)k << lognr);
-            if (a.post_lo) {
-                uint64_t f = gl_mul(a.post_lo[x & ((1ULL << a.post_bits) - 1)], a.post_hi[x >> a.post_bits]);
-                v = gl_mul(v, f);
-            } else if (a.post_scale != 1) {
-                v = gl_mul(v, a.post_scale);
-            }
-            dst[x] = v;
+        for (int k2 = 0; k2 < R2; k2++) {
+            const int r = brev_c(k2, L2);
+            uint64_t x = v[r];
+            if (f != 1) x = gl_mul(x, f);
+            dst[x0 + ((uint64_t)(R1 * k2) << lognr)] = x;
+            if (a.post_lo) f = gl_mul(f, a.post_step);
         }
     }
 }
 
 // ---------------------------------------------------------------- small NTT
 // one workgroup per column, whole column (n <= 4096) in LDS
+constexpr int PASS_THREADS = 256;
+
 struct SmallArgs {
     const uint64_t *src;
     uint64_t src_ld;
@@ -288,22 +345,26 @@ static void split_radix(uint32_t logn, uint32_t *npass, uint32_t rbits[NTT_MAX_P
     for (uint32_t i = 0; i < P; i++) rbits[i] = base + (i >= P - extra ? 1 : 0);
 }
 
-template <int LOGR>
-static void launch_pass(const PassArgs &a, uint64_t ncols, hipStream_t s)
+template <int L1, int L2>
+static void launch_pass(const PassArgs &a, uint64_t ncols, int inverse, hipStream_t s)
 {
+    constexpr int LOGR = L1 + L2;
     uint64_t units = (1ULL << (a.logn - LOGR)) / 16;
     dim3 grid((uint32_t)units, (uint32_t)ncols);
-    hipLaunchKernelGGL(k_ntt_pass<LOGR>, grid, dim3(PASS_THREADS), 0, s, a);
+    if (inverse)
+        hipLaunchKernelGGL((k_ntt_pass<L1, L2, true>), grid, dim3(16 << L2), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_ntt_pass<L1, L2, false>), grid, dim3(16 << L2), 0, s, a);
 }
 
-static void dispatch_pass(uint32_t logr, const PassArgs &a, uint64_t ncols, hipStream_t s)
+static void dispatch_pass(uint32_t logr, const PassArgs &a, uint64_t ncols, int inverse, hipStream_t s)
 {
     switch (logr) {
-    case 4: launch_pass<4>(a, ncols, s); break;
-    case 5: launch_pass<5>(a, ncols, s); break;
-    case 6: launch_pass<6>(a, ncols, s); break;
-    case 7: launch_pass<7>(a, ncols, s); break;
-    case 8: launch_pass<8>(a, ncols, s); break;
+    case 4: launch_pass<2, 2>(a, ncols, inverse, s); break;
+    case 5: launch_pass<2, 3>(a, ncols, inverse, s); break;
+    case 6: launch_pass<3, 3>(a, ncols, inverse, s); break;
+    case 7: launch_pass<3, 4>(a, ncols, inverse, s); break;
+    case 8: launch_pass<4, 4>(a, ncols, inverse, s); break;
     default: break;
     }
 }
@@ -315,7 +376,7 @@ static void dispatch_pass(uint32_t logr, const PassArgs &a, uint64_t ncols, hipS
 //   post: optional per-row factor tables (last pass)
 int ntt_columns(Ctx &ctx, uint64_t *dst, uint64_t dst_ld, const uint64_t *src, uint64_t src_ld, uint64_t src_valid,
                 uint64_t *tmp, uint64_t tmp_ld, uint32_t logn, uint64_t ncols, int inverse, const uint64_t *post_lo,
-                const uint64_t *post_hi, uint32_t post_bits, uint64_t post_scale, hipStream_t s)
+                const uint64_t *post_hi, uint32_t post_bits, uint64_t post_base, uint64_t post_scale, hipStream_t s)
 {
     if (ncols == 0) return 0;
     if (logn > TW_MAX_LOG) return set_error(ZKGPU_ERR_ARG, "ntt: log2(n) exceeds %u", TW_MAX_LOG);
@@ -347,20 +408,21 @@ int ntt_columns(Ctx &ctx, uint64_t *dst, uint64_t dst_ld, const uint64_t *src, u
         return check_launch("k_ntt_small");
     }
     PassArgs a;
-    a.rt_small = ctx.rt_small[d];
     a.tw_lo = ctx.tw_lo[d];
     a.tw_hi = ctx.tw_hi[d];
     a.logn = logn;
     split_radix(logn, &a.npass, a.rbits);
     uint32_t logm = logn;
     for (uint32_t p = 0; p < a.npass; p++) {
-        a.pass_idx = p;
         a.logm = logm;
         a.last = (p == a.npass - 1);
         a.post_lo = a.last ? post_lo : nullptr;
         a.post_hi = a.last ? post_hi : nullptr;
         a.post_bits = post_bits;
         a.post_scale = a.last ? post_scale : 1;
+        // factor ratio between outputs k1 + R1*k2 and k1 + R1*(k2+1): base^(R1 * n/R)
+        const uint32_t rb = a.rbits[p];
+        a.post_step = h_pow(post_base, (uint64_t)(1u << (rb / 2)) << (logn - rb));
         if (p == 0) {
             a.src = src;
             a.src_ld = src_ld;
@@ -385,10 +447,10 @@ int ntt_columns(Ctx &ctx, uint64_t *dst, uint64_t dst_ld, const uint64_t *src, u
             b.src = a.src + c0 * a.src_ld;
             b.dst = a.dst + c0 * a.dst_ld;
             prof_begin(s);
-            dispatch_pass(a.rbits[p], b, nc, s);
-            prof_end(PASS_NAMES[a.rbits[p]], 8.0 * (double)(nread + n) * (double)nc, s);
+            dispatch_pass(rb, b, nc, inverse, s);
+            prof_end(PASS_NAMES[rb], 8.0 * (double)(nread + n) * (double)nc, s);
         }
-        logm -= a.rbits[p];
+        logm -= rb;
     }
     return check_launch("k_ntt_pass");
 }

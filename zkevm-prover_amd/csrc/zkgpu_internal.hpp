@@ -59,7 +59,7 @@ void prof_end(const char *kernel, double bytes, hipStream_t s);
 // ---- ntt.hip
 int ntt_columns(Ctx &c, uint64_t *dst, uint64_t dst_ld, const uint64_t *src, uint64_t src_ld, uint64_t src_valid,
                 uint64_t *tmp, uint64_t tmp_ld, uint32_t logn, uint64_t ncols, int inverse, const uint64_t *post_lo,
-                const uint64_t *post_hi, uint32_t post_bits, uint64_t post_scale, hipStream_t s);
+                const uint64_t *post_hi, uint32_t post_bits, uint64_t post_base, uint64_t post_scale, hipStream_t s);
 void rows_to_cols(const uint64_t *in, uint64_t *out, uint64_t nrows, uint64_t ncols, uint64_t ld, hipStream_t s);
 void cols_to_rows(const uint64_t *in, uint64_t *out, uint64_t nrows, uint64_t ncols, uint64_t ld, hipStream_t s);
 void fill_powers(uint64_t *out, uint64_t base, uint64_t step, uint64_t scale, uint64_t count, hipStream_t s);

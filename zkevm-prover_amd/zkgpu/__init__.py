@@ -76,6 +76,16 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ZkgpuError("libzkgpu.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
+        # One HIP runtime per process: torch ships its own libamdhip64.so.7
+        # (same SONAME as /opt/rocm's).  Loading torch first makes the dynamic
+        # linker bind libzkgpu to that copy, so device pointers and streams
+        # are shared; loading ours first would bring up a second runtime.
+        try:
+            import torch  # noqa: F401
+            if torch.version.hip is not None:
+                torch.cuda.device_count()
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             f = getattr(L, name)
