@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--blowup-bits", type=int, default=1)
     ap.add_argument("--cpu-sample-cols", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_COLS", "4")))
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--workload", choices=["lde", "merkle"], default="lde",
+                    help="lde = configs[1] (headline); merkle = configs[2] (2^23 x 100 Poseidon tree)")
     return ap.parse_args()
 
 
@@ -62,6 +64,24 @@ def cpu_baseline(log_n, blow, ncols_sample):
     return {"value": out_elems / dt / 1e9, "unit": "Gelem/s", "cores": threads, "kind": "port",
             "sample": "oracle extendPol 2^%d->2^%d x %d cols, %.1f s, %d threads (%s)"
                       % (log_n, log_n + blow, ncols_sample, dt, threads, _cpu_model())}
+
+
+def cpu_baseline_merkle(log_n, ncols):
+    """Oracle merkletree (OpenMP) on a bounded sample of the same shape (fewer rows)."""
+    import numpy as np
+    from oracle import oracle as oc
+    oc.lib()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    oc.lib().oc_set_num_threads(threads)
+    rows = 1 << min(log_n, 16)
+    rng = np.random.default_rng(0x5EED)
+    x = rng.integers(0, 2**63, size=(rows, ncols), dtype=np.uint64)
+    t0 = time.perf_counter()
+    oc.merkletree(x)
+    dt = time.perf_counter() - t0
+    return {"value": rows * ncols / dt / 1e9, "unit": "Gelem/s", "cores": threads, "kind": "port",
+            "sample": "oracle merkletree 2^%d rows x %d cols, %.1f s, %d threads (%s)"
+                      % (min(log_n, 16), ncols, dt, threads, _cpu_model())}
 
 
 def _cpu_model():
@@ -97,11 +117,19 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED + rank)
     # canonical Goldilocks values: uniform in [0, 2^63) < p
-    trace = torch.randint(0, 2**63 - 1, (C, n), dtype=torch.int64, device=dev, generator=g)
-    out = torch.empty((C, ne), dtype=torch.int64, device=dev)
+    if args.workload == "lde":
+        trace = torch.randint(0, 2**63 - 1, (C, n), dtype=torch.int64, device=dev, generator=g)
+        out = torch.empty((C, ne), dtype=torch.int64, device=dev)
 
-    def step():
-        zkgpu.extend_pol_dev(out, ne, trace, n, ne, n, C)
+        def step():
+            zkgpu.extend_pol_dev(out, ne, trace, n, ne, n, C)
+    else:
+        rows = n
+        src = torch.randint(0, 2**63 - 1, (C, rows), dtype=torch.int64, device=dev, generator=g)
+        nodes = torch.empty(zkgpu.merkle_num_elements(rows), dtype=torch.int64, device=dev)
+
+        def step():
+            zkgpu.merkletree_dev(nodes, src, rows, C, rows)
 
     for _ in range(args.warmup):
         step()
@@ -137,16 +165,29 @@ def main():
     elapsed = float(t.item())
 
     if rank == 0:
-        total_elems = ne * C * world * args.steps
+        if args.workload == "lde":
+            total_elems = ne * C * world * args.steps
+            unit, metric_unit = "Gelem/s", "LDE output elements"
+            alg_step = 8 * (n + ne) * C  # per step per GPU
+        else:
+            total_elems = n * C * world * args.steps
+            unit, metric_unit = "Gelem/s", "Merkle leaf elements hashed"
+            alg_step = 8 * n * C + 32 * n + 96 * (n - 1)
         value = total_elems / elapsed / 1e9
         cpu = None
-        if world == 1 and not args.no_cpu:
+        if world == 1 and not args.no_cpu and args.workload == "lde":
             cpu = cpu_baseline(args.log_n, args.blowup_bits, args.cpu_sample_cols)
-        lde_bytes = 8 * (n + ne) * C  # per step per GPU
+        if world == 1 and not args.no_cpu and args.workload == "merkle":
+            cpu = cpu_baseline_merkle(args.log_n, C)
+        workload = ("LDE 2^%d -> 2^%d rows x %d cols per GPU (extendPol, starks.cpp:53), column-major in HBM"
+                    % (args.log_n, args.log_n + args.blowup_bits, C)) if args.workload == "lde" else (
+                    "Poseidon-GL Merkle tree over 2^%d rows x %d cols per GPU (merkelize, merkleTreeGL.cpp:37-44)"
+                    % (args.log_n, C))
         res = {
             "metric": METRIC,
             "value": round(value, 4),
-            "unit": "Gelem/s",
+            "unit": unit,
+            "value_meaning": metric_unit + " per second, all GPUs",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -157,8 +198,7 @@ def main():
             "dtype": "u64 (Goldilocks)",
             "data": "synthetic (uniform canonical Goldilocks, torch generator seed 0x5EED+rank)",
             "config": {
-                "workload": "LDE 2^%d -> 2^%d rows x %d cols per GPU (extendPol, starks.cpp:53), column-major in HBM"
-                            % (args.log_n, args.log_n + args.blowup_bits, C),
+                "workload": workload,
                 "log_n": args.log_n, "blowup_bits": args.blowup_bits, "ncols_per_gpu": C,
                 "parallelism": "column-sharded x%d (no data-path collective)" % world,
             },
@@ -172,7 +212,7 @@ def main():
                 "traffic": None,
                 "avg_launch_ms": round(avg_ms, 4),
                 "alg_bytes_per_launch": by / launches,
-                "lde_frac": round(lde_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                "step_frac": round(alg_step / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
             },
             "kernels": {k: {"launches": v[0], "avg_ms": round(v[1] / v[0], 4),
                             "GB/s": round(v[2] / v[0] / (v[1] / v[0] * 1e-3) / 1e9, 1)} for k, v in kernels.items()},

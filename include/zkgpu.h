@@ -111,6 +111,14 @@ int zkgpu_fri_fold_dev(uint64_t *out, const uint64_t *pol, uint32_t pol_bits, ui
 /* FRIProve::getTransposed (friProve.cpp:252-270), ext elements, device */
 int zkgpu_fri_transpose_dev(uint64_t *aux, const uint64_t *pol, uint64_t degree, uint32_t transpose_bits);
 
+/* ---- arithmetic self-test hook -----------------------------------------------
+ * Runs one device field operation elementwise on arbitrary u64 inputs
+ * (including non-canonical values >= p) and stores canonical results:
+ * op 0 a+b, 1 a-b, 2 a*b, 3 -a, 4 a*2^12, 5 a*2^48, 6 a*2^84, 7 a*2^100,
+ * 8 a^7, 9 cubic-extension a*b (a, b, out are n x 3).  Used by the parity
+ * tests to pin the arithmetic core against big-integer references. */
+int zkgpu_gl_field_selftest_dev(uint64_t *out, const uint64_t *a, const uint64_t *b, uint64_t n, int op);
+
 /* ---- live kernel profiling --------------------------------------------------
  * With profiling on, every kernel launch is bracketed by HIP events recorded
  * on the launch stream, tagged with the kernel name and its algorithmic bytes

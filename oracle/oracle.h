@@ -93,6 +93,23 @@ void oc_fri_fold_group(uint64_t out[3], const uint64_t *vals, uint64_t nx, uint6
 /* FRIProve::getTransposed (friProve.cpp:252-270) on ext elements */
 void oc_fri_get_transposed(uint64_t *aux, const uint64_t *pol, uint64_t degree, uint64_t transpose_bits);
 
+/* ---- STARK stages (stark.c) ---- */
+uint64_t oc_rand_u64(uint64_t seed, uint64_t stream, uint64_t col, uint64_t row);
+void oc_rand_cols(uint64_t *buf, uint64_t stride, const uint32_t *cols, uint64_t ncols, uint64_t nrows, uint64_t seed,
+                  uint64_t stream);
+struct zxp_instr_s;
+void oc_zxp_eval(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_tmp1, uint32_t n_tmp3,
+                 uint64_t **sec, const uint64_t *stride, uint64_t dom, const uint64_t *challenges,
+                 const uint64_t *publics, const uint64_t *evals, const uint64_t *x, const uint64_t *xdiv,
+                 const uint64_t *xdivw, const uint64_t *zhinv, uint64_t zhinv_size);
+int oc_calculate_z(uint64_t *z, uint64_t zs, const uint64_t *num, uint64_t ns, const uint64_t *den, uint64_t ds,
+                   uint64_t n);
+void oc_evmap(uint64_t *evals, const uint64_t *const *pols, const uint64_t *strides, const uint32_t *dims,
+              const uint32_t *primes, uint64_t n_ev, const uint64_t *lev, const uint64_t *lpev, uint64_t n,
+              uint32_t extend_bits);
+void oc_xdivxsub(uint64_t *xdiv, uint64_t *xdivw, const uint64_t *x, uint64_t n, const uint64_t xi[3], uint64_t w);
+void oc_powers(uint64_t *out, uint64_t start, uint64_t w, uint64_t n);
+
 /* ---- misc ---- */
 void oc_batch_inverse3(uint64_t *out, const uint64_t *in, uint64_t n); /* Polinomial::batchInverse */
 int oc_num_threads(void);

@@ -60,6 +60,16 @@ def lib():
             "oc_fri_fold_group": (None, [ptr, ptr, u64, u64, u64, ptr, u64]),
             "oc_fri_get_transposed": (None, [ptr, ptr, u64, u64]),
             "oc_batch_inverse3": (None, [ptr, ptr, u64]),
+            "oc_rand_u64": (u64, [u64, u64, u64, u64]),
+            "oc_rand_cols": (None, [ptr, u64, ctypes.c_void_p, u64, u64, u64, u64]),
+            "oc_zxp_eval": (None, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                   ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, u64, ptr, ptr, ptr, ptr,
+                                   ptr, ptr, ptr, u64]),
+            "oc_calculate_z": (ctypes.c_int, [ptr, u64, ptr, u64, ptr, u64, u64]),
+            "oc_evmap": (None, [ptr, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, u64, ptr,
+                                ptr, u64, ctypes.c_uint32]),
+            "oc_xdivxsub": (None, [ptr, ptr, ptr, u64, ptr, u64]),
+            "oc_powers": (None, [ptr, u64, u64, u64]),
             "oc_num_threads": (ctypes.c_int, []),
             "oc_set_num_threads": (None, [ctypes.c_int]),
         }

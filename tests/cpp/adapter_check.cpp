@@ -1,0 +1,74 @@
+// C++ host-adapter check: calls the reference-shaped API (NTT_Goldilocks,
+// PoseidonGoldilocks, MerklehashGoldilocks from host/zkgpu_goldilocks.hpp)
+// the way src/starkpil does, and compares against the CPU oracle
+// (oracle/liboracle.so, test infrastructure).  Exit code 0 = all equal.
+#include <stdio.h>
+#include <string.h>
+
+#include <random>
+#include <vector>
+
+#include "../../oracle/oracle.h"
+#include "../../zkevm-prover_amd/host/zkgpu_goldilocks.hpp"
+
+struct Element {  // stand-in with the layout of Goldilocks::Element
+    uint64_t fe;
+};
+
+static int failures = 0;
+static void expect(bool ok, const char *what)
+{
+    printf("%-48s %s\n", what, ok ? "ok" : "MISMATCH");
+    if (!ok) failures++;
+}
+
+int main()
+{
+    std::mt19937_64 rng(42);
+    const uint64_t P = 0xFFFFFFFF00000001ULL;
+    // --- extendPol as starks.cpp:53 calls it (row-major, ncols stride)
+    const uint64_t N = 1 << 14, NE = 1 << 15, NC = 7;
+    std::vector<Element> in(N * NC), out(NE * NC), buf(NE * NC);
+    for (auto &e : in) e.fe = rng() % P;
+    zkgpu::NTT_Goldilocks ntt(N);
+    zkgpu::NTT_Goldilocks nttExtended(NE);
+    nttExtended.extendPol(out.data(), in.data(), NE, N, NC, buf.data());
+    std::vector<uint64_t> ref(NE * NC);
+    oc_extend_pol(ref.data(), (uint64_t *)in.data(), NE, N, NC);
+    expect(memcmp(ref.data(), out.data(), ref.size() * 8) == 0, "NTT_Goldilocks::extendPol 2^14->2^15 x7");
+
+    // --- INTT(dst, src, NE, 3, NULL, 2, 1) as starks.cpp:262
+    std::vector<Element> q(NE * 3), qq(NE * 3);
+    for (auto &e : q) e.fe = rng() % P;
+    nttExtended.INTT(qq.data(), q.data(), NE, 3, (Element *)nullptr, 2, 1);
+    std::vector<uint64_t> qref(NE * 3);
+    oc_ntt(qref.data(), (uint64_t *)q.data(), NE, 3, 1);
+    expect(memcmp(qref.data(), qq.data(), qref.size() * 8) == 0, "NTT_Goldilocks::INTT 2^15 x3");
+    nttExtended.NTT(qq.data(), qq.data(), NE, 3);
+    expect(memcmp(q.data(), qq.data(), q.size() * 8) == 0, "NTT(INTT(x)) == x in place");
+
+    // --- Poseidon as transcript.cpp:23
+    Element st[12], o[12];
+    uint64_t oref[12];
+    for (auto &e : st) e.fe = rng() % P;
+    zkgpu::PoseidonGoldilocks::hash_full_result(o, st);
+    oc_poseidon_full(oref, (uint64_t *)st);
+    expect(memcmp(oref, o, sizeof oref) == 0, "PoseidonGoldilocks::hash_full_result");
+
+    // --- merkletree_avx as merkleTreeGL.cpp:42, root as MerkleTreeGL::getRoot
+    const uint64_t H = 1 << 12, W = 37;
+    std::vector<Element> src(H * W);
+    for (auto &e : src) e.fe = rng() % P;
+    uint64_t ne = zkgpu::MerklehashGoldilocks::getTreeNumElements(H);
+    std::vector<Element> nodes(ne);
+    zkgpu::PoseidonGoldilocks::merkletree_avx(nodes.data(), src.data(), W, H);
+    std::vector<uint64_t> nref(oc_merkle_num_elements(H));
+    oc_merkletree(nref.data(), (uint64_t *)src.data(), W, H);
+    expect(ne == nref.size() && memcmp(nref.data(), nodes.data(), ne * 8) == 0, "PoseidonGoldilocks::merkletree_avx");
+    Element root[4];
+    zkgpu::MerklehashGoldilocks::root(root, nodes.data(), ne);
+    expect(memcmp(root, &nref[ne - 4], 32) == 0, "MerklehashGoldilocks::root");
+
+    printf("%s\n", failures ? "FAILED" : "ALL OK");
+    return failures ? 1 : 0;
+}

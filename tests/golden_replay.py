@@ -32,7 +32,7 @@ def arr(x):
     return np.array([int(v) for v in np.ravel(np.array(x, dtype=object))], dtype=np.uint64)
 
 
-def transcript_challenges(oc, proof, verkey, publics, meta):
+def transcript_challenges(oc, proof, verkey, publics, steps, n_queries):
     """Return (challenges dict, special_x list, query indices)."""
     t = oc.Transcript()
     t.put(arr(verkey))
@@ -51,7 +51,6 @@ def transcript_challenges(oc, proof, verkey, publics, meta):
     t.put(arr(proof["evals"]))
     ch[5] = t.get_field()
     ch[6] = t.get_field()
-    steps = meta["friSteps"]
     special = []
     for si in range(len(steps)):
         special.append(t.get_field())
@@ -59,64 +58,59 @@ def transcript_challenges(oc, proof, verkey, publics, meta):
             t.put(arr(proof["s%d_root" % (si + 1)]))
         else:
             t.put(arr(proof["finalPol"]))
-    ys = t.get_permutations(meta["nQueries"], steps[0])
+    ys = t.get_permutations(n_queries, steps[0])
     return ch, special, [int(y) for y in ys]
 
 
-def check_proof(oc, name, root_from_proof=None, fold_group=None):
-    """Replay one golden proof; returns a dict of mismatch counters (all 0 = pass).
-
-    root_from_proof(vals, siblings, idx) and fold_group(vals, g, pol_bits,
-    special_x, shift_inv) default to the oracle; tests pass GPU-backed ones.
-    """
-    meta = load_meta()
-    proof = load_proof(name)
-    verkey = meta[meta["proofs"][name]["verkey"]]
-    publics = list(proof["publics"]) + list(meta["recursive2_constRoot"])
+def verify_fri(oc, proof, verkey, publics, steps, n_queries, root_from_proof=None, fold_group=None):
+    """Re-derive transcript, openings and folds of a zkin-layout proof.
+    Returns (mismatch counters, query indices, challenges)."""
     root_from_proof = root_from_proof or oc.merkle_root_from_proof
     fold_group = fold_group or oc.fri_fold_group
-
-    ch, special, ys = transcript_challenges(oc, proof, verkey, publics, meta)
-    steps = meta["friSteps"]
-    nq = meta["nQueries"]
+    ch, special, ys = transcript_challenges(oc, proof, verkey, publics, steps, n_queries)
     bad = {"s0": 0, "fri_tree": 0, "fold": 0, "final": 0, "checked": 0}
-
-    s0_trees = [("1", proof["root1"]), ("3", proof["root3"]), ("4", proof["root4"]), ("C", verkey)]
+    s0_trees = [("1", proof["root1"]), ("2", proof["root2"]), ("3", proof["root3"]), ("4", proof["root4"]),
+                ("C", verkey)]
     for tag, root in s0_trees:
         key = "s0_vals" + tag
         if key not in proof:
             continue
-        for q in range(nq):
+        for q in range(n_queries):
             r = root_from_proof(arr(proof[key][q]), arr(proof["s0_siblings" + tag][q]), ys[q])
             bad["checked"] += 1
             if not np.array_equal(r, arr(root)):
                 bad["s0"] += 1
-
     shift_inv = oc.gl_inv(7)
-    # shiftInv after si=0 (reductionBits 0): unchanged
     for si in range(1, len(steps)):
         pol_bits = steps[si - 1]
         out_bits = steps[si]
-        vals_key = "s%d_vals" % si
-        for q in range(nq):
-            g_full = ys[q] % (1 << pol_bits)
-            g = g_full % (1 << out_bits)
-            vals = arr(proof[vals_key][q])
+        for q in range(n_queries):
+            g = ys[q] % (1 << out_bits)
+            vals = arr(proof["s%d_vals" % si][q])
             r = root_from_proof(vals, arr(proof["s%d_siblings" % si][q]), g)
             bad["checked"] += 1
             if not np.array_equal(r, arr(proof["s%d_root" % si])):
                 bad["fri_tree"] += 1
             folded = fold_group(vals, g, pol_bits, special[si], shift_inv)
             if si < len(steps) - 1:
-                nb = steps[si + 1]
-                j = g >> nb
+                j = g >> steps[si + 1]
                 expect = arr(proof["s%d_vals" % (si + 1)][q])[3 * j:3 * j + 3]
                 if not np.array_equal(folded, expect):
                     bad["fold"] += 1
             else:
-                expect = arr(proof["finalPol"][g])
-                if not np.array_equal(folded, expect):
+                if not np.array_equal(folded, arr(proof["finalPol"][g])):
                     bad["final"] += 1
         for _ in range(pol_bits - out_bits):
             shift_inv = oc.gl_mul(shift_inv, shift_inv)
+    return bad, ys, ch
+
+
+def check_proof(oc, name, root_from_proof=None, fold_group=None):
+    """Replay one golden proof; returns (mismatch counters, query indices)."""
+    meta = load_meta()
+    proof = load_proof(name)
+    verkey = meta[meta["proofs"][name]["verkey"]]
+    publics = list(proof["publics"]) + list(meta["recursive2_constRoot"])
+    bad, ys, _ = verify_fri(oc, proof, verkey, publics, meta["friSteps"], meta["nQueries"],
+                            root_from_proof=root_from_proof, fold_group=fold_group)
     return bad, ys

@@ -196,3 +196,59 @@ def test_golden_replay_on_gpu(oracle, zkgpu, name):
 
     bad, _ = check_proof(oracle, name, root_from_proof=root_from_proof, fold_group=fold_group)
     assert bad["s0"] == 0 and bad["fri_tree"] == 0 and bad["fold"] == 0 and bad["final"] == 0
+
+
+# ------------------------------------------------------------------ arithmetic core
+def _adversarial(rng, n):
+    """u64 values concentrated on the reduction edges (>= p, near 2^64, 2^32 boundaries)."""
+    special = [0, 1, 2, P - 2, P - 1, P, P + 1, P + 2**31, 2**64 - 2, 2**64 - 1, 2**32 - 1, 2**32, 2**32 + 1,
+               2**63, 2**63 - 1, 2**64 - 2**32, 2**64 - 2**32 - 1, 2**48, 2**96 % P, 0xFFFFFFFF00000000]
+    vals = list(special) + [int(v) for v in rng.integers(0, 2**64 - 1, size=n - len(special), dtype=np.uint64,
+                                                            endpoint=True)]
+    # half of the random ones pushed into [p, 2^64)
+    out = []
+    for i, v in enumerate(vals):
+        if i >= len(special) and i % 2:
+            v = P + v % (2**64 - P)
+        out.append(v)
+    return np.array(out, dtype=np.uint64)
+
+
+@pytest.mark.parametrize("op", list(range(9)))
+def test_field_core_adversarial(zkgpu, op):
+    import torch
+    rng = np.random.default_rng(op)
+    n = 4096
+    a = _adversarial(rng, n)
+    b = _adversarial(rng, n)[::-1].copy()
+    # all pairs of the special values too
+    sp = a[:20]
+    a = np.concatenate([a, np.repeat(sp, 20)])
+    b = np.concatenate([b, np.tile(sp, 20)])
+    n = a.size
+    out = torch.zeros(n, dtype=torch.int64, device="cuda:0")
+    zkgpu.field_selftest_dev(out, zkgpu.to_device(a), zkgpu.to_device(b), n, op)
+    torch.cuda.synchronize()
+    got = zkgpu.from_device(out)
+    A = [int(x) for x in a]
+    B = [int(x) for x in b]
+    f = {0: lambda x, y: x + y, 1: lambda x, y: x - y, 2: lambda x, y: x * y, 3: lambda x, y: -x,
+         4: lambda x, y: x << 12, 5: lambda x, y: x << 48, 6: lambda x, y: x << 84, 7: lambda x, y: x << 100,
+         8: lambda x, y: pow(x, 7, P)}[op]
+    exp = np.array([f(x, y) % P for x, y in zip(A, B)], dtype=np.uint64)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, [(hex(A[i]), hex(B[i]), hex(int(got[i])), hex(int(exp[i]))) for i in bad[:5]]
+
+
+def test_field_cubic_adversarial(oracle, zkgpu):
+    import torch
+    rng = np.random.default_rng(99)
+    n = 2000
+    a = _adversarial(rng, 3 * n)
+    b = _adversarial(rng, 3 * n)[::-1].copy()
+    out = torch.zeros(3 * n, dtype=torch.int64, device="cuda:0")
+    zkgpu.field_selftest_dev(out, zkgpu.to_device(a), zkgpu.to_device(b), n, 9)
+    torch.cuda.synchronize()
+    got = zkgpu.from_device(out)
+    for i in range(n):
+        assert np.array_equal(got[3 * i:3 * i + 3], oracle.gl3_mul(a[3 * i:3 * i + 3], b[3 * i:3 * i + 3])), i

@@ -46,6 +46,11 @@ for step in "$@"; do
             echo "batch=$b $(python -c "import json;d=json.load(open('gpurun_out/sweep_b$b.json'));print(d['ms_per_step'],'ms',d['value'],'Gelem/s',d['kernels'])")"
         done
         ;;
+    merkle)
+        timeout -k 10 600 python bench.py --workload merkle --steps 3 --warmup 1 > gpurun_out/bench_merkle.json 2> gpurun_out/bench_merkle.err
+        ok_or_stop $? "bench merkle"
+        cat gpurun_out/bench_merkle.json
+        ;;
     prof)
         cd /tmp
         timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run \

@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 runs into profiles/: kernel stats + per-launch HBM traffic.
+
+HBM bytes per launch follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and
+WRITE_SIZE come from separate --pmc passes (TCC slots), in KiB; on gfx950
+FETCH_SIZE reports half of the bytes of a wide coalesced streaming read, so
+traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+
+Usage: tools/pmc_traffic.py <gpurun_out dir> <round tag, e.g. r01>
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def per_kernel(path, counter):
+    agg = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        agg.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    dst = os.path.join(root, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    fetch = per_kernel(os.path.join(src, "pmc_fetch/run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(src, "pmc_write/run_counter_collection.csv"), "WRITE_SIZE")
+    out = {}
+    for k in fetch:
+        if k in write:
+            out[k] = {"FETCH_SIZE_KiB": fetch[k], "WRITE_SIZE_KiB": write[k],
+                      "hbm_bytes_per_launch": (2 * fetch[k] + write[k]) * 1024.0}
+    meta = {"_doc": "per-launch HBM traffic = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE half-count "
+                    "correction, MI355X_MICROARCH.md HBM); separate --pmc passes of `python3 bench.py --no-cpu "
+                    "--steps 2 --warmup 1`", "kernels": out}
+    with open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    shutil.copy(os.path.join(src, "prof/run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    if os.path.exists(os.path.join(src, "prof_bench.json")):
+        shutil.copy(os.path.join(src, "prof_bench.json"), os.path.join(dst, f"{tag}_prof_bench.json"))
+    print(json.dumps(meta, indent=1)[:2000])
+
+
+if __name__ == "__main__":
+    main()

@@ -172,11 +172,54 @@ static int ntt_dev(uint64_t *dst, uint64_t ld_dst, const uint64_t *src, uint64_t
                        c.stream);
 }
 
+__global__ void k_field_selftest(uint64_t *out, const uint64_t *a, const uint64_t *b, uint64_t n, int op)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (op == 9) {
+        gl3 x{{a[3 * i], a[3 * i + 1], a[3 * i + 2]}}, y{{b[3 * i], b[3 * i + 1], b[3 * i + 2]}};
+        gl3 r = gl3_canon(gl3_mul(x, y));
+        out[3 * i] = r.v[0];
+        out[3 * i + 1] = r.v[1];
+        out[3 * i + 2] = r.v[2];
+        return;
+    }
+    uint64_t x = a[i], y = b[i], r = 0;
+    switch (op) {
+    case 0: r = gl_add(x, y); break;
+    case 1: r = gl_sub(x, y); break;
+    case 2: r = gl_mul(x, y); break;
+    case 3: r = gl_neg(x); break;
+    case 4: r = mul2e<12>(x); break;
+    case 5: r = mul2e<48>(x); break;
+    case 6: r = mul2e<84>(x); break;
+    case 7: r = mul2e<100>(x); break;
+    case 8: {
+        uint64_t x2 = gl_mul(x, x), x3 = gl_mul(x2, x), x4 = gl_mul(x2, x2);
+        r = gl_mul(x3, x4);
+        break;
+    }
+    default: break;
+    }
+    out[i] = gl_canon(r);
+}
+
 }  // namespace zk
 
 using namespace zk;
 
 extern "C" {
+
+int zkgpu_gl_field_selftest_dev(uint64_t *out, const uint64_t *a, const uint64_t *b, uint64_t n, int op)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (op < 0 || op > 9) return set_error(ZKGPU_ERR_ARG, "field_selftest: unknown op %d", op);
+    if (!n) return 0;
+    hipLaunchKernelGGL(k_field_selftest, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, g_ctx.stream, out, a, b, n,
+                       op);
+    return check_launch("k_field_selftest");
+}
 
 int zkgpu_abi_version(void) { return 1; }
 

@@ -32,9 +32,9 @@ __global__ void __launch_bounds__(256) k_fri_fold(uint64_t *out, const uint64_t 
     for (int i = 0; i < NX; i++) {
         const uint64_t *p = pol + 3 * ((uint64_t)i * n_out + g);
         int r = brev(i, LOGNX);
-        v[r].v[0] = gl_canon(p[0]);
-        v[r].v[1] = gl_canon(p[1]);
-        v[r].v[2] = gl_canon(p[2]);
+        v[r].v[0] = p[0];
+        v[r].v[1] = p[1];
+        v[r].v[2] = p[2];
     }
 #pragma unroll
     for (int s = 1; s <= LOGNX; s++) {
@@ -68,9 +68,9 @@ __global__ void __launch_bounds__(256) k_fri_fold(uint64_t *out, const uint64_t 
 #pragma unroll
     for (int i = NX - 2; i >= 0; i--) acc = gl3_add(gl3_mul(acc, sx), v[i]);
     uint64_t *o = out + 3 * g;
-    o[0] = acc.v[0];
-    o[1] = acc.v[1];
-    o[2] = acc.v[2];
+    o[0] = gl_canon(acc.v[0]);
+    o[1] = gl_canon(acc.v[1]);
+    o[2] = gl_canon(acc.v[2]);
 }
 
 __global__ void k_fri_transpose(uint64_t *aux, const uint64_t *pol, uint64_t w, uint64_t h)

@@ -1,68 +1,83 @@
 // Goldilocks field F_p (p = 2^64 - 2^32 + 1) and cubic extension F_p[x]/(x^3-x-1)
 // for gfx950 device code.
 //
-// Semantics follow the reference's Goldilocks/Goldilocks3 API (submodule, used
-// e.g. at polinomial.hpp:178-207): every function returns a canonical value
-// (< p) given canonical inputs; loads from user buffers go through gl_canon so
-// non-canonical u64 inputs are accepted like the reference does.
+// Representation: "lazy".  Every operation accepts ANY u64 as an element
+// (value = x mod p) and returns some u64 congruent to the result -- not
+// necessarily < p.  Kernels canonicalise exactly once, with gl_canon() on
+// every store to a user-visible buffer (outputs are canonical, like the
+// reference's toU64/toString), and before any comparison of values.
+// Measured on MI355X (tools/microbench.hip): the lazy multiply runs 1.6x
+// faster than one that canonicalises every product.
 //
-// CDNA4 has no 64x64 multiply: the product is built from four 32x32->64
-// partial products (v_mad_u64_u32) and reduced with 2^64 = 2^32-1 (mod p),
-// 2^96 = -1 (mod p).
+// CDNA4 has no 64x64 multiply: the 128-bit product is built from four
+// 32x32->64 multiply-adds (v_mad_u64_u32) and folded with
+// 2^64 = 2^32 - 1 (mod p) and 2^96 = -1 (mod p).
+//
+// Semantics match the reference's Goldilocks/Goldilocks3 API (submodule,
+// used e.g. at polinomial.hpp:178-207) after canonicalisation.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #define ZK_P 0xFFFFFFFF00000001ULL
-#define ZK_EPS 0xFFFFFFFFULL
+#define ZK_EPS 0xFFFFFFFFULL  // 2^64 mod p
 
 namespace zk {
 
+// any u64 -> [0, p)   (x < 2^64 < 2p, so one conditional subtraction)
 __device__ __forceinline__ uint64_t gl_canon(uint64_t a) { return a >= ZK_P ? a - ZK_P : a; }
 
+// a + b (mod p), any inputs, lazy output
 __device__ __forceinline__ uint64_t gl_add(uint64_t a, uint64_t b)
 {
-    uint64_t s = a + b;
-    s += (s < a) ? ZK_EPS : 0;
-    return gl_canon(s);
+    uint64_t s, s2;
+    bool c = __builtin_add_overflow(a, b, &s);  // a + b = s + 2^64 c  ==  s + EPS c
+    bool c2 = __builtin_add_overflow(s, c ? ZK_EPS : 0ULL, &s2);
+    return s2 + (c2 ? ZK_EPS : 0ULL);  // c2 => s2 < EPS: no third carry
 }
 
+// a - b (mod p), any inputs, lazy output
 __device__ __forceinline__ uint64_t gl_sub(uint64_t a, uint64_t b)
 {
-    uint64_t d = a - b;
-    d -= (a < b) ? ZK_EPS : 0;
-    return d;
+    uint64_t d, d2;
+    bool br = __builtin_sub_overflow(a, b, &d);  // a - b = d - 2^64 br  ==  d - EPS br
+    bool br2 = __builtin_sub_overflow(d, br ? ZK_EPS : 0ULL, &d2);
+    return d2 - (br2 ? ZK_EPS : 0ULL);  // br2 => d2 > 2^64 - EPS: no third borrow
 }
 
-__device__ __forceinline__ uint64_t gl_neg(uint64_t a) { return a ? ZK_P - a : 0; }
+__device__ __forceinline__ uint64_t gl_neg(uint64_t a) { return gl_sub(0, a); }
 
-// (hi:lo) mod p, canonical
+// (hi:lo) mod p, lazy output.  hi*2^64 = hh*2^96 + hl*2^64 == -hh + hl*EPS
 __device__ __forceinline__ uint64_t gl_reduce128(uint64_t lo, uint64_t hi)
 {
-    uint32_t hh = (uint32_t)(hi >> 32);
-    uint32_t hl = (uint32_t)hi;
-    uint64_t t0 = lo - hh;
-    t0 -= (lo < hh) ? ZK_EPS : 0;
-    uint64_t t1 = ((uint64_t)hl << 32) - hl;  // hl * (2^32 - 1)
-    uint64_t r = t0 + t1;
-    r += (r < t1) ? ZK_EPS : 0;
-    return gl_canon(r);
+    const uint32_t hh = (uint32_t)(hi >> 32);
+    const uint32_t hl = (uint32_t)hi;
+    uint64_t t0, r;
+    bool br = __builtin_sub_overflow(lo, (uint64_t)hh, &t0);
+    t0 -= br ? ZK_EPS : 0ULL;  // br => t0 >= 2^64 - 2^32 + 1 > EPS
+    const uint64_t t1 = ((uint64_t)hl << 32) - hl;  // hl * EPS, <= 2^64 - 2^33 + 1
+    bool c = __builtin_add_overflow(t0, t1, &r);
+    return r + (c ? ZK_EPS : 0ULL);  // c => r < t1: no second carry
+}
+
+// lo + hl*2^64 for hl < 2^32 (no 2^96 term)
+__device__ __forceinline__ uint64_t gl_reduce96(uint64_t lo, uint32_t hl)
+{
+    const uint64_t t1 = ((uint64_t)hl << 32) - hl;
+    uint64_t r;
+    bool c = __builtin_add_overflow(lo, t1, &r);
+    return r + (c ? ZK_EPS : 0ULL);
 }
 
 __device__ __forceinline__ uint64_t gl_mul(uint64_t a, uint64_t b)
 {
-    uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);
-    uint32_t b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
-    uint64_t p00 = (uint64_t)a0 * b0;
-    uint64_t p01 = (uint64_t)a0 * b1;
-    uint64_t p10 = (uint64_t)a1 * b0;
-    uint64_t p11 = (uint64_t)a1 * b1;
-    // mid = p01 + p10 (65 bits)
-    uint64_t mid = p01 + p10;
-    uint64_t mid_c = (mid < p01) ? 1ULL : 0ULL;
-    uint64_t lo = p00 + (mid << 32);
-    uint64_t lo_c = (lo < p00) ? 1ULL : 0ULL;
-    uint64_t hi = p11 + (mid >> 32) + (mid_c << 32) + lo_c;
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);
+    const uint32_t b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const uint64_t p00 = (uint64_t)a0 * b0;
+    const uint64_t t = (uint64_t)a0 * b1 + (p00 >> 32);          // < 2^64
+    const uint64_t u = (uint64_t)a1 * b0 + (uint32_t)t;          // < 2^64
+    const uint64_t hi = (uint64_t)a1 * b1 + (t >> 32) + (u >> 32);  // < 2^64
+    const uint64_t lo = (u << 32) | (uint32_t)p00;
     return gl_reduce128(lo, hi);
 }
 
@@ -79,16 +94,22 @@ __device__ __forceinline__ uint64_t gl_pow(uint64_t a, uint64_t e)
     return r;
 }
 
-// x * m for a small constant m (< 2^32): two 32x32 products
-__device__ __forceinline__ uint64_t gl_mul_small(uint64_t a, uint32_t m)
+// x * 2^E (mod p), compile-time E in [0, 192): 2^96 = -1, 2^192 = 1.
+template <int E>
+__device__ __forceinline__ uint64_t mul2e(uint64_t x)
 {
-    uint64_t lo_p = (uint64_t)(uint32_t)a * m;
-    uint64_t hi_p = (uint64_t)(uint32_t)(a >> 32) * m;  // < 2^64
-    // a*m = lo_p + hi_p * 2^32
-    uint64_t lo = lo_p + (hi_p << 32);
-    uint64_t c = (lo < lo_p) ? 1ULL : 0ULL;
-    uint64_t hi = (hi_p >> 32) + c;
-    return gl_reduce128(lo, hi);
+    static_assert(E >= 0 && E < 192, "exponent range");
+    if constexpr (E == 0) {
+        return x;
+    } else if constexpr (E >= 96) {
+        return gl_neg(mul2e<E - 96>(x));
+    } else if constexpr (E <= 32) {
+        return gl_reduce96(x << E, (uint32_t)(x >> (64 - E)));
+    } else if constexpr (E < 64) {
+        return gl_reduce128(x << E, x >> (64 - E));
+    } else {
+        return mul2e<E - 48>(mul2e<48>(x));
+    }
 }
 
 // ---------------------------------------------------------------- F_p^3
@@ -109,6 +130,11 @@ __device__ __forceinline__ gl3 gl3_sub(const gl3 &a, const gl3 &b)
 __device__ __forceinline__ gl3 gl3_mul1(const gl3 &a, uint64_t b)
 {
     return gl3{{gl_mul(a.v[0], b), gl_mul(a.v[1], b), gl_mul(a.v[2], b)}};
+}
+
+__device__ __forceinline__ gl3 gl3_canon(const gl3 &a)
+{
+    return gl3{{gl_canon(a.v[0]), gl_canon(a.v[1]), gl_canon(a.v[2])}};
 }
 
 // polinomial.hpp:195-205 (Karatsuba over x^3 = x + 1)

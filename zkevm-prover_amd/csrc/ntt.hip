@@ -31,7 +31,7 @@ __global__ void k_fill_powers(uint64_t *out, uint64_t base, uint64_t step, uint6
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     uint64_t b = gl_pow(base, step);
-    out[i] = gl_mul(scale, gl_pow(b, i));
+    out[i] = gl_canon(gl_mul(scale, gl_pow(b, i)));
 }
 
 __device__ __forceinline__ uint32_t bitrev_u32(uint32_t x, uint32_t bits)
@@ -68,30 +68,17 @@ struct PassArgs {
 
 constexpr int GROUPS = 16;
 
-// x * 2^E mod p for a compile-time E in [0, 192) (2^96 = -1 mod p): the
-// twiddles of every DFT of size <= 64 are such powers (omega_R = 2^(192/R)).
-template <int E>
-__device__ __forceinline__ uint64_t mul2e(uint64_t x)
-{
-    if constexpr (E == 0) {
-        return x;
-    } else if constexpr (E >= 96) {
-        return gl_neg(mul2e<E - 96>(x));
-    } else if constexpr (E < 64) {
-        return gl_reduce128(x << E, x >> (64 - E));
-    } else {
-        return mul2e<E - 48>(mul2e<48>(x));
-    }
-}
-
 // radix-2 DIF network on R = 2^LOG registers; afterwards v[r] = X[bitrev(r)].
-// twiddle omega_{2h}^i = 2^(96 i / h) (forward), 2^(192 - 96 i / h) (inverse).
-template <int LOG, bool INV, int H, int I>
-__device__ __forceinline__ uint64_t dif_tw(uint64_t d)
+// twiddle omega_{2h}^i = 2^e with e = 96 i / h in [0, 96) (forward); the
+// inverse twiddle 2^(192 - e) = -2^(96 - e), so the inverse butterfly
+// computes (c - a) * 2^(96 - e) and never needs a negation.
+template <bool INV, int H, int I>
+__device__ __forceinline__ uint64_t dif_odd(uint64_t a, uint64_t c)
 {
     constexpr int e = (96 * I) / H;
-    if constexpr (e == 0) return d;
-    else return mul2e<INV ? (192 - e) % 192 : e>(d);
+    if constexpr (e == 0) return gl_sub(a, c);
+    else if constexpr (!INV) return mul2e<e>(gl_sub(a, c));
+    else return mul2e<96 - e>(gl_sub(c, a));
 }
 
 template <int LOG, bool INV, int H = (1 << LOG) / 2>
@@ -108,7 +95,7 @@ __device__ __forceinline__ void dft_regs(uint64_t *v)
                                 uint64_t a = v[B * 2 * H + I];
                                 uint64_t c = v[B * 2 * H + I + H];
                                 v[B * 2 * H + I] = gl_add(a, c);
-                                v[B * 2 * H + I + H] = dif_tw<LOG, INV, H, I>(gl_sub(a, c));
+                                v[B * 2 * H + I + H] = dif_odd<INV, H, I>(a, c);
                             }.template operator()<Is>(),
                             ...);
                     }(std::make_integer_sequence<int, H>{});
@@ -164,7 +151,7 @@ __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
 #pragma unroll
         for (int j1 = 0; j1 < R1; j1++) {
             uint64_t pos = base + ((uint64_t)(R2 * j1 + j2) << logmp) + g;
-            v[j1] = pos < a.src_valid ? gl_canon(src[pos]) : 0;
+            v[j1] = pos < a.src_valid ? src[pos] : 0;
         }
     } else {
         j2 = tid & (R2 - 1);
@@ -176,7 +163,7 @@ __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
 #pragma unroll
         for (int j1 = 0; j1 < R1; j1++) {
             uint64_t pos = (blk << LOGR) + R2 * j1 + j2;
-            v[j1] = pos < a.src_valid ? gl_canon(src[pos]) : 0;
+            v[j1] = pos < a.src_valid ? src[pos] : 0;
         }
     }
     dft_regs<L1, INV>(v);
@@ -207,7 +194,7 @@ __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
             const int r = brev_c(k2, L2);
             uint64_t x = v[r];
             if (k1 | k2) x = gl_mul(x, t);
-            dst[base + ((uint64_t)(k1 + R1 * k2) << logmp) + g] = x;
+            dst[base + ((uint64_t)(k1 + R1 * k2) << logmp) + g] = x;  // intermediate: lazy
             t = gl_mul(t, step);
         }
     } else {
@@ -229,17 +216,15 @@ __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
         }
         const uint32_t lognr = a.logn - LOGR;
         const uint64_t x0 = (k1g * 16 + g) + (rrev << a.rbits[0]) + ((uint64_t)k1 << lognr);
-        uint64_t f = 1;
-        if (a.post_lo)
-            f = gl_mul(a.post_lo[x0 & ((1ULL << a.post_bits) - 1)], a.post_hi[x0 >> a.post_bits]);
-        else
-            f = a.post_scale;
+        const bool scaled = a.post_lo != nullptr || a.post_scale != 1;
+        uint64_t f = a.post_scale;
+        if (a.post_lo) f = gl_mul(a.post_lo[x0 & ((1ULL << a.post_bits) - 1)], a.post_hi[x0 >> a.post_bits]);
 #pragma unroll
         for (int k2 = 0; k2 < R2; k2++) {
             const int r = brev_c(k2, L2);
             uint64_t x = v[r];
-            if (f != 1) x = gl_mul(x, f);
-            dst[x0 + ((uint64_t)(R1 * k2) << lognr)] = x;
+            if (scaled) x = gl_mul(x, f);
+            dst[x0 + ((uint64_t)(R1 * k2) << lognr)] = gl_canon(x);
             if (a.post_lo) f = gl_mul(f, a.post_step);
         }
     }
@@ -270,7 +255,7 @@ __global__ void __launch_bounds__(PASS_THREADS) k_ntt_small(SmallArgs a)
     const uint64_t *src = a.src + (uint64_t)col * a.src_ld;
     uint64_t *dst = a.dst + (uint64_t)col * a.dst_ld;
     const uint32_t n = 1u << a.logn;
-    for (uint32_t i = threadIdx.x; i < n; i += PASS_THREADS) lds[i] = i < a.src_valid ? gl_canon(src[i]) : 0;
+    for (uint32_t i = threadIdx.x; i < n; i += PASS_THREADS) lds[i] = i < a.src_valid ? src[i] : 0;
     for (int lh = (int)a.logn - 1; lh >= 0; lh--) {
         const uint32_t h = 1u << lh;
         __syncthreads();
@@ -292,7 +277,7 @@ __global__ void __launch_bounds__(PASS_THREADS) k_ntt_small(SmallArgs a)
             v = gl_mul(v, gl_mul(a.post_lo[k & ((1u << a.post_bits) - 1)], a.post_hi[k >> a.post_bits]));
         else if (a.post_scale != 1)
             v = gl_mul(v, a.post_scale);
-        dst[k] = v;
+        dst[k] = gl_canon(v);
     }
 }
 

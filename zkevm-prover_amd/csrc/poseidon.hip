@@ -92,10 +92,10 @@ __global__ void k_poseidon_batch(uint64_t *out, const uint64_t *in, uint64_t n, 
     if (i >= n) return;
     uint64_t st[12];
 #pragma unroll
-    for (int k = 0; k < 12; k++) st[k] = gl_canon(in[i * 12 + k]);
+    for (int k = 0; k < 12; k++) st[k] = in[i * 12 + k];
     poseidon_perm(st);
     const int w = full ? 12 : 4;
-    for (int k = 0; k < w; k++) out[i * w + k] = st[k];
+    for (int k = 0; k < w; k++) out[i * w + k] = gl_canon(st[k]);
 }
 
 // leaf digests from a column-major source (column c at src + c*ld)
@@ -118,13 +118,13 @@ __global__ void __launch_bounds__(256) k_leaves_cols(uint64_t *digests, const ui
                 for (int k = 0; k < 4; k++) st[8 + k] = st[k];
             }
 #pragma unroll
-            for (int k = 0; k < 8; k++) st[k] = (uint64_t)k < nk ? gl_canon(src[(c0 + k) * ld + i]) : 0;
+            for (int k = 0; k < 8; k++) st[k] = (uint64_t)k < nk ? src[(c0 + k) * ld + i] : 0;
             poseidon_perm(st);
         }
     }
     uint64_t *d = digests + 4 * i;
 #pragma unroll
-    for (int k = 0; k < 4; k++) d[k] = st[k];
+    for (int k = 0; k < 4; k++) d[k] = ncols <= 4 ? st[k] : gl_canon(st[k]);
 }
 
 // leaf digests from a row-major source (row i at src + i*ncols)
@@ -148,13 +148,13 @@ __global__ void __launch_bounds__(256) k_leaves_rows(uint64_t *digests, const ui
                 for (int k = 0; k < 4; k++) st[8 + k] = st[k];
             }
 #pragma unroll
-            for (int k = 0; k < 8; k++) st[k] = (uint64_t)k < nk ? gl_canon(row[c0 + k]) : 0;
+            for (int k = 0; k < 8; k++) st[k] = (uint64_t)k < nk ? row[c0 + k] : 0;
             poseidon_perm(st);
         }
     }
     uint64_t *d = digests + 4 * i;
 #pragma unroll
-    for (int k = 0; k < 4; k++) d[k] = st[k];
+    for (int k = 0; k < 4; k++) d[k] = ncols <= 4 ? st[k] : gl_canon(st[k]);
 }
 
 // one tree level: dst[i] = hash(lvl[2i] || lvl[2i+1] || 0000)
@@ -169,7 +169,7 @@ __global__ void __launch_bounds__(256) k_merkle_level(uint64_t *dst, const uint6
     for (int k = 8; k < 12; k++) st[k] = 0;
     poseidon_perm(st);
 #pragma unroll
-    for (int k = 0; k < 4; k++) dst[4 * i + k] = st[k];
+    for (int k = 0; k < 4; k++) dst[4 * i + k] = gl_canon(st[k]);
 }
 
 // openings: vals[q*ncols + c] = src[c*ld + idx[q]]; sibs[q][l][0..3]

@@ -1,0 +1,163 @@
+// zkgpu_goldilocks.hpp -- C++ host adapter: the reference's Goldilocks-library
+// class surface (NTT_Goldilocks, PoseidonGoldilocks, MerklehashGoldilocks)
+// implemented on top of the libzkgpu C-ABI (include/zkgpu.h).
+//
+// A zkevm-prover build swaps `#include "ntt_goldilocks.hpp"` /
+// `"poseidon_goldilocks.hpp"` / `"merklehash_goldilocks.hpp"` (the absent
+// src/goldilocks submodule, .gitmodules:1-3) for this header; the call sites in
+// src/starkpil (starks.cpp:53,134,215,262,285,326-327; merkleTreeGL.cpp:40-42;
+// transcript.cpp:23,46; friProve.cpp:100-102) compile unchanged because the
+// names, argument order and meaning are the reference's.  Element is any
+// 8-byte trivially-copyable type holding the u64 (Goldilocks::Element is
+// `struct { uint64_t fe; }`).
+//
+// Error behaviour mirrors the reference: a failing call logs and ends the
+// process (zklog.error + exitProcess(), exit_process.cpp:7); install a
+// different handler with zkgpu::set_error_handler.
+#pragma once
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <type_traits>
+
+#include "../../include/zkgpu.h"
+
+namespace zkgpu {
+
+using ErrorHandler = void (*)(const char *where, int code, const char *msg);
+
+inline void default_error_handler(const char *where, int code, const char *msg)
+{
+    fprintf(stderr, "zkgpu error in %s (%d): %s\n", where, code, msg);
+    exit(-1);  // exitProcess() in the reference
+}
+
+inline ErrorHandler &error_handler()
+{
+    static ErrorHandler h = default_error_handler;
+    return h;
+}
+inline void set_error_handler(ErrorHandler h) { error_handler() = h; }
+
+inline void check(int rc, const char *where)
+{
+    if (rc != ZKGPU_OK) error_handler()(where, rc, zkgpu_last_error());
+}
+
+inline void ensure_init(int device = 0)
+{
+    static bool done = false;
+    if (!done) {
+        check(zkgpu_init(device), "zkgpu_init");
+        done = true;
+    }
+}
+
+template <typename E>
+inline uint64_t *u64p(E *p)
+{
+    static_assert(sizeof(E) == 8 && std::is_trivially_copyable<E>::value, "Element must be one u64");
+    return reinterpret_cast<uint64_t *>(p);
+}
+template <typename E>
+inline const uint64_t *u64p(const E *p)
+{
+    static_assert(sizeof(E) == 8 && std::is_trivially_copyable<E>::value, "Element must be one u64");
+    return reinterpret_cast<const uint64_t *>(p);
+}
+
+// NTT_Goldilocks(maxDomainSize, nThreads, extension) -- starks.hpp:81-82.
+// nThreads/extension/buffer/nphase/nblock are CPU tuning knobs of the
+// reference; the GPU path ignores them (same results).
+class NTT_Goldilocks
+{
+public:
+    explicit NTT_Goldilocks(uint64_t maxDomainSize, uint32_t nThreads = 0, int extension = 1)
+        : maxDomainSize_(maxDomainSize)
+    {
+        (void)nThreads;
+        (void)extension;
+        ensure_init();
+    }
+
+    template <typename E>
+    void NTT(E *dst, E *src, uint64_t size, uint64_t ncols = 1, E *buffer = nullptr, uint64_t nphase = 3,
+             uint64_t nblock = 1)
+    {
+        (void)buffer, (void)nphase, (void)nblock;
+        check(zkgpu_gl_ntt(u64p(dst), u64p(src), size, ncols, 0), "NTT_Goldilocks::NTT");
+    }
+
+    template <typename E>
+    void INTT(E *dst, E *src, uint64_t size, uint64_t ncols = 1, E *buffer = nullptr, uint64_t nphase = 3,
+              uint64_t nblock = 1)
+    {
+        (void)buffer, (void)nphase, (void)nblock;
+        check(zkgpu_gl_ntt(u64p(dst), u64p(src), size, ncols, 1), "NTT_Goldilocks::INTT");
+    }
+
+    template <typename E>
+    void extendPol(E *output, E *input, uint64_t N_Extended, uint64_t N, uint64_t ncols, E *buffer = nullptr,
+                   uint64_t nphase = 3, uint64_t nblock = 1)
+    {
+        (void)buffer, (void)nphase, (void)nblock;
+        check(zkgpu_gl_extend_pol(u64p(output), u64p(input), N_Extended, N, ncols), "NTT_Goldilocks::extendPol");
+    }
+
+    uint64_t maxDomainSize() const { return maxDomainSize_; }
+
+private:
+    uint64_t maxDomainSize_;
+};
+
+// PoseidonGoldilocks static API -- transcript.cpp:23,46, merkleTreeGL.cpp:40-42
+struct PoseidonGoldilocks {
+    template <typename E>
+    static void hash_full_result(E *out, const E *in)
+    {
+        ensure_init();
+        check(zkgpu_gl_poseidon_full(u64p(out), u64p(in)), "PoseidonGoldilocks::hash_full_result");
+    }
+    template <typename E>
+    static void hash(E *out, const E *in)
+    {
+        ensure_init();
+        check(zkgpu_gl_poseidon_hash(u64p(out), u64p(in)), "PoseidonGoldilocks::hash");
+    }
+    template <typename E>
+    static void linear_hash(E *out, E *in, uint64_t size)
+    {
+        ensure_init();
+        check(zkgpu_gl_linear_hash(u64p(out), u64p(in), size), "PoseidonGoldilocks::linear_hash");
+    }
+    template <typename E>
+    static void merkletree(E *tree, E *input, uint64_t num_cols, uint64_t num_rows)
+    {
+        ensure_init();
+        check(zkgpu_gl_merkletree(u64p(tree), u64p(input), num_cols, num_rows), "PoseidonGoldilocks::merkletree");
+    }
+    // the reference selects these by __AVX512__ (merkleTreeGL.cpp:39-43)
+    template <typename E>
+    static void merkletree_avx(E *tree, E *input, uint64_t num_cols, uint64_t num_rows)
+    {
+        merkletree(tree, input, num_cols, num_rows);
+    }
+    template <typename E>
+    static void merkletree_avx512(E *tree, E *input, uint64_t num_cols, uint64_t num_rows)
+    {
+        merkletree(tree, input, num_cols, num_rows);
+    }
+};
+
+// MerklehashGoldilocks -- stark_info.hpp:332, build_const_tree.cpp:566-569
+struct MerklehashGoldilocks {
+    static uint64_t getTreeNumElements(uint64_t numRows) { return zkgpu_gl_merkle_num_elements(numRows); }
+    template <typename E>
+    static void root(E *out, E *tree, uint64_t numElementsTree)
+    {
+        for (int i = 0; i < 4; i++) out[i] = tree[numElementsTree - 4 + i];
+    }
+};
+
+}  // namespace zkgpu

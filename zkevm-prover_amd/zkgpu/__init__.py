@@ -57,6 +57,7 @@ _SIGS = {
     "zkgpu_gl_merkle_open_dev": (ctypes.c_int, [vp, vp, vp, vp, u64, u64, u64, vp, u64]),
     "zkgpu_fri_fold_dev": (ctypes.c_int, [vp, vp, u32, u32, vp, u64]),
     "zkgpu_fri_transpose_dev": (ctypes.c_int, [vp, vp, u64, u32]),
+    "zkgpu_gl_field_selftest_dev": (ctypes.c_int, [vp, vp, vp, u64, ctypes.c_int]),
     "zkgpu_prof_enable": (ctypes.c_int, [ctypes.c_int]),
     "zkgpu_prof_reset": (ctypes.c_int, []),
     "zkgpu_prof_query": (ctypes.c_int, [ctypes.c_char_p, pu64, ctypes.POINTER(ctypes.c_double),
@@ -247,6 +248,10 @@ def fri_fold_dev(out, pol, pol_bits, out_bits, special_x, shift_inv):
 
 def fri_transpose_dev(aux, pol, degree, transpose_bits):
     _check(lib().zkgpu_fri_transpose_dev(_addr(aux), _addr(pol), degree, transpose_bits), "zkgpu_fri_transpose_dev")
+
+
+def field_selftest_dev(out, a, b, n, op):
+    _check(lib().zkgpu_gl_field_selftest_dev(_addr(out), _addr(a), _addr(b), n, op), "zkgpu_gl_field_selftest_dev")
 
 
 # ---------------------------------------------------------------- profiling

@@ -1,0 +1,328 @@
+"""Synthetic starkinfo-shaped STARK instance.
+
+The real fork-9 zkEVM instance cannot run here (its starkinfo, constant tree,
+verkey and input are absent, and its memory map exceeds one GPU), so the
+full-STARK workload is a synthetic AIR with the same stage structure as
+Starks::genProof (starks.cpp:9-404):
+
+  constants  K_0..K_{nK-1} (pseudo-random), L_first (1 at row 0)
+  stage 1    cm1 = 3t columns; a[3j], a[3j+1] pseudo-random,
+             a[3j+2] = a[3j]*a[3j+1]*K_{j mod nK} + a[3j]             (degree 3)
+  stage 2    challenges u = ch[0], defVal = ch[1];
+             m extension columns h_j = sum_k a[s_j+k] u^(k+1) + defVal (cm2, 3m cols)
+  stage 3    challenges gamma = ch[2], beta = ch[3];
+             num_j = (h_j(x) + gamma) beta, den_j = (h_j(w x) + gamma) beta (tmpExp)
+             Z_j = grand product of num_j/den_j (calculateZ, polinomial.hpp:586-607);
+             it closes because den is num shifted by one row (cm3, 3m cols)
+  stage 4    alpha = ch[4]; C = Horner_alpha of all constraints; q = C / Z_H
+             (step42ns semantics, op 69), split into qDeg = 2 pieces (cm4, 6 cols)
+  stage 5    xi = ch[7]; evals (evmap); v1 = ch[5], v2 = ch[6];
+             f = Horner_v1(committed cols) + Horner_v2(p - p(xi)) x/(x-xi)
+                 + Horner_v2(p' - p(w xi)) x/(x - w xi)                (step52ns form)
+  FRI        FRIProve::prove (friProve.cpp), queries on the 5 trees.
+
+The constraint/expression programs are emitted in the ZXP format
+(include/zkgpu_zxp.h) and evaluated by the GPU expression kernel (product) and
+by the oracle's C evaluator (tests).  The instance is valid: a correct prover
+produces a proof whose FRI layers are consistent and whose final polynomial
+has degree < 2^last / blowup.
+"""
+import numpy as np
+
+# kinds / ops / sections mirror include/zkgpu_zxp.h
+TMP1, TMP3, COL, COL3, LIT, CHAL, PUB, X, EVAL, XDIV, XDIVW, ZI = range(12)
+ADD, SUB, MUL, COPY = range(4)
+(SEC_CM1_N, SEC_CM2_N, SEC_CM3_N, SEC_TMP_N, SEC_CONST_N, SEC_CM1_2NS, SEC_CM2_2NS, SEC_CM3_2NS, SEC_CM4_2NS,
+ SEC_CONST_2NS, SEC_Q_2NS, SEC_F_2NS) = range(12)
+SEC_N_TO_2NS = {SEC_CM1_N: SEC_CM1_2NS, SEC_CM2_N: SEC_CM2_2NS, SEC_CM3_N: SEC_CM3_2NS, SEC_CONST_N: SEC_CONST_2NS}
+
+P = 0xFFFFFFFF00000001
+
+
+class Program:
+    """Builder for one ZXP program; operands are interned."""
+
+    def __init__(self, domain_ext):
+        self.domain_ext = int(domain_ext)
+        self.opnd = []
+        self._idx = {}
+        self.instr = []
+        self.n_tmp1 = 0
+        self.n_tmp3 = 0
+
+    def o(self, kind, a=0, b=0, c=0):
+        key = (kind, a & 0xFFFFFFFF, b & 0xFFFFFFFF, c & 0xFFFFFFFF)
+        if key not in self._idx:
+            self._idx[key] = len(self.opnd)
+            self.opnd.append(key)
+        return self._idx[key]
+
+    def tmp1(self):
+        self.n_tmp1 += 1
+        return self.o(TMP1, self.n_tmp1 - 1)
+
+    def tmp3(self):
+        self.n_tmp3 += 1
+        return self.o(TMP3, self.n_tmp3 - 1)
+
+    def col(self, sec, c, shift=0):
+        return self.o(COL, sec, c, shift)
+
+    def col3(self, sec, c, shift=0):
+        return self.o(COL3, sec, c, shift)
+
+    def lit(self, v):
+        v %= P
+        return self.o(LIT, v & 0xFFFFFFFF, v >> 32)
+
+    def chal(self, k):
+        return self.o(CHAL, k)
+
+    def ev(self, k):
+        return self.o(EVAL, k)
+
+    def op(self, op, dst, a, b=0):
+        self.instr.append((op, dst, a, b))
+        return dst
+
+    def arrays(self):
+        ins = np.array(self.instr, dtype=np.uint32).reshape(-1, 4)
+        opn = np.array(self.opnd, dtype=np.uint32).reshape(-1, 4)
+        return ins, opn
+
+
+class SyntheticStark:
+    def __init__(self, n_bits=10, blowup_bits=1, t=4, m=2, n_k=3, n_queries=16, fri_steps=None, n_publics=8,
+                 seed=0x5EED):
+        self.n_bits = n_bits
+        self.n_bits_ext = n_bits + blowup_bits
+        self.blowup_bits = blowup_bits
+        self.t, self.m, self.n_k = t, m, n_k
+        self.n_cm1 = 3 * t
+        self.n_cm2 = 3 * m
+        self.n_cm3 = 3 * m
+        self.n_tmp = 6 * m
+        self.n_const = n_k + 1
+        self.l_first = n_k  # const column index of L_first
+        self.q_deg, self.q_dim = 2, 3
+        self.n_cm4 = self.q_deg * self.q_dim
+        self.n_queries = n_queries
+        self.n_publics = n_publics
+        self.seed = seed
+        if fri_steps is None:
+            fri_steps = [self.n_bits_ext]
+            while fri_steps[-1] - 4 >= max(5, blowup_bits + 3):
+                fri_steps.append(fri_steps[-1] - 4)
+        self.fri_steps = fri_steps
+        # stage-2 groups: partition the cm1 columns into m contiguous groups
+        cols = list(range(self.n_cm1))
+        size = (len(cols) + m - 1) // m
+        self.groups = [cols[j * size:(j + 1) * size] for j in range(m)]
+        assert all(self.groups), "too many stage-2 groups for the cm1 width"
+        self.z_ctx = [(6 * j, 6 * j + 3, 3 * j) for j in range(m)]  # (num tmp col, den tmp col, z cm3 col)
+        self._build_evmap()
+        self.programs = {
+            "step1": self._prog_step1(),
+            "step2": self._prog_step2(),
+            "step3prev": self._prog_step3prev(),
+            "step42ns": self._prog_step42ns(),
+            "step52ns": self._prog_step52ns(),
+        }
+
+    # ------------------------------------------------------------ evMap
+    def _build_evmap(self):
+        """evMap entries (section_2ns, col, dim, prime), in the order the
+        transcript absorbs the evals (starks.cpp:336-339)."""
+        ev = []
+        for c in range(self.n_cm1):
+            ev.append((SEC_CM1_2NS, c, 1, 0))
+        for k in range(self.n_const):
+            ev.append((SEC_CONST_2NS, k, 1, 0))
+        for j in range(self.m):
+            ev.append((SEC_CM2_2NS, 3 * j, 3, 0))
+            ev.append((SEC_CM2_2NS, 3 * j, 3, 1))
+        for j in range(self.m):
+            ev.append((SEC_CM3_2NS, 3 * j, 3, 0))
+            ev.append((SEC_CM3_2NS, 3 * j, 3, 1))
+        for p in range(self.q_deg):
+            ev.append((SEC_CM4_2NS, 3 * p, 3, 0))
+        self.evmap = ev
+        self.ev_index = {(s, c, pr): i for i, (s, c, d, pr) in enumerate(ev)}
+
+    # ------------------------------------------------------------ programs
+    def _prog_step1(self):
+        """Trace derivation (executor stand-in): a[3j+2] = a[3j] a[3j+1] K_j + a[3j]."""
+        p = Program(0)
+        t = p.tmp1()
+        for j in range(self.t):
+            a0, a1, a2 = (p.col(SEC_CM1_N, 3 * j + k) for k in range(3))
+            kk = p.col(SEC_CONST_N, j % self.n_k)
+            p.op(MUL, t, a0, a1)
+            p.op(MUL, t, t, kk)
+            p.op(ADD, t, t, a0)
+            p.op(COPY, a2, t)
+        return p
+
+    def _emit_h(self, p, grp, sec, shift, dst3):
+        """dst3 = sum_k a[s+k] u^(k+1) + defVal over the group's columns."""
+        u = p.chal(0)
+        dv = p.chal(1)
+        cols = grp
+        p.op(MUL, dst3, u, p.col(sec, cols[-1], shift))
+        for c in reversed(cols[:-1]):
+            p.op(ADD, dst3, dst3, p.col(sec, c, shift))
+            p.op(MUL, dst3, dst3, u)
+        p.op(ADD, dst3, dst3, dv)
+        return dst3
+
+    def _prog_step2(self):
+        p = Program(0)
+        h = p.tmp3()
+        for j, grp in enumerate(self.groups):
+            self._emit_h(p, grp, SEC_CM1_N, 0, h)
+            p.op(COPY, p.col3(SEC_CM2_N, 3 * j), h)
+        return p
+
+    def _prog_step3prev(self):
+        p = Program(0)
+        t = p.tmp3()
+        gamma, beta = p.chal(2), p.chal(3)
+        for j in range(self.m):
+            num_c, den_c, _ = self.z_ctx[j]
+            p.op(ADD, t, p.col3(SEC_CM2_N, 3 * j, 0), gamma)
+            p.op(MUL, p.col3(SEC_TMP_N, num_c), t, beta)
+            p.op(ADD, t, p.col3(SEC_CM2_N, 3 * j, 1), gamma)
+            p.op(MUL, p.col3(SEC_TMP_N, den_c), t, beta)
+        return p
+
+    def constraints(self, p, nxt):
+        """Yield (emit_fn) for each constraint; each writes its value into a
+        fresh temp and returns it.  nxt = row shift of "next row"."""
+        out = []
+        for j in range(self.t):
+            def c_mul(j=j):
+                r = p.tmp1()
+                a0, a1, a2 = (p.col(SEC_CM1_2NS, 3 * j + k) for k in range(3))
+                p.op(MUL, r, a0, a1)
+                p.op(MUL, r, r, p.col(SEC_CONST_2NS, j % self.n_k))
+                p.op(ADD, r, r, a0)
+                p.op(SUB, r, a2, r)
+                return r
+            out.append(c_mul)
+        for j, grp in enumerate(self.groups):
+            def c_h(j=j, grp=grp):
+                r = p.tmp3()
+                self._emit_h(p, grp, SEC_CM1_2NS, 0, r)
+                p.op(SUB, r, p.col3(SEC_CM2_2NS, 3 * j), r)
+                return r
+            out.append(c_h)
+        for j in range(self.m):
+            def c_first(j=j):
+                r = p.tmp3()
+                p.op(SUB, r, p.col3(SEC_CM3_2NS, 3 * j), p.lit(1))
+                p.op(MUL, r, r, p.col(SEC_CONST_2NS, self.l_first))
+                return r
+            out.append(c_first)
+        for j in range(self.m):
+            def c_z(j=j):
+                gamma, beta = p.chal(2), p.chal(3)
+                r = p.tmp3()
+                s = p.tmp3()
+                p.op(ADD, r, p.col3(SEC_CM2_2NS, 3 * j, nxt), gamma)
+                p.op(MUL, r, r, beta)
+                p.op(MUL, r, r, p.col3(SEC_CM3_2NS, 3 * j, nxt))
+                p.op(ADD, s, p.col3(SEC_CM2_2NS, 3 * j, 0), gamma)
+                p.op(MUL, s, s, beta)
+                p.op(MUL, s, s, p.col3(SEC_CM3_2NS, 3 * j, 0))
+                p.op(SUB, r, r, s)
+                return r
+            out.append(c_z)
+        return out
+
+    def _prog_step42ns(self):
+        p = Program(1)
+        nxt = 1 << self.blowup_bits
+        alpha = p.chal(4)
+        acc = p.tmp3()
+        first = True
+        for emit in self.constraints(p, nxt):
+            r = emit()
+            if first:
+                p.op(COPY, acc, r)
+                first = False
+            else:
+                p.op(MUL, acc, acc, alpha)
+                p.op(ADD, acc, acc, r)
+        p.op(MUL, p.col3(SEC_Q_2NS, 0), acc, p.o(ZI))
+        return p
+
+    def committed_columns(self):
+        """(section, col, dim) of every committed polynomial, Horner order of f."""
+        cols = [(SEC_CM1_2NS, c, 1) for c in range(self.n_cm1)]
+        cols += [(SEC_CM2_2NS, 3 * j, 3) for j in range(self.m)]
+        cols += [(SEC_CM3_2NS, 3 * j, 3) for j in range(self.m)]
+        cols += [(SEC_CM4_2NS, 3 * q, 3) for q in range(self.q_deg)]
+        return cols
+
+    def _prog_step52ns(self):
+        p = Program(1)
+        v1, v2 = p.chal(5), p.chal(6)
+        acc = p.tmp3()
+        first = True
+        for sec, c, dim in self.committed_columns():
+            opnd = p.col(sec, c) if dim == 1 else p.col3(sec, c)
+            if first:
+                p.op(MUL, acc, opnd, v1)  # promote to F_p^3 via v1 (reference op 0: T0 = pols * v1)
+                first = False
+            else:
+                p.op(MUL, acc, acc, v1)
+                p.op(ADD, acc, acc, opnd)
+        for prime, xdiv in ((0, XDIV), (1, XDIVW)):
+            g = p.tmp3()
+            d = p.tmp3()
+            firstg = True
+            for i, (sec, c, dim, pr) in enumerate(self.evmap):
+                if pr != prime:
+                    continue
+                opnd = p.col(sec, c) if dim == 1 else p.col3(sec, c)
+                p.op(SUB, d, opnd, p.ev(i))
+                if firstg:
+                    p.op(COPY, g, d)
+                    firstg = False
+                else:
+                    p.op(MUL, g, g, v2)
+                    p.op(ADD, g, g, d)
+            p.op(MUL, g, g, p.o(xdiv))
+            p.op(ADD, acc, acc, g)
+        p.op(COPY, p.col3(SEC_F_2NS, 0), acc)
+        return p
+
+    # ------------------------------------------------------------ description
+    def info(self):
+        return {
+            "nBits": self.n_bits, "nBitsExt": self.n_bits_ext, "nQueries": self.n_queries,
+            "friSteps": self.fri_steps, "nCm1": self.n_cm1, "nCm2": self.n_cm2, "nCm3": self.n_cm3,
+            "nCm4": self.n_cm4, "nTmp": self.n_tmp, "nConst": self.n_const, "nPublics": self.n_publics,
+            "qDeg": self.q_deg, "qDim": self.q_dim, "lFirst": self.l_first, "seed": self.seed,
+            "randomCm1Cols": [c for c in range(self.n_cm1) if c % 3 != 2],
+            "zCtx": self.z_ctx, "evMap": self.evmap,
+        }
+
+    def random_cm1_cols(self):
+        return [c for c in range(self.n_cm1) if c % 3 != 2]
+
+
+# ---------------------------------------------------------------- PRNG
+MASK64 = (1 << 64) - 1
+
+
+def rand_u64(seed, stream, col, row):
+    """Deterministic pseudo-random canonical element (splitmix64 finaliser);
+    the same function is implemented by the GPU trace generator
+    (csrc/stark.hip k_rand_cols) and the oracle (oracle/stark.c)."""
+    x = (seed ^ (stream << 56) ^ (col * 0x9E3779B97F4A7C15) ^ (row * 0xC2B2AE3D27D4EB4F)) & MASK64
+    z = (x + 0x9E3779B97F4A7C15) & MASK64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & MASK64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & MASK64
+    z ^= z >> 31
+    return z >> 1
