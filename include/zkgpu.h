@@ -111,6 +111,72 @@ int zkgpu_fri_fold_dev(uint64_t *out, const uint64_t *pol, uint32_t pol_bits, ui
 /* FRIProve::getTransposed (friProve.cpp:252-270), ext elements, device */
 int zkgpu_fri_transpose_dev(uint64_t *aux, const uint64_t *pol, uint64_t degree, uint32_t transpose_bits);
 
+/* ---- device memory (the host orchestrator owns HBM through these) -------- */
+int zkgpu_dev_malloc(void **ptr, uint64_t bytes);
+int zkgpu_dev_free(void *ptr);
+int zkgpu_memcpy_h2d(void *dst, const void *src, uint64_t bytes);
+int zkgpu_memcpy_d2h(void *dst, const void *src, uint64_t bytes);
+int zkgpu_memcpy_d2d(void *dst, const void *src, uint64_t bytes);
+int zkgpu_memset_dev(void *dst, int value, uint64_t bytes);
+
+/* ---- STARK stage primitives (device-resident, column-major sections) ------
+ * Section table for the expression programs: base pointer + leading
+ * dimension per eSection (include/zkgpu_zxp.h SEC_*), the device analogue of
+ * the reference's mapOffsets/mapSectionsN (stark_info.cpp:473-482). */
+typedef struct {
+    uint64_t *sec[12];
+    uint64_t ld[12];    /* leading dimension = rows allocated per column */
+    uint32_t ncols[12]; /* columns allocated (bounds-checked at launch) */
+} zkgpu_sections;
+
+/* Executor stand-in for synthetic traces: column cols[k] of a column-major
+ * buffer gets the deterministic pseudo-random elements rand(seed, stream, col, row). */
+int zkgpu_rand_cols_dev(uint64_t *base, uint64_t ld, const uint32_t *cols, uint32_t ncols, uint64_t nrows,
+                        uint64_t seed, uint64_t stream);
+
+/* Steps::step*_parser_first (steps.hpp:21-58; used at starks.cpp:73,155,193,
+ * 241,371): evaluate one expression program (include/zkgpu_zxp.h) over every
+ * row of its domain (2^log_dom rows).  instr/opnd are host arrays (uploaded),
+ * challenges (8 x 3), publics and evals are host arrays; xdiv/xdivw are
+ * device arrays (2n x 3 interleaved) for the FRI program, else NULL;
+ * extend_bits sizes zhInv (zhInv.cpp:7-31); x_start = 1 (n domain) or 7 (2n). */
+int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd, uint32_t n_tmp1,
+                       uint32_t n_tmp3, const zkgpu_sections *sections, uint32_t log_dom, const uint64_t *challenges,
+                       const uint64_t *publics, uint32_t n_publics, const uint64_t *evals, uint32_t n_evals,
+                       const uint64_t *xdiv, const uint64_t *xdivw, uint32_t extend_bits, uint64_t x_start);
+
+/* Polinomial::calculateZ(z, num, den) (polinomial.hpp:586-607), F_p^3 columns
+ * (3 consecutive columns of ld each).  *closes = 1 iff z[n-1]*num[n-1]/den[n-1] == 1
+ * (the reference's zkassert). */
+int zkgpu_calculate_z_dev(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,
+                          uint64_t den_ld, uint64_t n, int *closes);
+
+/* Starks::evmap (starks.cpp:556-669): evals[e] = sum_{k<n} L(k) * pol_e[k << extend_bits],
+ * L = lev or lpev (device, 3 columns of ld l_ld).  cols = host array of device
+ * column pointers (first column of each polynomial), lds / dims / primes per
+ * entry.  evals_out: host (n_ev x 3). */
+int zkgpu_evmap_dev(uint64_t *evals_out, const uint64_t *const *cols, const uint64_t *lds, const uint32_t *dims,
+                    const uint32_t *primes, uint32_t n_ev, const uint64_t *lev, const uint64_t *lpev, uint64_t l_ld,
+                    uint64_t n, uint32_t extend_bits);
+
+/* xDivXSubXi / xDivXSubWXi (starks.cpp:344-366) over x_k = 7 w_{2n}^k, k < 2^n_bits_ext;
+ * w = Goldilocks::w(n_bits).  Outputs interleaved (2n x 3), device. */
+int zkgpu_xdivxsub_dev(uint64_t *xdiv, uint64_t *xdivw, const uint64_t xi[3], uint32_t n_bits, uint32_t n_bits_ext);
+
+/* base^k for k < n into 3 columns of ld (LEv / LpEv, starks.cpp:308-324) */
+int zkgpu_ext_powers_dev(uint64_t *out, uint64_t ld, const uint64_t base[3], uint64_t n);
+
+/* quotient split (starks.cpp:266-281): qq2 col 3p+d row k = qq1 col d row pN+k * shift_in^p, k < n */
+int zkgpu_qsplit_dev(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t q_deg,
+                     uint64_t shift_in);
+
+/* 3 ext columns (ld) -> interleaved n x 3 (the FRI polynomial layout, friProve.cpp) */
+int zkgpu_cols3_to_interleaved_dev(uint64_t *out, const uint64_t *cols, uint64_t ld, uint64_t n);
+
+/* MerkleTreeGL::getGroupProof for a row-major device source (FRI trees) */
+int zkgpu_gl_merkle_open_rows_dev(uint64_t *vals_out, uint64_t *sibs_out, const uint64_t *nodes, const uint64_t *src,
+                                  uint64_t ncols, uint64_t nrows, const uint64_t *idx, uint64_t nq);
+
 /* ---- arithmetic self-test hook -----------------------------------------------
  * Runs one device field operation elementwise on arbitrary u64 inputs
  * (including non-canonical values >= p) and stores canonical results:

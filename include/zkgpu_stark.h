@@ -1,0 +1,70 @@
+/*
+ * zkgpu_stark.h -- C-ABI of libzkgpu_stark, the host-side STARK prover
+ * (a C++ restatement of Starks::genProof, starks.cpp:9-404, and
+ * FRIProve::prove, friProve.cpp:5-190) that drives the MI355X kernels only
+ * through include/zkgpu.h.  The instance description plays the role of the
+ * reference's StarkInfo (stark_info.hpp:269-336) + Steps (steps.hpp).
+ *
+ * Proof output: one flat u64 buffer in the reference's zkin order
+ * (proof2zkinStark.cpp:8-82), canonical values:
+ *   root1[4] root2[4] root3[4] root4[4] evals[n_ev*3]
+ *   for si = 1 .. n_fri_steps-1:
+ *       s{si}_root[4]  s{si}_vals[Q][3*2^(steps[si-1]-steps[si])]  s{si}_siblings[Q][steps[si]][4]
+ *   s0_vals1[Q][n_cm1] s0_vals2[Q][n_cm2] s0_vals3[Q][n_cm3] s0_vals4[Q][n_cm4] s0_valsC[Q][n_const]
+ *   s0_siblings{1,2,3,4,C}[Q][n_bits_ext][4]
+ *   finalPol[2^steps[last]][3]
+ */
+#ifndef ZKGPU_STARK_H
+#define ZKGPU_STARK_H
+#include <stdint.h>
+
+#include "zkgpu_zxp.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    const zxp_instr *instr;
+    uint32_t n_instr;
+    const zxp_operand *opnd;
+    uint32_t n_opnd;
+    uint32_t n_tmp1, n_tmp3;
+} zkgpu_zxp_prog;
+
+typedef struct {
+    uint32_t n_bits, n_bits_ext, n_queries, n_fri_steps;
+    uint32_t fri_steps[32];
+    uint32_t n_cm1, n_cm2, n_cm3, n_cm4, n_tmp, n_const, n_publics, q_deg, l_first, n_k;
+    uint64_t seed;
+    uint32_t n_random_cols;
+    const uint32_t *random_cols; /* cm1 columns filled by the trace generator */
+    uint32_t n_zctx;
+    const uint32_t *zctx; /* (num tmp col, den tmp col, z cm3 col) triples */
+    uint32_t n_ev;
+    const uint32_t *ev; /* evMap (section_2ns, col, dim, prime) quads */
+    zkgpu_zxp_prog step1, step2, step3prev, step42ns, step52ns;
+} zkgpu_stark_info;
+
+/* allocate the HBM memory map, build the constant polynomials, their LDE and
+ * the constant tree (the reference loads these from files; setup, untimed) */
+int zkgpu_stark_create(void **handle, const zkgpu_stark_info *info);
+/* synthetic committed trace cm1_n (executor stand-in: PRNG columns + step1) */
+int zkgpu_stark_witness(void *handle);
+/* load cm1_n from a host row-major buffer (n rows x n_cm1), the reference's
+ * commit-pols layout (commit_pols.hpp:18) */
+int zkgpu_stark_set_cm1(void *handle, const uint64_t *rows);
+uint64_t zkgpu_stark_proof_len(void *handle);
+int zkgpu_stark_prove(void *handle, uint64_t *proof_out);
+int zkgpu_stark_verkey(void *handle, uint64_t out[4]);
+int zkgpu_stark_publics(void *handle, uint64_t *out);
+/* STARK_STEP_* timers of the last prove (starks.cpp:49-403 names):
+ * names '\n'-separated into names_buf, milliseconds into ms; returns count */
+int zkgpu_stark_timers(void *handle, char *names_buf, uint64_t names_len, double *ms, uint32_t max);
+void zkgpu_stark_destroy(void *handle);
+const char *zkgpu_stark_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZKGPU_STARK_H */

@@ -467,6 +467,280 @@ int zkgpu_gl_merkle_open_dev(uint64_t *vals_out, uint64_t *sibs_out, const uint6
     return check_hip(hipStreamSynchronize(c.stream), "merkle_open sync");
 }
 
+// ---------------------------------------------------------------- device memory
+int zkgpu_dev_malloc(void **ptr, uint64_t bytes)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (hipMalloc(ptr, bytes ? bytes : 8) != hipSuccess) {
+        *ptr = nullptr;
+        return set_error(ZKGPU_ERR_OOM, "hipMalloc(%llu) failed", (unsigned long long)bytes);
+    }
+    return 0;
+}
+int zkgpu_dev_free(void *ptr) { return ptr ? check_hip(hipFree(ptr), "hipFree") : 0; }
+int zkgpu_memcpy_h2d(void *dst, const void *src, uint64_t bytes)
+{
+    if (!bytes) return 0;
+    int rc = check_hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, g_ctx.stream), "H2D");
+    return rc ? rc : check_hip(hipStreamSynchronize(g_ctx.stream), "H2D sync");
+}
+int zkgpu_memcpy_d2h(void *dst, const void *src, uint64_t bytes)
+{
+    if (!bytes) return 0;
+    int rc = check_hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, g_ctx.stream), "D2H");
+    return rc ? rc : check_hip(hipStreamSynchronize(g_ctx.stream), "D2H sync");
+}
+int zkgpu_memcpy_d2d(void *dst, const void *src, uint64_t bytes)
+{
+    if (!bytes) return 0;
+    return check_hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, g_ctx.stream), "D2D");
+}
+int zkgpu_memset_dev(void *dst, int value, uint64_t bytes)
+{
+    if (!bytes) return 0;
+    return check_hip(hipMemsetAsync(dst, value, bytes, g_ctx.stream), "memset");
+}
+
+// ---------------------------------------------------------------- STARK stages
+// small host arrays staged through a grow-only device buffer (ws slot 3 is the
+// host-API staging area; stage params use their own allocation)
+static uint64_t *g_param = nullptr;
+static size_t g_param_bytes = 0;
+static char *param_buf(size_t bytes)
+{
+    if (bytes > g_param_bytes) {
+        (void)hipStreamSynchronize(g_ctx.stream);
+        if (g_param) (void)hipFree(g_param);
+        g_param = nullptr;
+        if (hipMalloc((void **)&g_param, bytes) != hipSuccess) {
+            g_param_bytes = 0;
+            return nullptr;
+        }
+        g_param_bytes = bytes;
+    }
+    return (char *)g_param;
+}
+
+int zkgpu_rand_cols_dev(uint64_t *base, uint64_t ld, const uint32_t *cols, uint32_t ncols, uint64_t nrows,
+                        uint64_t seed, uint64_t stream)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!ncols) return 0;
+    char *p = param_buf(ncols * 4);
+    if (!p) return set_error(ZKGPU_ERR_OOM, "param buffer");
+    if ((rc = check_hip(hipMemcpyAsync(p, cols, ncols * 4, hipMemcpyHostToDevice, g_ctx.stream), "H2D"))) return rc;
+    return rand_cols(base, ld, (const uint32_t *)p, ncols, nrows, seed, stream, g_ctx.stream);
+}
+
+int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd, uint32_t n_tmp1,
+                       uint32_t n_tmp3, const zkgpu_sections *sections, uint32_t log_dom, const uint64_t *challenges,
+                       const uint64_t *publics, uint32_t n_publics, const uint64_t *evals, uint32_t n_evals,
+                       const uint64_t *xdiv, const uint64_t *xdivw, uint32_t extend_bits, uint64_t x_start)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (log_dom > TW_MAX_LOG) return set_error(ZKGPU_ERR_ARG, "zxp: domain too large");
+    // validate operands on the host (no out-of-range reads in the kernel)
+    const zxp_instr *in = (const zxp_instr *)instr;
+    const zxp_operand *op = (const zxp_operand *)opnd;
+    for (uint32_t k = 0; k < n_instr; k++)
+        if (in[k].dst >= n_opnd || in[k].a >= n_opnd || (in[k].op != ZXP_COPY && in[k].b >= n_opnd) || in[k].op > 3)
+            return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u out of range", k);
+    for (uint32_t k = 0; k < n_opnd; k++) {
+        const zxp_operand &o = op[k];
+        bool bad = false;
+        switch (o.kind) {
+        case ZXP_TMP1: bad = o.a >= n_tmp1; break;
+        case ZXP_TMP3: bad = o.a >= n_tmp3; break;
+        case ZXP_COL:
+        case ZXP_COL3: {
+            const uint32_t w = o.kind == ZXP_COL3 ? 3 : 1;
+            bad = o.a >= SEC_COUNT || !sections->sec[o.a] || (uint64_t)o.b + w > sections->ncols[o.a] ||
+                  sections->ld[o.a] < (1ULL << log_dom);
+            break;
+        }
+        case ZXP_CHAL: bad = o.a >= 8; break;
+        case ZXP_PUB: bad = o.a >= n_publics; break;
+        case ZXP_EVAL: bad = o.a >= n_evals; break;
+        case ZXP_XDIV: bad = !xdiv; break;
+        case ZXP_XDIVW: bad = !xdivw; break;
+        case ZXP_LIT:
+        case ZXP_X:
+        case ZXP_ZI: break;
+        default: bad = true;
+        }
+        if (bad) return set_error(ZKGPU_ERR_ARG, "zxp: operand %u (kind %u) invalid", k, o.kind);
+    }
+    const uint32_t n_logz = extend_bits;
+    const size_t zh = (size_t)1 << n_logz;
+    size_t off_instr = 0, off_opnd = off_instr + ((n_instr * 16 + 15) & ~15ULL);
+    size_t off_ch = off_opnd + ((n_opnd * 16 + 15) & ~15ULL);
+    size_t off_pub = off_ch + 8 * 24;
+    size_t off_ev = off_pub + ((n_publics * 8 + 15) & ~15ULL);
+    size_t off_zh = off_ev + ((n_evals * 24 + 15) & ~15ULL);
+    size_t total = off_zh + zh * 8 + 16;
+    char *p = param_buf(total);
+    if (!p) return set_error(ZKGPU_ERR_OOM, "param buffer");
+    // zhInv[j] = 1/(7^N * W[eb]^j - 1)  (zhInv.cpp:7-31), N = 2^(log_dom - eb)
+    uint64_t zhv[64];
+    if (zh > 64) return set_error(ZKGPU_ERR_ARG, "zxp: extend bits > 6");
+    {
+        uint64_t sn = h_pow(7, 1ULL << (log_dom - extend_bits));
+        uint64_t we = h_w(extend_bits), w = 1;
+        for (size_t j = 0; j < zh; j++) {
+            zhv[j] = h_inv((h_mul(sn, w) + HP - 1) % HP);
+            w = h_mul(w, we);
+        }
+    }
+    hipStream_t s = g_ctx.stream;
+    if ((rc = check_hip(hipMemcpyAsync(p + off_instr, instr, n_instr * 16, hipMemcpyHostToDevice, s), "H2D")) ||
+        (rc = check_hip(hipMemcpyAsync(p + off_opnd, opnd, n_opnd * 16, hipMemcpyHostToDevice, s), "H2D")) ||
+        (rc = check_hip(hipMemcpyAsync(p + off_ch, challenges, 8 * 24, hipMemcpyHostToDevice, s), "H2D")) ||
+        (n_publics &&
+         (rc = check_hip(hipMemcpyAsync(p + off_pub, publics, n_publics * 8, hipMemcpyHostToDevice, s), "H2D"))) ||
+        (n_evals && (rc = check_hip(hipMemcpyAsync(p + off_ev, evals, n_evals * 24, hipMemcpyHostToDevice, s), "H2D"))) ||
+        (rc = check_hip(hipMemcpyAsync(p + off_zh, zhv, zh * 8, hipMemcpyHostToDevice, s), "H2D")))
+        return rc;
+    ZxpLaunch L;
+    for (int k = 0; k < SEC_COUNT; k++) {
+        L.sec[k] = sections->sec[k];
+        L.ld[k] = sections->ld[k];
+    }
+    L.instr = (const zxp_instr *)(p + off_instr);
+    L.opnd = (const zxp_operand *)(p + off_opnd);
+    L.n_instr = n_instr;
+    L.n_tmp1 = n_tmp1;
+    L.n_tmp3 = n_tmp3;
+    L.logdom = log_dom;
+    L.challenges = (const uint64_t *)(p + off_ch);
+    L.publics = (const uint64_t *)(p + off_pub);
+    L.evals = (const uint64_t *)(p + off_ev);
+    L.xdiv = xdiv;
+    L.xdivw = xdivw;
+    L.zhinv = (const uint64_t *)(p + off_zh);
+    L.zhinv_mask = (uint32_t)(zh - 1);
+    L.x_start = x_start % HP;
+    // algorithmic bytes: every distinct column operand read once per row + written columns
+    double cols = 0;
+    for (uint32_t k = 0; k < n_opnd; k++)
+        if (op[k].kind == ZXP_COL) cols += 1;
+        else if (op[k].kind == ZXP_COL3) cols += 3;
+        else if (op[k].kind == ZXP_XDIV || op[k].kind == ZXP_XDIVW) cols += 3;
+    L.bytes = 8.0 * cols * (double)(1ULL << log_dom);
+    return zxp_eval(L, s);
+}
+
+int zkgpu_calculate_z_dev(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,
+                          uint64_t den_ld, uint64_t n, int *closes)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!n) return 0;
+    const uint64_t chunk = 256 * 16;
+    uint64_t nb = (n + chunk - 1) / chunk;
+    uint64_t *scr = workspace(2, (3 * n + 6 * nb + 8) * sizeof(uint64_t));
+    if (!scr) return ZKGPU_ERR_OOM;
+    uint32_t *ok = (uint32_t *)(scr + 3 * n + 6 * nb);
+    if ((rc = calculate_z(z, z_ld, num, num_ld, den, den_ld, n, scr, ok, g_ctx.stream))) return rc;
+    uint32_t okh = 0;
+    if ((rc = check_hip(hipMemcpyAsync(&okh, ok, 4, hipMemcpyDeviceToHost, g_ctx.stream), "D2H"))) return rc;
+    if ((rc = check_hip(hipStreamSynchronize(g_ctx.stream), "calculateZ sync"))) return rc;
+    if (closes) *closes = (int)okh;
+    return 0;
+}
+
+int zkgpu_evmap_dev(uint64_t *evals_out, const uint64_t *const *cols, const uint64_t *lds, const uint32_t *dims,
+                    const uint32_t *primes, uint32_t n_ev, const uint64_t *lev, const uint64_t *lpev, uint64_t l_ld,
+                    uint64_t n, uint32_t extend_bits)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!n_ev) return 0;
+    const size_t es = evmap_entry_size();
+    struct E {
+        const uint64_t *col;
+        uint64_t ld;
+        uint32_t dim, prime;
+    };
+    if (es != sizeof(E)) return set_error(ZKGPU_ERR_ARG, "evmap entry layout");
+    E *h = (E *)malloc(n_ev * sizeof(E));
+    for (uint32_t e = 0; e < n_ev; e++) h[e] = E{cols[e], lds[e], dims[e], primes[e]};
+    uint32_t nchunks = 256;
+    while (nchunks > 1 && (n / nchunks) < 4096) nchunks >>= 1;
+    size_t off_part = ((n_ev * sizeof(E) + 15) & ~15ULL);
+    size_t off_ev = off_part + (size_t)n_ev * nchunks * 24;
+    char *p = param_buf(off_ev + n_ev * 24);
+    if (!p) {
+        free(h);
+        return set_error(ZKGPU_ERR_OOM, "param buffer");
+    }
+    rc = check_hip(hipMemcpyAsync(p, h, n_ev * sizeof(E), hipMemcpyHostToDevice, g_ctx.stream), "H2D");
+    free(h);
+    if (rc) return rc;
+    if ((rc = evmap((uint64_t *)(p + off_ev), p, n_ev, lev, lpev, l_ld, n, extend_bits, (uint64_t *)(p + off_part),
+                    nchunks, g_ctx.stream)))
+        return rc;
+    if ((rc = check_hip(hipMemcpyAsync(evals_out, p + off_ev, n_ev * 24, hipMemcpyDeviceToHost, g_ctx.stream), "D2H")))
+        return rc;
+    return check_hip(hipStreamSynchronize(g_ctx.stream), "evmap sync");
+}
+
+int zkgpu_xdivxsub_dev(uint64_t *xdiv, uint64_t *xdivw, const uint64_t xi[3], uint32_t n_bits, uint32_t n_bits_ext)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (n_bits_ext > TW_MAX_LOG || n_bits > n_bits_ext) return set_error(ZKGPU_ERR_ARG, "xdivxsub: bits");
+    return xdivxsub(xdiv, xdivw, xi, h_w(n_bits), n_bits_ext, g_ctx.stream);
+}
+
+int zkgpu_ext_powers_dev(uint64_t *out, uint64_t ld, const uint64_t base[3], uint64_t n)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!n) return 0;
+    return ext_powers(out, ld, base, n, g_ctx.stream);
+}
+
+int zkgpu_qsplit_dev(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t q_deg,
+                     uint64_t shift_in)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!n) return 0;
+    return qsplit(qq2, ld2, qq1, ld1, n, q_deg, shift_in, g_ctx.stream);
+}
+
+int zkgpu_cols3_to_interleaved_dev(uint64_t *out, const uint64_t *cols, uint64_t ld, uint64_t n)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!n) return 0;
+    return cols3_to_interleaved(out, cols, ld, n, g_ctx.stream);
+}
+
+int zkgpu_gl_merkle_open_rows_dev(uint64_t *vals_out, uint64_t *sibs_out, const uint64_t *nodes, const uint64_t *src,
+                                  uint64_t ncols, uint64_t nrows, const uint64_t *idx, uint64_t nq)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!nq) return 0;
+    Ctx &c = g_ctx;
+    uint32_t nlev = log2u(nrows);
+    for (uint64_t q = 0; q < nq; q++)
+        if (idx[q] >= nrows) return set_error(ZKGPU_ERR_ARG, "merkle_open: index out of range");
+    size_t nv = nq * ncols, ns = nq * nlev * 4;
+    uint64_t *d = workspace(2, (nq + nv + ns + 1) * sizeof(uint64_t));
+    if (!d) return ZKGPU_ERR_OOM;
+    uint64_t *didx = d, *dv = d + nq, *ds = d + nq + nv;
+    if ((rc = check_hip(hipMemcpyAsync(didx, idx, nq * 8, hipMemcpyHostToDevice, c.stream), "H2D"))) return rc;
+    if ((rc = merkle_open_strided(dv, ds, nodes, src, ncols, nrows, ncols, 1, didx, nq, c.stream))) return rc;
+    if (nv && (rc = check_hip(hipMemcpyAsync(vals_out, dv, nv * 8, hipMemcpyDeviceToHost, c.stream), "D2H"))) return rc;
+    if (ns && (rc = check_hip(hipMemcpyAsync(sibs_out, ds, ns * 8, hipMemcpyDeviceToHost, c.stream), "D2H"))) return rc;
+    return check_hip(hipStreamSynchronize(c.stream), "merkle_open_rows sync");
+}
+
 // ---------------------------------------------------------------- FRI
 int zkgpu_fri_fold_dev(uint64_t *out, const uint64_t *pol, uint32_t pol_bits, uint32_t out_bits,
                        const uint64_t special_x[3], uint64_t shift_inv)

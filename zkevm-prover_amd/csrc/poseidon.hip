@@ -172,15 +172,16 @@ __global__ void __launch_bounds__(256) k_merkle_level(uint64_t *dst, const uint6
     for (int k = 0; k < 4; k++) dst[4 * i + k] = gl_canon(st[k]);
 }
 
-// openings: vals[q*ncols + c] = src[c*ld + idx[q]]; sibs[q][l][0..3]
+// openings: vals[q*ncols + c] = src[row*row_stride + c*col_stride]; sibs[q][l][0..3]
 __global__ void k_merkle_open(uint64_t *vals, uint64_t *sibs, const uint64_t *nodes, const uint64_t *src,
-                              uint64_t ncols, uint64_t nrows, uint64_t ld, const uint64_t *idx, uint64_t nq,
-                              uint32_t nlevels)
+                              uint64_t ncols, uint64_t nrows, uint64_t row_stride, uint64_t col_stride,
+                              const uint64_t *idx, uint64_t nq, uint32_t nlevels)
 {
     uint64_t q = blockIdx.x;
     if (q >= nq) return;
     uint64_t row = idx[q];
-    for (uint64_t c = threadIdx.x; c < ncols; c += blockDim.x) vals[q * ncols + c] = src[c * ld + row];
+    for (uint64_t c = threadIdx.x; c < ncols; c += blockDim.x)
+        vals[q * ncols + c] = src[row * row_stride + c * col_stride];
     if (threadIdx.x == 0) {
         uint64_t off = 0, pending = nrows, id = row;
         for (uint32_t l = 0; l < nlevels; l++) {
@@ -242,15 +243,22 @@ int merkle_levels(uint64_t *nodes, uint64_t nrows, hipStream_t s)
     return check_launch("k_merkle_level");
 }
 
-int merkle_open_cols(uint64_t *vals, uint64_t *sibs, const uint64_t *nodes, const uint64_t *src, uint64_t ncols,
-                     uint64_t nrows, uint64_t ld, const uint64_t *idx, uint64_t nq, hipStream_t s)
+int merkle_open_strided(uint64_t *vals, uint64_t *sibs, const uint64_t *nodes, const uint64_t *src, uint64_t ncols,
+                        uint64_t nrows, uint64_t row_stride, uint64_t col_stride, const uint64_t *idx, uint64_t nq,
+                        hipStream_t s)
 {
     if (!nq) return 0;
     uint32_t nlevels = 0;
     while ((1ULL << nlevels) < nrows) nlevels++;
-    hipLaunchKernelGGL(k_merkle_open, dim3((uint32_t)nq), dim3(64), 0, s, vals, sibs, nodes, src, ncols, nrows, ld,
-                       idx, nq, nlevels);
+    hipLaunchKernelGGL(k_merkle_open, dim3((uint32_t)nq), dim3(64), 0, s, vals, sibs, nodes, src, ncols, nrows,
+                       row_stride, col_stride, idx, nq, nlevels);
     return check_launch("k_merkle_open");
+}
+
+int merkle_open_cols(uint64_t *vals, uint64_t *sibs, const uint64_t *nodes, const uint64_t *src, uint64_t ncols,
+                     uint64_t nrows, uint64_t ld, const uint64_t *idx, uint64_t nq, hipStream_t s)
+{
+    return merkle_open_strided(vals, sibs, nodes, src, ncols, nrows, 1, ld, idx, nq, s);
 }
 
 }  // namespace zk

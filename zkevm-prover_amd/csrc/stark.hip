@@ -1,0 +1,630 @@
+// STARK stage kernels for gfx950: expression programs, grand products,
+// evaluations at xi, FRI-polynomial helpers, quotient split.
+//
+//   k_zxp_eval      Steps::step2prev / step3prev / step42ns / step52ns
+//                   (steps.hpp:21-58; op semantics of
+//                   zkevm.chelpers.step42ns.parser.cpp:24-784, step52ns.parser.cpp:9-226)
+//                   as a uniform-control-flow interpreter: one thread per row,
+//                   instructions and operand descriptors are wave-uniform
+//                   (scalar loads, scalar branches), temporaries live in LDS
+//                   slot-major (conflict-free), sections are column-major.
+//   calculateZ      Polinomial::calculateZ (polinomial.hpp:586-607): per-row
+//                   ratio num/den (chunked Montgomery batch inversion), then a
+//                   3-phase parallel exclusive prefix product in F_p^3.
+//   k_evmap         Starks::evmap (starks.cpp:556-669): sum_k L(k) pol[k << eb]
+//   k_xdivxsub      starks.cpp:344-366
+//   k_ext_powers    LEv / LpEv power sequences (starks.cpp:308-324)
+//   k_qsplit        quotient split (starks.cpp:264-281)
+// F_p^3 arithmetic is associative/commutative and exact, so any reduction
+// order gives the reference's values bit for bit.
+#include "gl_device.hpp"
+#include "zkgpu_internal.hpp"
+#include "../../include/zkgpu_zxp.h"
+
+namespace zk {
+
+// ---------------------------------------------------------------- F_p^3 inverse
+// a * b = 1 with M(a) b = e0, M(a) = [[a0, a2, a1], [a1, a0+a2, a1+a2], [a2, a1, a0+a2]]
+// (x^3 = x + 1); b = first column of adj(M) / det(M).
+template <int K>
+__device__ __forceinline__ uint64_t sqr_n(uint64_t x)
+{
+#pragma unroll
+    for (int i = 0; i < K; i++) x = gl_sqr(x);
+    return x;
+}
+
+// a^(p-2), p - 2 = (2^31 - 1) * 2^33 + (2^32 - 1): 64 squarings + 9 multiplications
+__device__ __forceinline__ uint64_t gl_inv_base(uint64_t x)
+{
+    uint64_t t2 = gl_mul(gl_sqr(x), x);          // 2^2 - 1
+    uint64_t t3 = gl_mul(gl_sqr(t2), x);         // 2^3 - 1
+    uint64_t t6 = gl_mul(sqr_n<3>(t3), t3);      // 2^6 - 1
+    uint64_t t12 = gl_mul(sqr_n<6>(t6), t6);     // 2^12 - 1
+    uint64_t t24 = gl_mul(sqr_n<12>(t12), t12);  // 2^24 - 1
+    uint64_t t30 = gl_mul(sqr_n<6>(t24), t6);    // 2^30 - 1
+    uint64_t t31 = gl_mul(gl_sqr(t30), x);       // 2^31 - 1
+    uint64_t t32 = gl_mul(gl_sqr(t31), x);       // 2^32 - 1
+    return gl_mul(sqr_n<33>(t31), t32);
+}
+
+__device__ __forceinline__ gl3 gl3_inv(const gl3 &a)
+{
+    uint64_t a0 = a.v[0], a1 = a.v[1], a2 = a.v[2];
+    uint64_t s02 = gl_add(a0, a2), s12 = gl_add(a1, a2);
+    uint64_t c0 = gl_sub(gl_mul(s02, s02), gl_mul(s12, a1));
+    uint64_t c1 = gl_sub(gl_mul(s12, a2), gl_mul(a1, s02));
+    uint64_t c2 = gl_sub(gl_mul(a1, a1), gl_mul(s02, a2));
+    uint64_t det = gl_add(gl_add(gl_mul(a0, c0), gl_mul(a2, c1)), gl_mul(a1, c2));
+    uint64_t di = gl_inv_base(det);
+    return gl3{{gl_mul(c0, di), gl_mul(c1, di), gl_mul(c2, di)}};
+}
+
+__device__ __forceinline__ gl3 ld3(const uint64_t *p0, uint64_t ld)
+{
+    return gl3{{p0[0], p0[ld], p0[2 * ld]}};
+}
+
+__device__ __forceinline__ void st3(uint64_t *p0, uint64_t ld, const gl3 &v)
+{
+    p0[0] = gl_canon(v.v[0]);
+    p0[ld] = gl_canon(v.v[1]);
+    p0[2 * ld] = gl_canon(v.v[2]);
+}
+
+// ---------------------------------------------------------------- PRNG columns
+__device__ __forceinline__ uint64_t rand_u64(uint64_t seed, uint64_t stream, uint64_t col, uint64_t row)
+{
+    uint64_t x = seed ^ (stream << 56) ^ (col * 0x9E3779B97F4A7C15ULL) ^ (row * 0xC2B2AE3D27D4EB4FULL);
+    uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    return z >> 1;
+}
+
+__global__ void k_rand_cols(uint64_t *base, uint64_t ld, const uint32_t *cols, uint32_t ncols, uint64_t nrows,
+                            uint64_t seed, uint64_t stream)
+{
+    uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t k = blockIdx.y;
+    if (r >= nrows || k >= ncols) return;
+    uint32_t c = cols[k];
+    base[(uint64_t)c * ld + r] = rand_u64(seed, stream, c, r);
+}
+
+// ---------------------------------------------------------------- ZXP interpreter
+struct ZxpEnv {
+    uint64_t *sec[SEC_COUNT];
+    uint64_t ld[SEC_COUNT];
+    const zxp_instr *instr;
+    const zxp_operand *opnd;
+    uint32_t n_instr;
+    uint32_t n_slots;  // LDS slots per thread (tmp1 + 3*tmp3)
+    uint32_t tmp3_base;
+    uint32_t logdom;
+    const uint64_t *challenges;  // device, 3 per challenge
+    const uint64_t *publics;
+    const uint64_t *evals;
+    const uint64_t *xdiv;  // dom x 3 interleaved
+    const uint64_t *xdivw;
+    const uint64_t *zhinv;  // 2^eb entries
+    uint32_t zhinv_mask;
+    uint64_t x_start;     // x_i = x_start * omega_dom^i
+    const uint64_t *tw_lo;  // forward big twiddles (omega_2^28)
+    const uint64_t *tw_hi;
+};
+
+constexpr int ZXP_THREADS = 64;
+
+struct Val {
+    gl3 v;
+    int dim;
+};
+
+__device__ __forceinline__ Val zxp_load(const ZxpEnv &e, const zxp_operand &o, const uint64_t *lds, int lane,
+                                        uint64_t i)
+{
+    Val r;
+    r.dim = 1;
+    r.v.v[1] = r.v.v[2] = 0;
+    switch (o.kind) {
+    case ZXP_TMP1: r.v.v[0] = lds[o.a * ZXP_THREADS + lane]; break;
+    case ZXP_TMP3: {
+        const uint64_t *p = lds + (e.tmp3_base + 3 * o.a) * ZXP_THREADS + lane;
+        r.v = gl3{{p[0], p[ZXP_THREADS], p[2 * ZXP_THREADS]}};
+        r.dim = 3;
+        break;
+    }
+    case ZXP_COL:
+    case ZXP_COL3: {
+        const uint64_t dom_mask = (1ULL << e.logdom) - 1;
+        const uint64_t row = (i + (uint64_t)(int64_t)(int32_t)o.c) & dom_mask;
+        const uint64_t ld = e.ld[o.a];
+        const uint64_t *p = e.sec[o.a] + (uint64_t)o.b * ld + row;
+        r.v.v[0] = p[0];
+        if (o.kind == ZXP_COL3) {
+            r.v.v[1] = p[ld];
+            r.v.v[2] = p[2 * ld];
+            r.dim = 3;
+        }
+        break;
+    }
+    case ZXP_LIT: r.v.v[0] = (uint64_t)o.a | ((uint64_t)o.b << 32); break;
+    case ZXP_CHAL: r.v = gl3{{e.challenges[3 * o.a], e.challenges[3 * o.a + 1], e.challenges[3 * o.a + 2]}}; r.dim = 3; break;
+    case ZXP_PUB: r.v.v[0] = e.publics[o.a]; break;
+    case ZXP_X: {
+        uint64_t ex = i << (TW_MAX_LOG - e.logdom);
+        r.v.v[0] = gl_mul(e.x_start, gl_mul(e.tw_lo[ex & (TW_LEVEL_SIZE - 1)], e.tw_hi[ex >> TW_LEVEL_BITS]));
+        break;
+    }
+    case ZXP_EVAL: r.v = gl3{{e.evals[3 * o.a], e.evals[3 * o.a + 1], e.evals[3 * o.a + 2]}}; r.dim = 3; break;
+    case ZXP_XDIV: r.v = gl3{{e.xdiv[3 * i], e.xdiv[3 * i + 1], e.xdiv[3 * i + 2]}}; r.dim = 3; break;
+    case ZXP_XDIVW: r.v = gl3{{e.xdivw[3 * i], e.xdivw[3 * i + 1], e.xdivw[3 * i + 2]}}; r.dim = 3; break;
+    case ZXP_ZI: r.v.v[0] = e.zhinv[i & e.zhinv_mask]; break;
+    default: break;
+    }
+    return r;
+}
+
+__global__ void __launch_bounds__(ZXP_THREADS) k_zxp_eval(ZxpEnv e)
+{
+    extern __shared__ __attribute__((aligned(16))) uint64_t zlds[];
+    const int lane = threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * ZXP_THREADS + lane;  // dom is a multiple of 64 or padded
+    const uint64_t dom = 1ULL << e.logdom;
+    const bool active = i < dom;
+    for (uint32_t k = 0; k < e.n_instr; k++) {
+        const zxp_instr in = e.instr[k];
+        const zxp_operand oa = e.opnd[in.a];
+        Val a = zxp_load(e, oa, zlds, lane, active ? i : 0);
+        Val r;
+        if (in.op == ZXP_COPY) {
+            r = a;
+        } else {
+            const zxp_operand ob = e.opnd[in.b];
+            Val b = zxp_load(e, ob, zlds, lane, active ? i : 0);
+            r.dim = (a.dim == 3 || b.dim == 3) ? 3 : 1;
+            if (in.op == ZXP_MUL) {
+                if (a.dim == 3 && b.dim == 3)
+                    r.v = gl3_mul(a.v, b.v);
+                else if (a.dim == 3)
+                    r.v = gl3_mul1(a.v, b.v.v[0]);
+                else if (b.dim == 3)
+                    r.v = gl3_mul1(b.v, a.v.v[0]);
+                else
+                    r.v = gl3{{gl_mul(a.v.v[0], b.v.v[0]), 0, 0}};
+            } else if (in.op == ZXP_ADD) {
+                r.v = gl3_add(a.v, b.v);  // base operands carry zeros in components 1, 2
+            } else {
+                r.v = gl3_sub(a.v, b.v);
+            }
+        }
+        const zxp_operand od = e.opnd[in.dst];
+        switch (od.kind) {
+        case ZXP_TMP1: zlds[od.a * ZXP_THREADS + lane] = r.v.v[0]; break;
+        case ZXP_TMP3: {
+            uint64_t *p = zlds + (e.tmp3_base + 3 * od.a) * ZXP_THREADS + lane;
+            p[0] = r.v.v[0];
+            p[ZXP_THREADS] = r.dim == 3 ? r.v.v[1] : 0;
+            p[2 * ZXP_THREADS] = r.dim == 3 ? r.v.v[2] : 0;
+            break;
+        }
+        case ZXP_COL:
+        case ZXP_COL3:
+            if (active) {
+                const uint64_t ld = e.ld[od.a];
+                uint64_t *p = e.sec[od.a] + (uint64_t)od.b * ld + i;
+                p[0] = gl_canon(r.v.v[0]);
+                if (od.kind == ZXP_COL3) {
+                    p[ld] = r.dim == 3 ? gl_canon(r.v.v[1]) : 0;
+                    p[2 * ld] = r.dim == 3 ? gl_canon(r.v.v[2]) : 0;
+                }
+            }
+            break;
+        default: break;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- calculateZ
+// ratio[i] = num[i] / den[i]; each thread inverts CH strided elements with one
+// F_p^3 inversion (Montgomery's trick).
+constexpr int BI_CHUNK = 16;
+
+__global__ void __launch_bounds__(256) k_ratio(uint64_t *ratio, const uint64_t *num, uint64_t num_ld,
+                                               const uint64_t *den, uint64_t den_ld, uint64_t n)
+{
+    const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    gl3 pre[BI_CHUNK];
+    gl3 acc{{1, 0, 0}};
+#pragma unroll
+    for (int j = 0; j < BI_CHUNK; j++) {
+        uint64_t k = t + j * T;
+        gl3 d = k < n ? ld3(den + k, den_ld) : gl3{{1, 0, 0}};
+        acc = j ? gl3_mul(acc, d) : d;
+        pre[j] = acc;
+    }
+    gl3 inv = gl3_inv(acc);
+#pragma unroll
+    for (int j = BI_CHUNK - 1; j >= 0; j--) {
+        uint64_t k = t + j * T;
+        gl3 dinv = j ? gl3_mul(inv, pre[j - 1]) : inv;
+        if (k < n) {
+            gl3 d = ld3(den + k, den_ld);
+            gl3 r = gl3_mul(ld3(num + k, num_ld), dinv);
+            uint64_t *o = ratio + 3 * k;
+            o[0] = r.v[0];
+            o[1] = r.v[1];
+            o[2] = r.v[2];
+            inv = gl3_mul(inv, d);
+        }
+    }
+}
+
+// scan phase 1: each block reduces its contiguous chunk of the ratio array
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_PER_THREAD = 16;
+constexpr uint64_t SCAN_CHUNK = SCAN_THREADS * SCAN_PER_THREAD;
+
+__device__ gl3 block_exclusive_scan3(gl3 v, gl3 *sh, gl3 *total)
+{
+    // Hillis-Steele inclusive scan over 256 threads in LDS, then shift
+    const int t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int off = 1; off < SCAN_THREADS; off <<= 1) {
+        gl3 x = sh[t];
+        gl3 y = t >= off ? sh[t - off] : gl3{{1, 0, 0}};
+        __syncthreads();
+        sh[t] = t >= off ? gl3_mul(x, y) : x;
+        __syncthreads();
+    }
+    gl3 incl = sh[t];
+    gl3 excl = t ? sh[t - 1] : gl3{{1, 0, 0}};
+    *total = sh[SCAN_THREADS - 1];
+    __syncthreads();
+    (void)incl;
+    return excl;
+}
+
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_reduce(uint64_t *block_tot, const uint64_t *ratio, uint64_t n)
+{
+    __shared__ gl3 sh[SCAN_THREADS];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_CHUNK + (uint64_t)threadIdx.x * SCAN_PER_THREAD;
+    gl3 acc{{1, 0, 0}};
+    for (int j = 0; j < SCAN_PER_THREAD; j++) {
+        uint64_t k = base + j;
+        if (k < n) acc = gl3_mul(acc, gl3{{ratio[3 * k], ratio[3 * k + 1], ratio[3 * k + 2]}});
+    }
+    gl3 tot;
+    block_exclusive_scan3(acc, sh, &tot);
+    if (threadIdx.x == 0) {
+        block_tot[3 * blockIdx.x] = tot.v[0];
+        block_tot[3 * blockIdx.x + 1] = tot.v[1];
+        block_tot[3 * blockIdx.x + 2] = tot.v[2];
+    }
+}
+
+// scan phase 2: exclusive scan of the block totals (single block, sequential chunks)
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_totals(uint64_t *block_pre, const uint64_t *block_tot,
+                                                              uint64_t nblocks)
+{
+    __shared__ gl3 sh[SCAN_THREADS];
+    gl3 carry{{1, 0, 0}};
+    for (uint64_t b0 = 0; b0 < nblocks; b0 += SCAN_THREADS) {
+        uint64_t b = b0 + threadIdx.x;
+        gl3 v = b < nblocks ? gl3{{block_tot[3 * b], block_tot[3 * b + 1], block_tot[3 * b + 2]}} : gl3{{1, 0, 0}};
+        gl3 tot;
+        gl3 ex = block_exclusive_scan3(v, sh, &tot);
+        if (b < nblocks) {
+            gl3 r = gl3_mul(carry, ex);
+            block_pre[3 * b] = r.v[0];
+            block_pre[3 * b + 1] = r.v[1];
+            block_pre[3 * b + 2] = r.v[2];
+        }
+        carry = gl3_mul(carry, tot);
+    }
+}
+
+// scan phase 3: z[k] = block_pre * exclusive product within the block
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_apply(uint64_t *z, uint64_t z_ld, const uint64_t *ratio,
+                                                             const uint64_t *block_pre, uint64_t n)
+{
+    __shared__ gl3 sh[SCAN_THREADS];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_CHUNK + (uint64_t)threadIdx.x * SCAN_PER_THREAD;
+    gl3 acc{{1, 0, 0}};
+    gl3 loc[SCAN_PER_THREAD];
+#pragma unroll
+    for (int j = 0; j < SCAN_PER_THREAD; j++) {
+        uint64_t k = base + j;
+        loc[j] = k < n ? gl3{{ratio[3 * k], ratio[3 * k + 1], ratio[3 * k + 2]}} : gl3{{1, 0, 0}};
+        acc = gl3_mul(acc, loc[j]);
+    }
+    gl3 tot;
+    gl3 ex = block_exclusive_scan3(acc, sh, &tot);
+    gl3 run = gl3_mul(gl3{{block_pre[3 * blockIdx.x], block_pre[3 * blockIdx.x + 1], block_pre[3 * blockIdx.x + 2]}},
+                      ex);
+#pragma unroll
+    for (int j = 0; j < SCAN_PER_THREAD; j++) {
+        uint64_t k = base + j;
+        if (k < n) st3(z + k, z_ld, run);  // exclusive: z[k] = prod_{i<k} ratio[i]
+        run = gl3_mul(run, loc[j]);
+    }
+}
+
+// check value: z[n-1] * ratio[n-1] must be 1 (calculateZ zkassert)
+__global__ void k_z_check(uint32_t *ok, const uint64_t *z, uint64_t z_ld, const uint64_t *ratio, uint64_t n)
+{
+    gl3 zl = ld3(z + (n - 1), z_ld);
+    gl3 r{{ratio[3 * (n - 1)], ratio[3 * (n - 1) + 1], ratio[3 * (n - 1) + 2]}};
+    gl3 c = gl3_canon(gl3_mul(zl, r));
+    *ok = (c.v[0] == 1 && c.v[1] == 0 && c.v[2] == 0) ? 1u : 0u;
+}
+
+// ---------------------------------------------------------------- evmap
+struct EvEntry {
+    const uint64_t *col;  // first column of the polynomial (2ns section, column-major)
+    uint64_t ld;
+    uint32_t dim;
+    uint32_t prime;
+};
+
+constexpr int EV_THREADS = 256;
+
+// partial[e][blk] = sum over the block's rows k of L(k) * pol_e[k << eb]
+__global__ void __launch_bounds__(EV_THREADS) k_evmap(uint64_t *partial, const EvEntry *ents, uint32_t n_ev,
+                                                     const uint64_t *lev, const uint64_t *lpev, uint64_t l_ld,
+                                                     uint64_t n, uint32_t eb, uint64_t rows_per_block)
+{
+    __shared__ gl3 sh[EV_THREADS];
+    const uint32_t e = blockIdx.x;  // entry fastest: a chunk's L rows are reused from L2 by all entries
+    const uint64_t blk = blockIdx.y;
+    const EvEntry en = ents[e];
+    const uint64_t *L = en.prime ? lpev : lev;
+    gl3 acc{{0, 0, 0}};
+    const uint64_t r0 = blk * rows_per_block;
+    uint64_t r1 = r0 + rows_per_block;
+    if (r1 > n) r1 = n;
+    for (uint64_t k = r0 + threadIdx.x; k < r1; k += EV_THREADS) {
+        gl3 l = ld3(L + k, l_ld);
+        const uint64_t row = k << eb;
+        if (en.dim == 1)
+            acc = gl3_add(acc, gl3_mul1(l, en.col[row]));
+        else
+            acc = gl3_add(acc, gl3_mul(l, ld3(en.col + row, en.ld)));
+    }
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = EV_THREADS / 2; off > 0; off >>= 1) {
+        if (threadIdx.x < off) sh[threadIdx.x] = gl3_add(sh[threadIdx.x], sh[threadIdx.x + off]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        uint64_t *o = partial + 3 * ((uint64_t)e * gridDim.y + blk);
+        o[0] = sh[0].v[0];
+        o[1] = sh[0].v[1];
+        o[2] = sh[0].v[2];
+    }
+}
+
+__global__ void k_evmap_sum(uint64_t *evals, const uint64_t *partial, uint32_t n_ev, uint32_t nblk)
+{
+    uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_ev) return;
+    gl3 acc{{0, 0, 0}};
+    for (uint32_t b = 0; b < nblk; b++) {
+        const uint64_t *p = partial + 3 * ((uint64_t)e * nblk + b);
+        acc = gl3_add(acc, gl3{{p[0], p[1], p[2]}});
+    }
+    acc = gl3_canon(acc);
+    evals[3 * e] = acc.v[0];
+    evals[3 * e + 1] = acc.v[1];
+    evals[3 * e + 2] = acc.v[2];
+}
+
+// ---------------------------------------------------------------- xDivXSub
+// xdiv[k] = x_k / (x_k - xi), xdivw[k] = x_k / (x_k - w xi), x_k = 7 * omega_2n^k
+__global__ void __launch_bounds__(256) k_xdivxsub(uint64_t *xdiv, uint64_t *xdivw, gl3 xi, gl3 wxi, uint32_t logn,
+                                                  const uint64_t *tw_lo, const uint64_t *tw_hi)
+{
+    const uint64_t n = 1ULL << logn;
+    const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int which = 0; which < 2; which++) {
+        const gl3 s = which ? wxi : xi;
+        uint64_t *out = which ? xdivw : xdiv;
+        gl3 pre[BI_CHUNK];
+        uint64_t xs[BI_CHUNK];
+        gl3 acc{{1, 0, 0}};
+#pragma unroll
+        for (int j = 0; j < BI_CHUNK; j++) {
+            uint64_t k = t + j * T;
+            uint64_t ex = (k & (n - 1)) << (TW_MAX_LOG - logn);
+            xs[j] = gl_mul(7, gl_mul(tw_lo[ex & (TW_LEVEL_SIZE - 1)], tw_hi[ex >> TW_LEVEL_BITS]));
+            gl3 d = k < n ? gl3{{gl_sub(xs[j], s.v[0]), gl_neg(s.v[1]), gl_neg(s.v[2])}} : gl3{{1, 0, 0}};
+            acc = j ? gl3_mul(acc, d) : d;
+            pre[j] = acc;
+        }
+        gl3 inv = gl3_inv(acc);
+#pragma unroll
+        for (int j = BI_CHUNK - 1; j >= 0; j--) {
+            uint64_t k = t + j * T;
+            gl3 dinv = j ? gl3_mul(inv, pre[j - 1]) : inv;
+            if (k < n) {
+                gl3 d{{gl_sub(xs[j], s.v[0]), gl_neg(s.v[1]), gl_neg(s.v[2])}};
+                gl3 r = gl3_canon(gl3_mul1(dinv, xs[j]));
+                out[3 * k] = r.v[0];
+                out[3 * k + 1] = r.v[1];
+                out[3 * k + 2] = r.v[2];
+                inv = gl3_mul(inv, d);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- powers & split
+// out column-major (3 columns, ld): out[k] = base^k, k < n
+__global__ void k_ext_powers(uint64_t *out, uint64_t ld, gl3 base, uint64_t n, uint32_t per_thread)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t k0 = t * per_thread;
+    if (k0 >= n) return;
+    // base^k0 by square-and-multiply
+    gl3 r{{1, 0, 0}}, b = base;
+    uint64_t e = k0;
+    while (e) {
+        if (e & 1) r = gl3_mul(r, b);
+        b = gl3_mul(b, b);
+        e >>= 1;
+    }
+    for (uint32_t j = 0; j < per_thread && k0 + j < n; j++) {
+        st3(out + k0 + j, ld, r);
+        r = gl3_mul(r, base);
+    }
+}
+
+// qq2 column 3p+d, row k < N: qq1_d[p N + k] * shiftIn^p   (starks.cpp:266-281)
+__global__ void k_qsplit(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t qdeg,
+                         uint64_t shift_in)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    uint64_t f = 1;
+    for (uint32_t p = 0; p < qdeg; p++) {
+        for (int d = 0; d < 3; d++)
+            qq2[(uint64_t)(3 * p + d) * ld2 + k] = gl_canon(gl_mul(qq1[(uint64_t)d * ld1 + (uint64_t)p * n + k], f));
+        f = gl_mul(f, shift_in);
+    }
+}
+
+// interleave 3 column-major ext columns into an interleaved (n x 3) array
+__global__ void k_cols3_to_interleaved(uint64_t *out, const uint64_t *cols, uint64_t ld, uint64_t n)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    out[3 * k] = cols[k];
+    out[3 * k + 1] = cols[ld + k];
+    out[3 * k + 2] = cols[2 * ld + k];
+}
+
+// ---------------------------------------------------------------- host side
+static inline uint32_t nblk(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
+
+int rand_cols(uint64_t *base, uint64_t ld, const uint32_t *cols_dev, uint32_t ncols, uint64_t nrows, uint64_t seed,
+              uint64_t stream, hipStream_t s)
+{
+    if (!ncols || !nrows) return 0;
+    hipLaunchKernelGGL(k_rand_cols, dim3(nblk(nrows, 256), ncols), dim3(256), 0, s, base, ld, cols_dev, ncols, nrows,
+                       seed, stream);
+    return check_launch("k_rand_cols");
+}
+
+int zxp_eval(const ZxpLaunch &L, hipStream_t s)
+{
+    Ctx &c = ctx();
+    ZxpEnv e;
+    for (int k = 0; k < SEC_COUNT; k++) {
+        e.sec[k] = L.sec[k];
+        e.ld[k] = L.ld[k];
+    }
+    e.instr = L.instr;
+    e.opnd = L.opnd;
+    e.n_instr = L.n_instr;
+    e.n_slots = L.n_tmp1 + 3 * L.n_tmp3;
+    e.tmp3_base = L.n_tmp1;
+    e.logdom = L.logdom;
+    e.challenges = L.challenges;
+    e.publics = L.publics;
+    e.evals = L.evals;
+    e.xdiv = L.xdiv;
+    e.xdivw = L.xdivw;
+    e.zhinv = L.zhinv;
+    e.zhinv_mask = L.zhinv_mask;
+    e.x_start = L.x_start;
+    e.tw_lo = c.tw_lo[0];
+    e.tw_hi = c.tw_hi[0];
+    size_t lds = (size_t)(e.n_slots ? e.n_slots : 1) * ZXP_THREADS * sizeof(uint64_t);
+    if (lds > 160 * 1024) return set_error(ZKGPU_ERR_ARG, "zxp: %u temp slots exceed LDS", e.n_slots);
+    uint64_t dom = 1ULL << L.logdom;
+    prof_begin(s);
+    hipLaunchKernelGGL(k_zxp_eval, dim3(nblk(dom, ZXP_THREADS)), dim3(ZXP_THREADS), lds, s, e);
+    prof_end("k_zxp_eval", L.bytes, s);
+    return check_launch("k_zxp_eval");
+}
+
+int calculate_z(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,
+                uint64_t den_ld, uint64_t n, uint64_t *scratch, uint32_t *ok_dev, hipStream_t s)
+{
+    // scratch: ratio (3n) + block totals + block prefixes
+    uint64_t *ratio = scratch;
+    uint64_t nb = (n + SCAN_CHUNK - 1) / SCAN_CHUNK;
+    uint64_t *tot = ratio + 3 * n;
+    uint64_t *pre = tot + 3 * nb;
+    uint64_t threads = (n + BI_CHUNK - 1) / BI_CHUNK;
+    uint32_t blocks = nblk(threads, 256);
+    prof_begin(s);
+    hipLaunchKernelGGL(k_ratio, dim3(blocks), dim3(256), 0, s, ratio, num, num_ld, den, den_ld, n);
+    prof_end("k_ratio", 8.0 * 9 * n, s);
+    hipLaunchKernelGGL(k_scan_reduce, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, tot, ratio, n);
+    hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(SCAN_THREADS), 0, s, pre, tot, nb);
+    prof_begin(s);
+    hipLaunchKernelGGL(k_scan_apply, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, z, z_ld, ratio, pre, n);
+    prof_end("k_scan_apply", 8.0 * 6 * n, s);
+    hipLaunchKernelGGL(k_z_check, dim3(1), dim3(1), 0, s, ok_dev, z, z_ld, ratio, n);
+    return check_launch("calculateZ");
+}
+
+int evmap(uint64_t *evals, const void *ents_dev, uint32_t n_ev, const uint64_t *lev, const uint64_t *lpev,
+          uint64_t l_ld, uint64_t n, uint32_t eb, uint64_t *partial, uint32_t nchunks, hipStream_t s)
+{
+    if (!n_ev) return 0;
+    uint64_t rows_per_block = (n + nchunks - 1) / nchunks;
+    prof_begin(s);
+    hipLaunchKernelGGL(k_evmap, dim3(n_ev, nchunks), dim3(EV_THREADS), 0, s, partial, (const EvEntry *)ents_dev, n_ev,
+                       lev, lpev, l_ld, n, eb, rows_per_block);
+    prof_end("k_evmap", 8.0 * n * n_ev * 2.0 + 24.0 * n * 2, s);
+    hipLaunchKernelGGL(k_evmap_sum, dim3(nblk(n_ev, 64)), dim3(64), 0, s, evals, partial, n_ev, nchunks);
+    return check_launch("k_evmap");
+}
+
+size_t evmap_entry_size() { return sizeof(EvEntry); }
+
+int xdivxsub(uint64_t *xdiv, uint64_t *xdivw, const uint64_t xi[3], uint64_t w, uint32_t logn, hipStream_t s)
+{
+    Ctx &c = ctx();
+    gl3 x{{xi[0] % ZK_P, xi[1] % ZK_P, xi[2] % ZK_P}};
+    gl3 wx{{h_mul(x.v[0], w), h_mul(x.v[1], w), h_mul(x.v[2], w)}};
+    uint64_t n = 1ULL << logn;
+    uint64_t threads = (n + BI_CHUNK - 1) / BI_CHUNK;
+    prof_begin(s);
+    hipLaunchKernelGGL(k_xdivxsub, dim3(nblk(threads, 256)), dim3(256), 0, s, xdiv, xdivw, x, wx, logn, c.tw_lo[0],
+                       c.tw_hi[0]);
+    prof_end("k_xdivxsub", 48.0 * n, s);
+    return check_launch("k_xdivxsub");
+}
+
+int ext_powers(uint64_t *out, uint64_t ld, const uint64_t base[3], uint64_t n, hipStream_t s)
+{
+    gl3 b{{base[0] % ZK_P, base[1] % ZK_P, base[2] % ZK_P}};
+    const uint32_t per = 64;
+    uint64_t threads = (n + per - 1) / per;
+    hipLaunchKernelGGL(k_ext_powers, dim3(nblk(threads, 256)), dim3(256), 0, s, out, ld, b, n, per);
+    return check_launch("k_ext_powers");
+}
+
+int qsplit(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t qdeg,
+           uint64_t shift_in, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_qsplit, dim3(nblk(n, 256)), dim3(256), 0, s, qq2, ld2, qq1, ld1, n, qdeg, shift_in);
+    return check_launch("k_qsplit");
+}
+
+int cols3_to_interleaved(uint64_t *out, const uint64_t *cols, uint64_t ld, uint64_t n, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_cols3_to_interleaved, dim3(nblk(n, 256)), dim3(256), 0, s, out, cols, ld, n);
+    return check_launch("k_cols3_to_interleaved");
+}
+
+}  // namespace zk

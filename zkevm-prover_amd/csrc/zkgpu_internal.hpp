@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "../../include/zkgpu.h"
+#include "../../include/zkgpu_zxp.h"
 
 namespace zk {
 
@@ -77,5 +78,37 @@ int merkle_open_cols(uint64_t *vals, uint64_t *sibs, const uint64_t *nodes, cons
 int fri_fold(uint64_t *out, const uint64_t *pol, uint32_t pol_bits, uint32_t out_bits, const uint64_t sx[3],
              uint64_t shift_inv, hipStream_t s);
 int fri_transpose(uint64_t *aux, const uint64_t *pol, uint64_t degree, uint32_t tbits, hipStream_t s);
+
+// ---- stark.hip
+struct ZxpLaunch {
+    uint64_t *sec[SEC_COUNT];
+    uint64_t ld[SEC_COUNT];
+    const zxp_instr *instr;  // device
+    const zxp_operand *opnd; // device
+    uint32_t n_instr, n_tmp1, n_tmp3;
+    uint32_t logdom;
+    const uint64_t *challenges, *publics, *evals;  // device
+    const uint64_t *xdiv, *xdivw;                  // device (2n domain) or null
+    const uint64_t *zhinv;                         // device, 2^eb entries
+    uint32_t zhinv_mask;
+    uint64_t x_start;
+    double bytes;  // algorithmic bytes for profiling
+};
+int rand_cols(uint64_t *base, uint64_t ld, const uint32_t *cols_dev, uint32_t ncols, uint64_t nrows, uint64_t seed,
+              uint64_t stream, hipStream_t s);
+int zxp_eval(const ZxpLaunch &L, hipStream_t s);
+int calculate_z(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,
+                uint64_t den_ld, uint64_t n, uint64_t *scratch, uint32_t *ok_dev, hipStream_t s);
+int evmap(uint64_t *evals, const void *ents_dev, uint32_t n_ev, const uint64_t *lev, const uint64_t *lpev,
+          uint64_t l_ld, uint64_t n, uint32_t eb, uint64_t *partial, uint32_t nchunks, hipStream_t s);
+size_t evmap_entry_size();
+int xdivxsub(uint64_t *xdiv, uint64_t *xdivw, const uint64_t xi[3], uint64_t w, uint32_t logn, hipStream_t s);
+int ext_powers(uint64_t *out, uint64_t ld, const uint64_t base[3], uint64_t n, hipStream_t s);
+int qsplit(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t qdeg,
+           uint64_t shift_in, hipStream_t s);
+int cols3_to_interleaved(uint64_t *out, const uint64_t *cols, uint64_t ld, uint64_t n, hipStream_t s);
+int merkle_open_strided(uint64_t *vals, uint64_t *sibs, const uint64_t *nodes, const uint64_t *src, uint64_t ncols,
+                        uint64_t nrows, uint64_t row_stride, uint64_t col_stride, const uint64_t *idx, uint64_t nq,
+                        hipStream_t s);
 
 }  // namespace zk

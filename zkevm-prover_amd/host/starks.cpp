@@ -1,0 +1,549 @@
+// libzkgpu_stark: the host-side STARK prover on top of the libzkgpu C-ABI.
+//
+// A C++ restatement of the reference's host orchestration -- Starks::genProof
+// (src/starkpil/starks.cpp:9-404), FRIProve::prove / queryPol
+// (src/starkpil/fri/friProve.cpp:5-232) and Transcript
+// (src/starkpil/transcript/transcript.cpp:4-87) -- in which every bulk
+// operation is a device-resident libzkgpu call on column-major sections kept
+// in HBM for the whole proof.  Only roots, evals, challenges, query openings
+// and the final polynomial cross PCIe.  Host arithmetic is limited to the
+// scalars the reference also computes on the host (challenge transforms,
+// shift powers, zhInv table size), done with the 128-bit helpers below.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "../../include/zkgpu.h"
+#include "../../include/zkgpu_stark.h"
+
+namespace zkgpu_host {
+
+static thread_local char g_err[512] = "";
+static int fail(const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return -1;
+}
+#define CK(x)                                                                                                  \
+    do {                                                                                                       \
+        int _rc = (x);                                                                                         \
+        if (_rc) return fail("%s: %s (%s:%d)", #x, zkgpu_last_error(), __FILE__, __LINE__);                   \
+    } while (0)
+
+static const uint64_t P = 0xFFFFFFFF00000001ULL;
+static uint64_t mul(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) % P); }
+static uint64_t pw(uint64_t a, uint64_t e)
+{
+    uint64_t r = 1;
+    a %= P;
+    while (e) {
+        if (e & 1) r = mul(r, a);
+        a = mul(a, a);
+        e >>= 1;
+    }
+    return r;
+}
+static uint64_t inv(uint64_t a) { return pw(a, P - 2); }
+static uint64_t w_of(uint32_t n)  // Goldilocks::w(n)
+{
+    uint64_t w = 7277203076849721926ULL;
+    for (uint32_t i = n; i < 32; i++) w = mul(w, w);
+    return w;
+}
+static uint64_t rand_u64(uint64_t seed, uint64_t stream, uint64_t col, uint64_t row)
+{
+    uint64_t x = seed ^ (stream << 56) ^ (col * 0x9E3779B97F4A7C15ULL) ^ (row * 0xC2B2AE3D27D4EB4FULL);
+    uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    return z >> 1;
+}
+
+// ---------------------------------------------------------------- transcript
+// Transcript (transcript.cpp:4-87); the permutation runs on the GPU
+// (PoseidonGoldilocks::hash_full_result -> zkgpu_gl_poseidon_full).
+class Transcript
+{
+public:
+    uint64_t state[4] = {0, 0, 0, 0};
+    uint64_t pending[8] = {0};
+    uint64_t out[12] = {0};
+    uint32_t pending_cursor = 0, out_cursor = 0;
+    int err = 0;
+
+    void absorb()
+    {
+        uint64_t in[12];
+        memcpy(in, pending, 64);
+        memcpy(in + 8, state, 32);
+        if (zkgpu_gl_poseidon_full(out, in)) err = -1;
+        out_cursor = 12;
+        memset(pending, 0, sizeof pending);
+        pending_cursor = 0;
+        memcpy(state, out, 32);
+    }
+    void put(const uint64_t *v, uint64_t n)
+    {
+        for (uint64_t i = 0; i < n; i++) {
+            pending[pending_cursor++] = v[i];
+            out_cursor = 0;
+            if (pending_cursor == 8) absorb();
+        }
+    }
+    uint64_t get_fields1()
+    {
+        if (out_cursor == 0) absorb();
+        uint64_t r = out[(12 - out_cursor) % 12];
+        out_cursor--;
+        return r;
+    }
+    void get_field(uint64_t o[3])
+    {
+        for (int i = 0; i < 3; i++) o[i] = get_fields1();
+    }
+    void get_permutations(uint64_t *res, uint64_t n, uint64_t nbits)
+    {
+        uint64_t nfields = (n * nbits - 1) / 63 + 1;
+        std::vector<uint64_t> f(nfields);
+        for (auto &x : f) x = get_fields1() % P;
+        uint64_t cf = 0, cb = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            uint64_t a = 0;
+            for (uint64_t j = 0; j < nbits; j++) {
+                if ((f[cf] >> cb) & 1) a |= 1ULL << j;
+                if (++cb == 63) {
+                    cb = 0;
+                    cf++;
+                }
+            }
+            res[i] = a;
+        }
+    }
+};
+
+// ---------------------------------------------------------------- prover
+struct Prog {
+    std::vector<zxp_instr> instr;
+    std::vector<zxp_operand> opnd;
+    uint32_t n_tmp1 = 0, n_tmp3 = 0;
+    void set(const zkgpu_zxp_prog &p)
+    {
+        instr.assign(p.instr, p.instr + p.n_instr);
+        opnd.assign(p.opnd, p.opnd + p.n_opnd);
+        n_tmp1 = p.n_tmp1;
+        n_tmp3 = p.n_tmp3;
+    }
+};
+
+class Starks
+{
+public:
+    zkgpu_stark_info info;
+    std::vector<uint32_t> random_cols, zctx, ev;
+    std::vector<uint32_t> fri_steps;
+    Prog step1, step2, step3prev, step42ns, step52ns;
+    uint64_t N = 0, NE = 0;
+    uint32_t eb = 0;
+    zkgpu_sections S;
+    std::vector<void *> allocs;
+    uint64_t *nodes[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint64_t *const_nodes = nullptr;
+    uint64_t *qq1 = nullptr, *qq2 = nullptr, *lev = nullptr, *lpev = nullptr, *xdiv = nullptr, *xdivw = nullptr;
+    uint64_t *fri_pol[2] = {nullptr, nullptr};
+    std::vector<uint64_t *> fri_aux, fri_nodes;
+    uint64_t verkey[4];
+    std::vector<uint64_t> publics;
+    std::vector<std::pair<std::string, double>> timers;
+
+    ~Starks()
+    {
+        for (void *p : allocs) zkgpu_dev_free(p);
+    }
+
+    int dalloc(uint64_t **p, uint64_t elems)
+    {
+        void *v = nullptr;
+        CK(zkgpu_dev_malloc(&v, elems * 8));
+        allocs.push_back(v);
+        *p = (uint64_t *)v;
+        return 0;
+    }
+
+    int create(const zkgpu_stark_info *in)
+    {
+        info = *in;
+        random_cols.assign(in->random_cols, in->random_cols + in->n_random_cols);
+        zctx.assign(in->zctx, in->zctx + 3 * in->n_zctx);
+        ev.assign(in->ev, in->ev + 4 * in->n_ev);
+        fri_steps.assign(in->fri_steps, in->fri_steps + in->n_fri_steps);
+        step1.set(in->step1);
+        step2.set(in->step2);
+        step3prev.set(in->step3prev);
+        step42ns.set(in->step42ns);
+        step52ns.set(in->step52ns);
+        if (in->n_bits_ext < in->n_bits || in->n_bits_ext > 28 || in->n_fri_steps == 0 || in->n_fri_steps > 32 ||
+            in->fri_steps[0] != in->n_bits_ext || in->q_deg * 3 != in->n_cm4 ||
+            ((uint64_t)in->q_deg << in->n_bits) > (1ULL << in->n_bits_ext))
+            return fail("stark_create: inconsistent instance description");
+        N = 1ULL << in->n_bits;
+        NE = 1ULL << in->n_bits_ext;
+        eb = in->n_bits_ext - in->n_bits;
+        CK(zkgpu_init(0));
+        memset(&S, 0, sizeof S);
+        const uint32_t widths_n[5] = {in->n_cm1, in->n_cm2, in->n_cm3, in->n_tmp, in->n_const};
+        for (int s = 0; s < 5; s++) {
+            if (dalloc(&S.sec[s], (uint64_t)(widths_n[s] ? widths_n[s] : 1) * N)) return -1;
+            S.ld[s] = N;
+            S.ncols[s] = widths_n[s];
+        }
+        const uint32_t widths_e[7] = {in->n_cm1, in->n_cm2, in->n_cm3, in->n_cm4, in->n_const, 3, 3};
+        for (int s = 0; s < 7; s++) {
+            if (dalloc(&S.sec[SEC_CM1_2NS + s], (uint64_t)(widths_e[s] ? widths_e[s] : 1) * NE)) return -1;
+            S.ld[SEC_CM1_2NS + s] = NE;
+            S.ncols[SEC_CM1_2NS + s] = widths_e[s];
+        }
+        uint64_t tn = zkgpu_gl_merkle_num_elements(NE);
+        for (int t = 0; t < 4; t++)
+            if (dalloc(&nodes[t], tn)) return -1;
+        if (dalloc(&const_nodes, tn) || dalloc(&qq1, 3 * NE) || dalloc(&qq2, 6 * NE) || dalloc(&lev, 3 * N) ||
+            dalloc(&lpev, 3 * N) || dalloc(&xdiv, 3 * NE) || dalloc(&xdivw, 3 * NE) || dalloc(&fri_pol[0], 3 * NE) ||
+            dalloc(&fri_pol[1], 3 * NE))
+            return -1;
+        fri_aux.assign(fri_steps.size(), nullptr);
+        fri_nodes.assign(fri_steps.size(), nullptr);
+        for (size_t si = 1; si < fri_steps.size(); si++) {
+            uint64_t len = 3ULL << fri_steps[si - 1];
+            if (dalloc(&fri_aux[si], len) || dalloc(&fri_nodes[si], zkgpu_gl_merkle_num_elements(1ULL << fri_steps[si])))
+                return -1;
+        }
+        // constants (setup): K_k pseudo-random, L_first = [1, 0, ...]
+        std::vector<uint32_t> kc(in->n_k);
+        for (uint32_t k = 0; k < in->n_k; k++) kc[k] = k;
+        CK(zkgpu_memset_dev(S.sec[SEC_CONST_N], 0, (uint64_t)in->n_const * N * 8));
+        CK(zkgpu_rand_cols_dev(S.sec[SEC_CONST_N], N, kc.data(), in->n_k, N, in->seed, 1));
+        uint64_t one = 1;
+        CK(zkgpu_memcpy_h2d(S.sec[SEC_CONST_N] + (uint64_t)in->l_first * N, &one, 8));
+        CK(zkgpu_gl_extend_pol_dev(S.sec[SEC_CONST_2NS], NE, S.sec[SEC_CONST_N], N, NE, N, in->n_const));
+        CK(zkgpu_gl_merkletree_dev(const_nodes, S.sec[SEC_CONST_2NS], NE, in->n_const, NE));
+        CK(zkgpu_memcpy_d2h(verkey, const_nodes + tn - 4, 32));
+        publics.resize(in->n_publics);
+        for (uint32_t k = 0; k < in->n_publics; k++) publics[k] = rand_u64(in->seed, 2, k, 0);
+        return 0;
+    }
+
+    int run(const Prog &p, bool ext, const uint64_t ch[24], const uint64_t *evals, uint32_t n_ev)
+    {
+        CK(zkgpu_zxp_eval_dev(p.instr.data(), (uint32_t)p.instr.size(), p.opnd.data(), (uint32_t)p.opnd.size(),
+                              p.n_tmp1 ? p.n_tmp1 : 1, p.n_tmp3 ? p.n_tmp3 : 1, &S,
+                              ext ? info.n_bits_ext : info.n_bits, ch, publics.data(), (uint32_t)publics.size(),
+                              evals, n_ev, ext ? xdiv : nullptr, ext ? xdivw : nullptr, eb, ext ? 7 : 1));
+        return 0;
+    }
+
+    int witness()
+    {
+        CK(zkgpu_memset_dev(S.sec[SEC_CM1_N], 0, (uint64_t)info.n_cm1 * N * 8));
+        CK(zkgpu_rand_cols_dev(S.sec[SEC_CM1_N], N, random_cols.data(), (uint32_t)random_cols.size(), N, info.seed, 0));
+        uint64_t ch[24] = {0};
+        uint64_t ev0[3] = {0, 0, 0};
+        if (run(step1, false, ch, ev0, 0)) return -1;
+        CK(zkgpu_synchronize());
+        return 0;
+    }
+
+    int set_cm1(const uint64_t *rows)
+    {
+        void *tmp = nullptr;
+        CK(zkgpu_dev_malloc(&tmp, (uint64_t)info.n_cm1 * N * 8));
+        int rc = zkgpu_memcpy_h2d(tmp, rows, (uint64_t)info.n_cm1 * N * 8);
+        if (!rc) rc = zkgpu_rows_to_cols_dev(S.sec[SEC_CM1_N], N, (const uint64_t *)tmp, N, info.n_cm1);
+        if (!rc) rc = zkgpu_synchronize();
+        zkgpu_dev_free(tmp);
+        if (rc) return fail("set_cm1: %s", zkgpu_last_error());
+        return 0;
+    }
+
+    uint32_t q() const { return info.n_queries; }
+
+    uint64_t proof_len() const
+    {
+        uint64_t L = 16 + 3ULL * info.n_ev;
+        for (size_t si = 1; si < fri_steps.size(); si++)
+            L += 4 + (uint64_t)q() * (3ULL << (fri_steps[si - 1] - fri_steps[si])) + (uint64_t)q() * fri_steps[si] * 4;
+        L += (uint64_t)q() * (info.n_cm1 + info.n_cm2 + info.n_cm3 + info.n_cm4 + info.n_const);
+        L += 5ULL * q() * info.n_bits_ext * 4;
+        L += 3ULL << fri_steps.back();
+        return L;
+    }
+
+    using clk = std::chrono::steady_clock;
+    clk::time_point t0;
+    void tstart() { t0 = clk::now(); }
+    int tstop(const char *name)
+    {
+        CK(zkgpu_synchronize());
+        timers.emplace_back(name, std::chrono::duration<double, std::milli>(clk::now() - t0).count());
+        return 0;
+    }
+
+    int commit(int t, uint32_t sec_n, uint32_t sec_e, uint32_t ncols, Transcript &tr, uint64_t root[4],
+               const char *lde_name, const char *tree_name)
+    {
+        tstart();
+        CK(zkgpu_gl_extend_pol_dev(S.sec[sec_e], NE, S.sec[sec_n], N, NE, N, ncols));
+        if (tstop(lde_name)) return -1;
+        tstart();
+        CK(zkgpu_gl_merkletree_dev(nodes[t], S.sec[sec_e], NE, ncols, NE));
+        CK(zkgpu_memcpy_d2h(root, nodes[t] + zkgpu_gl_merkle_num_elements(NE) - 4, 32));
+        if (tstop(tree_name)) return -1;
+        tr.put(root, 4);
+        return 0;
+    }
+
+    int prove(uint64_t *out)
+    {
+        timers.clear();
+        auto tall = clk::now();
+        Transcript tr;
+        tr.put(verkey, 4);
+        tr.put(publics.data(), publics.size());
+        uint64_t ch[24] = {0};
+        uint64_t roots[4][4];
+        std::vector<uint64_t> evals(3 * info.n_ev);
+        // STAGE 1 (starks.cpp:49-63)
+        if (commit(0, SEC_CM1_N, SEC_CM1_2NS, info.n_cm1, tr, roots[0], "STARK_STEP_1_LDE", "STARK_STEP_1_MERKLETREE"))
+            return -1;
+        // STAGE 2 (:65-144)
+        tr.get_field(ch + 0);
+        tr.get_field(ch + 3);
+        tstart();
+        if (run(step2, false, ch, evals.data(), 0)) return -1;
+        if (tstop("STARK_STEP_2_CALCULATE_EXPS")) return -1;
+        if (commit(1, SEC_CM2_N, SEC_CM2_2NS, info.n_cm2, tr, roots[1], "STARK_STEP_2_LDE", "STARK_STEP_2_MERKLETREE"))
+            return -1;
+        // STAGE 3 (:146-224)
+        tr.get_field(ch + 6);
+        tr.get_field(ch + 9);
+        tstart();
+        if (run(step3prev, false, ch, evals.data(), 0)) return -1;
+        if (tstop("STARK_STEP_3_CALCULATE_EXPS")) return -1;
+        tstart();
+        for (uint32_t z = 0; z < info.n_zctx; z++) {
+            int closes = 0;
+            CK(zkgpu_calculate_z_dev(S.sec[SEC_CM3_N] + (uint64_t)zctx[3 * z + 2] * N, N,
+                                     S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * z] * N, N,
+                                     S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * z + 1] * N, N, N, &closes));
+            if (!closes) return fail("calculateZ: grand product %u does not close", z);
+        }
+        if (tstop("STARK_STEP_3_CALCULATE_Z")) return -1;
+        if (commit(2, SEC_CM3_N, SEC_CM3_2NS, info.n_cm3, tr, roots[2], "STARK_STEP_3_LDE", "STARK_STEP_3_MERKLETREE"))
+            return -1;
+        // STAGE 4 (:226-296)
+        tr.get_field(ch + 12);
+        tstart();
+        if (run(step42ns, true, ch, evals.data(), 0)) return -1;
+        if (tstop("STARK_STEP_4_CALCULATE_EXPS_2NS")) return -1;
+        tstart();
+        CK(zkgpu_gl_ntt_dev(qq1, NE, S.sec[SEC_Q_2NS], NE, NE, 3, 1));
+        CK(zkgpu_memset_dev(qq2, 0, 6 * NE * 8));
+        uint64_t shift_in = pw(inv(7), N);
+        CK(zkgpu_qsplit_dev(qq2, NE, qq1, NE, N, info.q_deg, shift_in));
+        CK(zkgpu_gl_ntt_dev(S.sec[SEC_CM4_2NS], NE, qq2, NE, NE, info.n_cm4, 0));
+        if (tstop("STARK_STEP_4_CALCULATE_EXPS_2NS_INTT_NTT")) return -1;
+        tstart();
+        CK(zkgpu_gl_merkletree_dev(nodes[3], S.sec[SEC_CM4_2NS], NE, info.n_cm4, NE));
+        CK(zkgpu_memcpy_d2h(roots[3], nodes[3] + zkgpu_gl_merkle_num_elements(NE) - 4, 32));
+        if (tstop("STARK_STEP_4_MERKLETREE")) return -1;
+        tr.put(roots[3], 4);
+        // STAGE 5 (:298-392)
+        tstart();
+        uint64_t *xi = ch + 21;
+        tr.get_field(xi);
+        uint64_t i7 = inv(7), wN = w_of(info.n_bits);
+        uint64_t xis[3], wxis[3];
+        for (int k = 0; k < 3; k++) {
+            xis[k] = mul(xi[k], i7);
+            wxis[k] = mul(mul(xi[k], wN), i7);
+        }
+        CK(zkgpu_ext_powers_dev(lev, N, xis, N));
+        CK(zkgpu_ext_powers_dev(lpev, N, wxis, N));
+        CK(zkgpu_gl_ntt_dev(lev, N, lev, N, N, 3, 1));
+        CK(zkgpu_gl_ntt_dev(lpev, N, lpev, N, N, 3, 1));
+        if (tstop("STARK_STEP_5_LEv_LpEv")) return -1;
+        tstart();
+        {
+            std::vector<const uint64_t *> cols(info.n_ev);
+            std::vector<uint64_t> lds(info.n_ev);
+            std::vector<uint32_t> dims(info.n_ev), primes(info.n_ev);
+            for (uint32_t e = 0; e < info.n_ev; e++) {
+                cols[e] = S.sec[ev[4 * e]] + (uint64_t)ev[4 * e + 1] * S.ld[ev[4 * e]];
+                lds[e] = S.ld[ev[4 * e]];
+                dims[e] = ev[4 * e + 2];
+                primes[e] = ev[4 * e + 3];
+            }
+            CK(zkgpu_evmap_dev(evals.data(), cols.data(), lds.data(), dims.data(), primes.data(), info.n_ev, lev, lpev,
+                               N, N, eb));
+        }
+        if (tstop("STARK_STEP_5_EVMAP")) return -1;
+        tr.put(evals.data(), evals.size());
+        tr.get_field(ch + 15);
+        tr.get_field(ch + 18);
+        tstart();
+        CK(zkgpu_xdivxsub_dev(xdiv, xdivw, xi, info.n_bits, info.n_bits_ext));
+        if (tstop("STARK_STEP_5_XDIVXSUB")) return -1;
+        tstart();
+        if (run(step52ns, true, ch, evals.data(), info.n_ev)) return -1;
+        CK(zkgpu_cols3_to_interleaved_dev(fri_pol[0], S.sec[SEC_F_2NS], NE, NE));
+        if (tstop("STARK_STEP_5_CALCULATE_EXPS")) return -1;
+        // FRI (friProve.cpp:5-190)
+        tstart();
+        uint64_t *w = out;
+        memcpy(w, roots, sizeof roots);
+        w += 16;
+        memcpy(w, evals.data(), evals.size() * 8);
+        w += evals.size();
+        uint32_t pol_bits = info.n_bits_ext;
+        uint64_t shift_inv = inv(7);
+        int cur = 0;
+        std::vector<uint64_t> fri_roots(4 * fri_steps.size(), 0);
+        std::vector<uint64_t> final_pol(3ULL << fri_steps.back());
+        for (size_t si = 0; si < fri_steps.size(); si++) {
+            uint32_t red = pol_bits - fri_steps[si];
+            uint64_t sx[3];
+            tr.get_field(sx);
+            if (si > 0) {
+                CK(zkgpu_fri_fold_dev(fri_pol[cur ^ 1], fri_pol[cur], pol_bits, fri_steps[si], sx, shift_inv));
+                cur ^= 1;
+            }
+            if (si < fri_steps.size() - 1) {
+                uint32_t nb = fri_steps[si + 1];
+                uint64_t ngroups = 1ULL << nb;
+                uint64_t width = (3ULL << fri_steps[si]) / ngroups;
+                CK(zkgpu_fri_transpose_dev(fri_aux[si + 1], fri_pol[cur], 1ULL << fri_steps[si], nb));
+                CK(zkgpu_gl_merkletree_rows_dev(fri_nodes[si + 1], fri_aux[si + 1], width, ngroups));
+                CK(zkgpu_memcpy_d2h(&fri_roots[4 * (si + 1)],
+                                    fri_nodes[si + 1] + zkgpu_gl_merkle_num_elements(ngroups) - 4, 32));
+                tr.put(&fri_roots[4 * (si + 1)], 4);
+            } else {
+                CK(zkgpu_memcpy_d2h(final_pol.data(), fri_pol[cur], final_pol.size() * 8));
+                tr.put(final_pol.data(), final_pol.size());
+            }
+            pol_bits = fri_steps[si];
+            for (uint32_t j = 0; j < red; j++) shift_inv = mul(shift_inv, shift_inv);
+        }
+        if (tstop("STARK_STEP_FRI_FOLDS")) return -1;
+        tstart();
+        std::vector<uint64_t> ys(q());
+        tr.get_permutations(ys.data(), q(), fri_steps[0]);
+        // FRI layers si >= 1: root, vals, siblings
+        std::vector<uint64_t> yq = ys;
+        std::vector<std::vector<uint64_t>> fri_open(fri_steps.size());
+        for (size_t si = 0; si < fri_steps.size(); si++) {
+            if (si > 0) {
+                uint64_t ngroups = 1ULL << fri_steps[si];
+                uint64_t width = (3ULL << fri_steps[si - 1]) / ngroups;
+                std::vector<uint64_t> vals(q() * width), sibs((uint64_t)q() * fri_steps[si] * 4);
+                CK(zkgpu_gl_merkle_open_rows_dev(vals.data(), sibs.data(), fri_nodes[si], fri_aux[si], width, ngroups,
+                                                 yq.data(), q()));
+                memcpy(w, &fri_roots[4 * si], 32);
+                w += 4;
+                memcpy(w, vals.data(), vals.size() * 8);
+                w += vals.size();
+                memcpy(w, sibs.data(), sibs.size() * 8);
+                w += sibs.size();
+            }
+            if (si < fri_steps.size() - 1)
+                for (auto &y : yq) y %= (1ULL << fri_steps[si + 1]);
+        }
+        // s0: the 4 stage trees + the constant tree at the original indices
+        const uint32_t secs[5] = {SEC_CM1_2NS, SEC_CM2_2NS, SEC_CM3_2NS, SEC_CM4_2NS, SEC_CONST_2NS};
+        const uint32_t widths[5] = {info.n_cm1, info.n_cm2, info.n_cm3, info.n_cm4, info.n_const};
+        uint64_t *trees[5] = {nodes[0], nodes[1], nodes[2], nodes[3], const_nodes};
+        std::vector<std::vector<uint64_t>> sib_all(5);
+        for (int t = 0; t < 5; t++) {
+            std::vector<uint64_t> vals((uint64_t)q() * widths[t] + 1);
+            sib_all[t].resize((uint64_t)q() * info.n_bits_ext * 4);
+            CK(zkgpu_gl_merkle_open_dev(vals.data(), sib_all[t].data(), trees[t], S.sec[secs[t]], NE, widths[t], NE,
+                                        ys.data(), q()));
+            memcpy(w, vals.data(), (uint64_t)q() * widths[t] * 8);
+            w += (uint64_t)q() * widths[t];
+        }
+        for (int t = 0; t < 5; t++) {
+            memcpy(w, sib_all[t].data(), sib_all[t].size() * 8);
+            w += sib_all[t].size();
+        }
+        memcpy(w, final_pol.data(), final_pol.size() * 8);
+        w += final_pol.size();
+        if (tstop("STARK_STEP_FRI_QUERIES")) return -1;
+        if (tr.err) return fail("transcript hashing failed: %s", zkgpu_last_error());
+        if ((uint64_t)(w - out) != proof_len()) return fail("proof length mismatch");
+        timers.emplace_back("STARK_TOTAL", std::chrono::duration<double, std::milli>(clk::now() - tall).count());
+        return 0;
+    }
+};
+
+}  // namespace zkgpu_host
+
+using zkgpu_host::Starks;
+
+extern "C" {
+
+const char *zkgpu_stark_last_error(void) { return zkgpu_host::g_err; }
+
+int zkgpu_stark_create(void **handle, const zkgpu_stark_info *info)
+{
+    Starks *s = new Starks();
+    if (s->create(info)) {
+        delete s;
+        *handle = nullptr;
+        return -1;
+    }
+    *handle = s;
+    return 0;
+}
+
+int zkgpu_stark_witness(void *h) { return ((Starks *)h)->witness(); }
+int zkgpu_stark_set_cm1(void *h, const uint64_t *rows) { return ((Starks *)h)->set_cm1(rows); }
+uint64_t zkgpu_stark_proof_len(void *h) { return ((Starks *)h)->proof_len(); }
+int zkgpu_stark_prove(void *h, uint64_t *out) { return ((Starks *)h)->prove(out); }
+int zkgpu_stark_verkey(void *h, uint64_t out[4])
+{
+    memcpy(out, ((Starks *)h)->verkey, 32);
+    return 0;
+}
+int zkgpu_stark_publics(void *h, uint64_t *out)
+{
+    Starks *s = (Starks *)h;
+    memcpy(out, s->publics.data(), s->publics.size() * 8);
+    return (int)s->publics.size();
+}
+int zkgpu_stark_timers(void *h, char *names_buf, uint64_t names_len, double *ms, uint32_t max)
+{
+    Starks *s = (Starks *)h;
+    std::string names;
+    uint32_t n = 0;
+    for (auto &t : s->timers) {
+        if (n >= max) break;
+        names += t.first + "\n";
+        ms[n++] = t.second;
+    }
+    if (names_len) {
+        size_t c = names.size() < names_len - 1 ? names.size() : names_len - 1;
+        memcpy(names_buf, names.data(), c);
+        names_buf[c] = 0;
+    }
+    return (int)n;
+}
+void zkgpu_stark_destroy(void *h) { delete (Starks *)h; }
+
+}  // extern "C"

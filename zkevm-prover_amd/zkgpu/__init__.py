@@ -58,6 +58,22 @@ _SIGS = {
     "zkgpu_fri_fold_dev": (ctypes.c_int, [vp, vp, u32, u32, vp, u64]),
     "zkgpu_fri_transpose_dev": (ctypes.c_int, [vp, vp, u64, u32]),
     "zkgpu_gl_field_selftest_dev": (ctypes.c_int, [vp, vp, vp, u64, ctypes.c_int]),
+    "zkgpu_dev_malloc": (ctypes.c_int, [ctypes.POINTER(vp), u64]),
+    "zkgpu_dev_free": (ctypes.c_int, [vp]),
+    "zkgpu_memcpy_h2d": (ctypes.c_int, [vp, vp, u64]),
+    "zkgpu_memcpy_d2h": (ctypes.c_int, [vp, vp, u64]),
+    "zkgpu_memcpy_d2d": (ctypes.c_int, [vp, vp, u64]),
+    "zkgpu_memset_dev": (ctypes.c_int, [vp, ctypes.c_int, u64]),
+    "zkgpu_rand_cols_dev": (ctypes.c_int, [vp, u64, vp, u32, u64, u64, u64]),
+    "zkgpu_zxp_eval_dev": (ctypes.c_int, [vp, u32, vp, u32, u32, u32, vp, u32, vp, vp, u32, vp, u32, vp, vp, u32,
+                                          u64]),
+    "zkgpu_calculate_z_dev": (ctypes.c_int, [vp, u64, vp, u64, vp, u64, u64, ctypes.POINTER(ctypes.c_int)]),
+    "zkgpu_evmap_dev": (ctypes.c_int, [vp, vp, vp, vp, vp, u32, vp, vp, u64, u64, u32]),
+    "zkgpu_xdivxsub_dev": (ctypes.c_int, [vp, vp, vp, u32, u32]),
+    "zkgpu_ext_powers_dev": (ctypes.c_int, [vp, u64, vp, u64]),
+    "zkgpu_qsplit_dev": (ctypes.c_int, [vp, u64, vp, u64, u64, u32, u64]),
+    "zkgpu_cols3_to_interleaved_dev": (ctypes.c_int, [vp, vp, u64, u64]),
+    "zkgpu_gl_merkle_open_rows_dev": (ctypes.c_int, [vp, vp, vp, vp, u64, u64, vp, u64]),
     "zkgpu_prof_enable": (ctypes.c_int, [ctypes.c_int]),
     "zkgpu_prof_reset": (ctypes.c_int, []),
     "zkgpu_prof_query": (ctypes.c_int, [ctypes.c_char_p, pu64, ctypes.POINTER(ctypes.c_double),
@@ -252,6 +268,37 @@ def fri_transpose_dev(aux, pol, degree, transpose_bits):
 
 def field_selftest_dev(out, a, b, n, op):
     _check(lib().zkgpu_gl_field_selftest_dev(_addr(out), _addr(a), _addr(b), n, op), "zkgpu_gl_field_selftest_dev")
+
+
+def calculate_z_dev(z, z_ld, num, num_ld, den, den_ld, n):
+    closes = ctypes.c_int(0)
+    _check(lib().zkgpu_calculate_z_dev(_addr(z), z_ld, _addr(num), num_ld, _addr(den), den_ld, n,
+                                       ctypes.byref(closes)), "zkgpu_calculate_z_dev")
+    return bool(closes.value)
+
+
+def xdivxsub_dev(xdiv, xdivw, xi, n_bits, n_bits_ext):
+    x = _np(xi)
+    _check(lib().zkgpu_xdivxsub_dev(_addr(xdiv), _addr(xdivw), x.ctypes.data, n_bits, n_bits_ext),
+           "zkgpu_xdivxsub_dev")
+
+
+def ext_powers_dev(out, ld, base, n):
+    b = _np(base)
+    _check(lib().zkgpu_ext_powers_dev(_addr(out), ld, b.ctypes.data, n), "zkgpu_ext_powers_dev")
+
+
+def evmap_dev(cols, lds, dims, primes, lev, lpev, l_ld, n, extend_bits):
+    n_ev = len(cols)
+    ptrs = (ctypes.c_void_p * n_ev)(*[_addr(c) for c in cols])
+    lds_a = _np(lds)
+    dims_a = np.ascontiguousarray(dims, np.uint32)
+    pr_a = np.ascontiguousarray(primes, np.uint32)
+    out = np.zeros((n_ev, 3), np.uint64)
+    _check(lib().zkgpu_evmap_dev(out.ctypes.data, ctypes.cast(ptrs, ctypes.c_void_p), lds_a.ctypes.data,
+                                 dims_a.ctypes.data, pr_a.ctypes.data, n_ev, _addr(lev), _addr(lpev), l_ld, n,
+                                 extend_bits), "zkgpu_evmap_dev")
+    return out
 
 
 # ---------------------------------------------------------------- profiling

@@ -1,0 +1,196 @@
+"""Python binding of libzkgpu_stark (host/starks.cpp): the GPU STARK prover.
+
+Builds the zkgpu_stark_info description (include/zkgpu_stark.h) from a
+SyntheticStark instance, runs setup / witness / prove, and returns the proof
+in the reference's zkin layout with canonical decimal strings (the same form
+as the reference's testvectors and the oracle's prover).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import ZkgpuError, lib as _zk_lib
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+STARK_LIB = os.path.join(os.path.dirname(_HERE), "lib", "libzkgpu_stark.so")
+P = 0xFFFFFFFF00000001
+
+
+class _Prog(ctypes.Structure):
+    _fields_ = [("instr", ctypes.c_void_p), ("n_instr", ctypes.c_uint32), ("opnd", ctypes.c_void_p),
+                ("n_opnd", ctypes.c_uint32), ("n_tmp1", ctypes.c_uint32), ("n_tmp3", ctypes.c_uint32)]
+
+
+class _Info(ctypes.Structure):
+    _fields_ = [("n_bits", ctypes.c_uint32), ("n_bits_ext", ctypes.c_uint32), ("n_queries", ctypes.c_uint32),
+                ("n_fri_steps", ctypes.c_uint32), ("fri_steps", ctypes.c_uint32 * 32),
+                ("n_cm1", ctypes.c_uint32), ("n_cm2", ctypes.c_uint32), ("n_cm3", ctypes.c_uint32),
+                ("n_cm4", ctypes.c_uint32), ("n_tmp", ctypes.c_uint32), ("n_const", ctypes.c_uint32),
+                ("n_publics", ctypes.c_uint32), ("q_deg", ctypes.c_uint32), ("l_first", ctypes.c_uint32),
+                ("n_k", ctypes.c_uint32), ("seed", ctypes.c_uint64),
+                ("n_random_cols", ctypes.c_uint32), ("random_cols", ctypes.c_void_p),
+                ("n_zctx", ctypes.c_uint32), ("zctx", ctypes.c_void_p),
+                ("n_ev", ctypes.c_uint32), ("ev", ctypes.c_void_p),
+                ("step1", _Prog), ("step2", _Prog), ("step3prev", _Prog), ("step42ns", _Prog), ("step52ns", _Prog)]
+
+
+_slib = None
+
+
+def slib():
+    global _slib
+    if _slib is None:
+        _zk_lib()  # binds the HIP runtime first (see zkgpu.lib)
+        if not os.path.exists(STARK_LIB):
+            raise ZkgpuError("libzkgpu_stark.so not built; run __graft_entry__.build()")
+        L = ctypes.CDLL(STARK_LIB)
+        vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+        for name, res, args in [
+            ("zkgpu_stark_create", ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(_Info)]),
+            ("zkgpu_stark_witness", ctypes.c_int, [vp]),
+            ("zkgpu_stark_set_cm1", ctypes.c_int, [vp, vp]),
+            ("zkgpu_stark_proof_len", u64, [vp]),
+            ("zkgpu_stark_prove", ctypes.c_int, [vp, vp]),
+            ("zkgpu_stark_verkey", ctypes.c_int, [vp, vp]),
+            ("zkgpu_stark_publics", ctypes.c_int, [vp, vp]),
+            ("zkgpu_stark_timers", ctypes.c_int, [vp, ctypes.c_char_p, u64, vp, ctypes.c_uint32]),
+            ("zkgpu_stark_destroy", None, [vp]),
+            ("zkgpu_stark_last_error", ctypes.c_char_p, []),
+        ]:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _slib = L
+    return _slib
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise ZkgpuError("%s failed: %s" % (what, slib().zkgpu_stark_last_error().decode(errors="replace")))
+
+
+class GpuStark:
+    def __init__(self, inst):
+        self.inst = inst
+        self._keep = []
+        info = _Info()
+        info.n_bits, info.n_bits_ext, info.n_queries = inst.n_bits, inst.n_bits_ext, inst.n_queries
+        info.n_fri_steps = len(inst.fri_steps)
+        for i, s in enumerate(inst.fri_steps):
+            info.fri_steps[i] = s
+        info.n_cm1, info.n_cm2, info.n_cm3, info.n_cm4 = inst.n_cm1, inst.n_cm2, inst.n_cm3, inst.n_cm4
+        info.n_tmp, info.n_const, info.n_publics = inst.n_tmp, inst.n_const, inst.n_publics
+        info.q_deg, info.l_first, info.n_k, info.seed = inst.q_deg, inst.l_first, inst.n_k, inst.seed
+        rc = np.array(inst.random_cm1_cols(), np.uint32)
+        zc = np.array(inst.z_ctx, np.uint32).reshape(-1)
+        ev = np.array(inst.evmap, np.uint32).reshape(-1)
+        self._keep += [rc, zc, ev]
+        info.n_random_cols, info.random_cols = rc.size, rc.ctypes.data
+        info.n_zctx, info.zctx = len(inst.z_ctx), zc.ctypes.data
+        info.n_ev, info.ev = len(inst.evmap), ev.ctypes.data
+        for name in ("step1", "step2", "step3prev", "step42ns", "step52ns"):
+            prog = inst.programs[name]
+            ins, opn = prog.arrays()
+            ins, opn = np.ascontiguousarray(ins), np.ascontiguousarray(opn)
+            self._keep += [ins, opn]
+            setattr(info, name, _Prog(ins.ctypes.data, ins.shape[0], opn.ctypes.data, opn.shape[0],
+                                      max(prog.n_tmp1, 1), max(prog.n_tmp3, 1)))
+        self._info = info
+        self.h = ctypes.c_void_p()
+        _check(slib().zkgpu_stark_create(ctypes.byref(self.h), ctypes.byref(info)), "zkgpu_stark_create")
+
+    def witness(self):
+        _check(slib().zkgpu_stark_witness(self.h), "zkgpu_stark_witness")
+
+    def set_cm1(self, rows):
+        rows = np.ascontiguousarray(rows, np.uint64)
+        _check(slib().zkgpu_stark_set_cm1(self.h, rows.ctypes.data), "zkgpu_stark_set_cm1")
+
+    def verkey(self):
+        v = np.zeros(4, np.uint64)
+        slib().zkgpu_stark_verkey(self.h, v.ctypes.data)
+        return v
+
+    def publics(self):
+        v = np.zeros(max(self.inst.n_publics, 1), np.uint64)
+        n = slib().zkgpu_stark_publics(self.h, v.ctypes.data)
+        return v[:n]
+
+    def prove_raw(self):
+        n = slib().zkgpu_stark_proof_len(self.h)
+        buf = np.zeros(n, np.uint64)
+        _check(slib().zkgpu_stark_prove(self.h, buf.ctypes.data), "zkgpu_stark_prove")
+        return buf
+
+    def prove(self):
+        return self.parse(self.prove_raw())
+
+    def timers(self):
+        names = ctypes.create_string_buffer(4096)
+        ms = np.zeros(64, np.float64)
+        n = slib().zkgpu_stark_timers(self.h, names, len(names), ms.ctypes.data, 64)
+        keys = names.value.decode().split("\n")[:n]
+        return dict(zip(keys, [float(x) for x in ms[:n]]))
+
+    def parse(self, buf):
+        inst = self.inst
+        q = inst.n_queries
+        steps = inst.fri_steps
+        pos = [0]
+
+        def take(n, shape=None):
+            a = buf[pos[0]:pos[0] + n]
+            pos[0] += n
+            return a.reshape(shape) if shape else a
+
+        out = {}
+        for k in ("root1", "root2", "root3", "root4"):
+            out[k] = take(4)
+        out["evals"] = take(3 * len(inst.evmap), (-1, 3))
+        for si in range(1, len(steps)):
+            width = 3 << (steps[si - 1] - steps[si])
+            out["s%d_root" % si] = take(4)
+            out["s%d_vals" % si] = take(q * width, (q, width))
+            out["s%d_siblings" % si] = take(q * steps[si] * 4, (q, steps[si], 4))
+        widths = [inst.n_cm1, inst.n_cm2, inst.n_cm3, inst.n_cm4, inst.n_const]
+        tags = ["1", "2", "3", "4", "C"]
+        for tag, wd in zip(tags, widths):
+            out["s0_vals" + tag] = take(q * wd, (q, wd))
+        for tag in tags:
+            out["s0_siblings" + tag] = take(q * inst.n_bits_ext * 4, (q, inst.n_bits_ext, 4))
+        out["finalPol"] = take(3 << steps[-1], (-1, 3))
+        assert pos[0] == buf.size
+        return to_json(out)
+
+    def close(self):
+        if self.h:
+            slib().zkgpu_stark_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def to_json(proof):
+    def conv(v):
+        if isinstance(v, np.ndarray):
+            return conv(v.tolist())
+        if isinstance(v, list):
+            return [conv(x) for x in v]
+        return str(int(v) % P)
+    out = {k: conv(proof[k]) for k in ("root1", "root2", "root3", "root4", "evals")}
+    i = 1
+    while "s%d_root" % i in proof:
+        for k in ("root", "vals", "siblings"):
+            out["s%d_%s" % (i, k)] = conv(proof["s%d_%s" % (i, k)])
+        i += 1
+    for tag in ("1", "2", "3", "4", "C"):
+        out["s0_vals" + tag] = conv(proof["s0_vals" + tag])
+    for tag in ("1", "2", "3", "4", "C"):
+        out["s0_siblings" + tag] = conv(proof["s0_siblings" + tag])
+    out["finalPol"] = conv(proof["finalPol"])
+    return out
