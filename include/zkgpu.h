@@ -39,7 +39,8 @@ extern "C" {
  * Replaces the implicit setup of the Goldilocks submodule objects:
  * NTT_Goldilocks(maxDomainSize, nThreads, extension) constructed at
  * starks.hpp:81-82 and friProve.cpp:100 (twiddle tables), plus the Poseidon
- * constant tables.  device = HIP device ordinal. */
+ * constant tables.  device = HIP device ordinal; device < 0 keeps the
+ * initialised device, or uses the calling thread's current HIP device. */
 int zkgpu_init(int device);
 void zkgpu_release(void);
 const char *zkgpu_last_error(void);

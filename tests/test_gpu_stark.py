@@ -124,3 +124,40 @@ def test_evmap_dev(oracle, zkgpu):
     got = zkgpu.evmap_dev([base + 8 * ne * c for c, _, _ in entries], [ne] * len(entries), dims, primes, dlev, dlpev,
                           n, n, eb)
     assert np.array_equal(got, ref)
+
+
+def _upload_sections(zkgpu, o):
+    """Oracle sections (row-major) -> device column-major {index: (tensor, ld, ncols)}."""
+    secs = {}
+    for k, a in o.S.items():
+        secs[k] = (zkgpu.to_device(np.ascontiguousarray(a.T)), a.shape[0], a.shape[1])
+    return secs
+
+
+@pytest.mark.parametrize("n_bits,blow", [(8, 1), (9, 2)])
+def test_step42ns_stage(oracle, zkgpu, n_bits, blow):
+    """Stage 4 piece by piece: constraint quotient on the 2^nBitsExt domain,
+    INTT, quotient split, NTT (starks.cpp:226-296) vs the oracle's sections."""
+    import torch
+    from zkgpu.synthetic import SyntheticStark, SEC_Q_2NS
+    inst = SyntheticStark(n_bits=n_bits, blowup_bits=blow, t=4, m=2, n_queries=8)
+    o, _ = oracle_proof(inst)
+    N, NE, eb = o.N, o.NE, o.eb
+    secs = _upload_sections(zkgpu, o)
+    q = torch.zeros((3, NE), dtype=torch.int64, device="cuda:0")
+    secs[SEC_Q_2NS] = (q, NE, 3)
+    zkgpu.zxp_eval_dev(inst.programs["step42ns"], secs, inst.n_bits_ext, o.challenges, o.publics,
+                       extend_bits=eb, x_start=7)
+    torch.cuda.synchronize()
+    assert np.array_equal(zkgpu.from_device(q).T, o.S[10])
+    qq1 = torch.zeros((3, NE), dtype=torch.int64, device="cuda:0")
+    zkgpu.ntt_dev(qq1, NE, q, NE, NE, 3, inverse=True)
+    ref_qq1 = oracle.ntt(o.S[10], True)
+    assert np.array_equal(zkgpu.from_device(qq1).T, ref_qq1)
+    qq2 = torch.zeros((inst.q_deg * 3, NE), dtype=torch.int64, device="cuda:0")
+    shift_in = pow(pow(7, P - 2, P), N, P)
+    zkgpu.qsplit_dev(qq2, NE, qq1, NE, N, inst.q_deg, shift_in)
+    cm4 = torch.zeros((inst.q_deg * 3, NE), dtype=torch.int64, device="cuda:0")
+    zkgpu.ntt_dev(cm4, NE, qq2, NE, NE, inst.q_deg * 3)
+    torch.cuda.synchronize()
+    assert np.array_equal(zkgpu.from_device(cm4).T, o.S[8])

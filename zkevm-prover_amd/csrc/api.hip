@@ -228,7 +228,15 @@ const char *zkgpu_last_error(void) { return g_err; }
 int zkgpu_init(int device)
 {
     Ctx &c = g_ctx;
+    if (device < 0) {
+        // keep whatever is initialised / current (torch.cuda.set_device in a rank)
+        if (c.ready) return 0;
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) cur = 0;
+        device = cur;
+    }
     if (c.ready && c.device == device) return 0;
+    if (c.ready) zkgpu_release();
     int rc;
     if ((rc = check_hip(hipSetDevice(device), "hipSetDevice"))) return rc;
     c.device = device;
@@ -531,6 +539,7 @@ int zkgpu_rand_cols_dev(uint64_t *base, uint64_t ld, const uint32_t *cols, uint3
     char *p = param_buf(ncols * 4);
     if (!p) return set_error(ZKGPU_ERR_OOM, "param buffer");
     if ((rc = check_hip(hipMemcpyAsync(p, cols, ncols * 4, hipMemcpyHostToDevice, g_ctx.stream), "H2D"))) return rc;
+    if ((rc = check_hip(hipStreamSynchronize(g_ctx.stream), "rand_cols param upload"))) return rc;
     return rand_cols(base, ld, (const uint32_t *)p, ncols, nrows, seed, stream, g_ctx.stream);
 }
 
@@ -590,7 +599,8 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
         uint64_t sn = h_pow(7, 1ULL << (log_dom - extend_bits));
         uint64_t we = h_w(extend_bits), w = 1;
         for (size_t j = 0; j < zh; j++) {
-            zhv[j] = h_inv((h_mul(sn, w) + HP - 1) % HP);
+            const uint64_t x = h_mul(sn, w);  // < HP
+            zhv[j] = h_inv(x ? x - 1 : HP - 1);
             w = h_mul(w, we);
         }
     }
@@ -603,6 +613,9 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
         (n_evals && (rc = check_hip(hipMemcpyAsync(p + off_ev, evals, n_evals * 24, hipMemcpyHostToDevice, s), "H2D"))) ||
         (rc = check_hip(hipMemcpyAsync(p + off_zh, zhv, zh * 8, hipMemcpyHostToDevice, s), "H2D")))
         return rc;
+    // the sources are pageable host memory (zhv lives on this stack): the
+    // uploads must complete before returning
+    if ((rc = check_hip(hipStreamSynchronize(s), "zxp param upload"))) return rc;
     ZxpLaunch L;
     for (int k = 0; k < SEC_COUNT; k++) {
         L.sec[k] = sections->sec[k];
@@ -677,6 +690,7 @@ int zkgpu_evmap_dev(uint64_t *evals_out, const uint64_t *const *cols, const uint
         return set_error(ZKGPU_ERR_OOM, "param buffer");
     }
     rc = check_hip(hipMemcpyAsync(p, h, n_ev * sizeof(E), hipMemcpyHostToDevice, g_ctx.stream), "H2D");
+    if (!rc) rc = check_hip(hipStreamSynchronize(g_ctx.stream), "evmap param upload");
     free(h);
     if (rc) return rc;
     if ((rc = evmap((uint64_t *)(p + off_ev), p, n_ev, lev, lpev, l_ld, n, extend_bits, (uint64_t *)(p + off_part),

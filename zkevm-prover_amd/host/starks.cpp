@@ -195,10 +195,13 @@ public:
             in->fri_steps[0] != in->n_bits_ext || in->q_deg * 3 != in->n_cm4 ||
             ((uint64_t)in->q_deg << in->n_bits) > (1ULL << in->n_bits_ext))
             return fail("stark_create: inconsistent instance description");
+        for (uint32_t si = 1; si < in->n_fri_steps; si++)
+            if (in->fri_steps[si] >= in->fri_steps[si - 1] || in->fri_steps[si - 1] - in->fri_steps[si] > 5)
+                return fail("stark_create: FRI steps must decrease by 1..5 bits");
         N = 1ULL << in->n_bits;
         NE = 1ULL << in->n_bits_ext;
         eb = in->n_bits_ext - in->n_bits;
-        CK(zkgpu_init(0));
+        CK(zkgpu_init(-1));
         memset(&S, 0, sizeof S);
         const uint32_t widths_n[5] = {in->n_cm1, in->n_cm2, in->n_cm3, in->n_tmp, in->n_const};
         for (int s = 0; s < 5; s++) {

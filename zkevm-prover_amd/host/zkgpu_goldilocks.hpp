@@ -45,7 +45,7 @@ inline void check(int rc, const char *where)
     if (rc != ZKGPU_OK) error_handler()(where, rc, zkgpu_last_error());
 }
 
-inline void ensure_init(int device = 0)
+inline void ensure_init(int device = -1)
 {
     static bool done = false;
     if (!done) {

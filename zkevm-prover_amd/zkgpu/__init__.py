@@ -288,6 +288,42 @@ def ext_powers_dev(out, ld, base, n):
     _check(lib().zkgpu_ext_powers_dev(_addr(out), ld, b.ctypes.data, n), "zkgpu_ext_powers_dev")
 
 
+class Sections(ctypes.Structure):
+    """zkgpu_sections (include/zkgpu.h): 12 column-major section bases."""
+    _fields_ = [("sec", vp * 12), ("ld", u64 * 12), ("ncols", u32 * 12)]
+
+
+def zxp_eval_dev(prog, sections, log_dom, challenges, publics, evals=None, xdiv=None, xdivw=None, extend_bits=0,
+                 x_start=1):
+    """Evaluate one ZXP program (zkgpu.synthetic.Program or (instr, opnd,
+    n_tmp1, n_tmp3)) over the domain; sections: {index: (tensor, ld, ncols)}."""
+    if hasattr(prog, "arrays"):
+        ins, opn = prog.arrays()
+        nt1, nt3 = prog.n_tmp1, prog.n_tmp3
+    else:
+        ins, opn, nt1, nt3 = prog
+    ins = np.ascontiguousarray(ins, np.uint32)
+    opn = np.ascontiguousarray(opn, np.uint32)
+    s = Sections()
+    for k, (t, ld, nc) in sections.items():
+        s.sec[k] = _addr(t)
+        s.ld[k] = ld
+        s.ncols[k] = nc
+    ch = np.zeros(24, np.uint64)
+    c = _np(challenges).reshape(-1)
+    ch[:c.size] = c
+    pub = _np(publics if publics is not None else np.zeros(1, np.uint64))
+    ev = _np(evals if evals is not None else np.zeros(3, np.uint64)).reshape(-1)
+    _check(lib().zkgpu_zxp_eval_dev(ins.ctypes.data, ins.shape[0], opn.ctypes.data, opn.shape[0], max(nt1, 1),
+                                    max(nt3, 1), ctypes.byref(s), log_dom, ch.ctypes.data, pub.ctypes.data,
+                                    pub.size if publics is not None else 0, ev.ctypes.data, ev.size // 3,
+                                    _addr(xdiv), _addr(xdivw), extend_bits, x_start), "zkgpu_zxp_eval_dev")
+
+
+def qsplit_dev(qq2, ld2, qq1, ld1, n, q_deg, shift_in):
+    _check(lib().zkgpu_qsplit_dev(_addr(qq2), ld2, _addr(qq1), ld1, n, q_deg, shift_in), "zkgpu_qsplit_dev")
+
+
 def evmap_dev(cols, lds, dims, primes, lev, lpev, l_ld, n, extend_bits):
     n_ev = len(cols)
     ptrs = (ctypes.c_void_p * n_ev)(*[_addr(c) for c in cols])
