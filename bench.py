@@ -43,8 +43,11 @@ def parse():
     ap.add_argument("--blowup-bits", type=int, default=1)
     ap.add_argument("--cpu-sample-cols", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_COLS", "4")))
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--workload", choices=["lde", "merkle"], default="lde",
-                    help="lde = configs[1] (headline); merkle = configs[2] (2^23 x 100 Poseidon tree)")
+    ap.add_argument("--workload", choices=["lde", "merkle", "stark"], default="lde",
+                    help="lde = configs[1] (headline); merkle = configs[2] (2^23 x 100 Poseidon tree); "
+                         "stark = configs[3] (full synthetic STARK proof, 2^23 trace)")
+    ap.add_argument("--queries", type=int, default=128)
+    ap.add_argument("--cpu-sample-bits", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_BITS", "16")))
     return ap.parse_args()
 
 
@@ -84,6 +87,43 @@ def cpu_baseline_merkle(log_n, ncols):
                       % (min(log_n, 16), ncols, dt, threads, _cpu_model())}
 
 
+def stark_instance(log_n, blow, ncols, n_queries):
+    """cm1/cm2/cm3 = ncols/24/24, 30 constants, qDeg 2,
+    FRI steps [nBitsExt, -4, ..., 5], n_queries queries (synthetic AIR)."""
+    from zkgpu.synthetic import SyntheticStark
+    nbe = log_n + blow
+    steps = [nbe]
+    while steps[-1] - 4 >= 5:
+        steps.append(steps[-1] - 4)
+    if steps[-1] > 5:
+        steps.append(5)
+    t = ncols // 3
+    return SyntheticStark(n_bits=log_n, blowup_bits=blow, t=t, n_free=ncols - 3 * t, m=8, n_k=29,
+                          n_queries=n_queries, fri_steps=steps)
+
+
+def cpu_baseline_stark(sample_bits, log_n, blow, ncols, n_queries):
+    """Oracle STARK prover (C/OpenMP kernels + numpy driver) on a bounded sample:
+    the same instance shape at 2^sample_bits rows."""
+    from oracle import oracle as oc
+    from oracle.stark_prover import OracleStark
+    oc.lib()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    oc.lib().oc_set_num_threads(threads)
+    inst = stark_instance(sample_bits, blow, ncols, n_queries)
+    o = OracleStark(inst)
+    o.witness()
+    t0 = time.perf_counter()
+    o.prove()
+    dt = time.perf_counter() - t0
+    scale = (1 << (log_n - sample_bits)) * (log_n + blow) / (sample_bits + blow)
+    return {"value": round(dt, 3), "unit": "s/proof (2^%d sample)" % sample_bits, "cores": threads, "kind": "port",
+            "extrapolated_full_s": round(dt * scale, 1),
+            "sample": "oracle genProof of the config-4 instance shape at 2^%d rows (%d cm1 cols, %d queries), "
+                      "%.1f s, %d threads (%s); extrapolated_full_s scales by N log N to 2^%d"
+                      % (sample_bits, ncols, n_queries, dt, threads, _cpu_model(), log_n)}
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -117,7 +157,16 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED + rank)
     # canonical Goldilocks values: uniform in [0, 2^63) < p
-    if args.workload == "lde":
+    gs = None
+    if args.workload == "stark":
+        from zkgpu.stark import GpuStark
+        inst = stark_instance(args.log_n, args.blowup_bits, C, args.queries)
+        gs = GpuStark(inst)  # setup: constants, constant LDE + tree (untimed, loaded from files in the reference)
+        gs.witness()         # executor stand-in: committed trace cm1 in HBM (untimed)
+
+        def step():
+            gs.prove_raw()
+    elif args.workload == "lde":
         trace = torch.randint(0, 2**63 - 1, (C, n), dtype=torch.int64, device=dev, generator=g)
         out = torch.empty((C, ne), dtype=torch.int64, device=dev)
 
@@ -165,7 +214,11 @@ def main():
     elapsed = float(t.item())
 
     if rank == 0:
-        if args.workload == "lde":
+        if args.workload == "stark":
+            total_elems = world * args.steps
+            unit, metric_unit = "s/proof", "proofs"
+            alg_step = 8 * (n + ne) * (C + 48 + 6)
+        elif args.workload == "lde":
             total_elems = ne * C * world * args.steps
             unit, metric_unit = "Gelem/s", "LDE output elements"
             alg_step = 8 * (n + ne) * C  # per step per GPU
@@ -174,33 +227,45 @@ def main():
             unit, metric_unit = "Gelem/s", "Merkle leaf elements hashed"
             alg_step = 8 * n * C + 32 * n + 96 * (n - 1)
         value = total_elems / elapsed / 1e9
+        if args.workload == "stark":
+            value = elapsed / total_elems  # seconds per proof, whole job
         cpu = None
+        if world == 1 and not args.no_cpu and args.workload == "stark":
+            cpu = cpu_baseline_stark(args.cpu_sample_bits, args.log_n, args.blowup_bits, C, args.queries)
         if world == 1 and not args.no_cpu and args.workload == "lde":
             cpu = cpu_baseline(args.log_n, args.blowup_bits, args.cpu_sample_cols)
         if world == 1 and not args.no_cpu and args.workload == "merkle":
             cpu = cpu_baseline_merkle(args.log_n, C)
-        workload = ("LDE 2^%d -> 2^%d rows x %d cols per GPU (extendPol, starks.cpp:53), column-major in HBM"
-                    % (args.log_n, args.log_n + args.blowup_bits, C)) if args.workload == "lde" else (
-                    "Poseidon-GL Merkle tree over 2^%d rows x %d cols per GPU (merkelize, merkleTreeGL.cpp:37-44)"
-                    % (args.log_n, C))
+        if args.workload == "lde":
+            workload = ("LDE 2^%d -> 2^%d rows x %d cols per GPU (extendPol, starks.cpp:53), column-major in HBM"
+                        % (args.log_n, args.log_n + args.blowup_bits, C))
+        elif args.workload == "merkle":
+            workload = ("Poseidon-GL Merkle tree over 2^%d rows x %d cols per GPU (merkelize, merkleTreeGL.cpp:37-44)"
+                        % (args.log_n, C))
+        else:
+            workload = ("full STARK proof (genProof stages 1-5 + FRI + queries, starks.cpp:9-404), synthetic "
+                        "config-4 instance: 2^%d trace, blowup 2^%d, cm1/cm2/cm3/cm4 = %d/24/24/6, 30 constants, "
+                        "FRI steps %s, %d queries; one independent proof per GPU"
+                        % (args.log_n, args.blowup_bits, C, inst.fri_steps, args.queries))
         res = {
             "metric": METRIC,
             "value": round(value, 4),
             "unit": unit,
-            "value_meaning": metric_unit + " per second, all GPUs",
+            "value_meaning": (metric_unit + " per second, all GPUs") if args.workload != "stark" else "wall seconds per proof, whole job",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
+            "higher_is_better": args.workload != "stark",
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u64 (Goldilocks)",
+            "dtype": "u64 (Goldilocks)" if args.workload != "stark" else "u64 (Goldilocks) + F_p^3",
             "data": "synthetic (uniform canonical Goldilocks, torch generator seed 0x5EED+rank)",
             "config": {
                 "workload": workload,
                 "log_n": args.log_n, "blowup_bits": args.blowup_bits, "ncols_per_gpu": C,
-                "parallelism": "column-sharded x%d (no data-path collective)" % world,
+                "parallelism": ("column-sharded x%d (no data-path collective)" % world) if args.workload != "stark"
+                else "replicas x%d (one independent proof per GPU)" % world,
             },
             "roofline": {
                 "kernel": dom,
@@ -218,6 +283,8 @@ def main():
                             "GB/s": round(v[2] / v[0] / (v[1] / v[0] * 1e-3) / 1e9, 1)} for k, v in kernels.items()},
             "cpu_baseline": cpu,
         }
+        if gs is not None:
+            res["stages_ms"] = {k: round(v, 3) for k, v in gs.timers().items()}
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -51,6 +51,25 @@ for step in "$@"; do
         ok_or_stop $? "bench merkle"
         cat gpurun_out/bench_merkle.json
         ;;
+    stark)
+        timeout -k 10 300 python bench.py --workload stark --log-n 16 --steps 2 --warmup 1 --no-cpu \
+            > gpurun_out/bench_stark16.json 2> gpurun_out/bench_stark16.err
+        ok_or_stop $? "bench stark 2^16"
+        cat gpurun_out/bench_stark16.json
+        timeout -k 10 900 python bench.py --workload stark --steps 3 --warmup 1 \
+            > gpurun_out/bench_stark.json 2> gpurun_out/bench_stark.err
+        ok_or_stop $? "bench stark"
+        cat gpurun_out/bench_stark.json
+        ;;
+    starkprof)
+        cd /tmp
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_stark" -o run \
+            --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --workload stark --no-cpu --steps 2 --warmup 1 \
+            > "$GRAFT_REPO_ROOT/gpurun_out/prof_stark_bench.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/prof_stark.err"
+        rc=$?
+        cd "$GRAFT_REPO_ROOT"
+        ok_or_stop $rc "rocprofv3 stark"
+        ;;
     prof)
         cd /tmp
         timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run \

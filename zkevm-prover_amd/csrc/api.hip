@@ -6,6 +6,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "gl_device.hpp"
 #include "zkgpu_internal.hpp"
 
@@ -543,6 +546,49 @@ int zkgpu_rand_cols_dev(uint64_t *base, uint64_t ld, const uint32_t *cols, uint3
     return rand_cols(base, ld, (const uint32_t *)p, ncols, nrows, seed, stream, g_ctx.stream);
 }
 
+// Temp-slot allocation for a ZXP program.  Program producers (the synthetic
+// builder, a chelpers converter) may give every intermediate its own temp;
+// the LDS footprint per workgroup is (slots x 64 rows x 8 B), which bounds
+// occupancy.  Each temp identity lives over [first occurrence, last
+// occurrence]; a linear scan packs the intervals of each pool (base / ext)
+// into the fewest slots.  An interval may start at the instruction where
+// another ends: the interpreter loads both sources before it stores the
+// destination.  The operand table is rewritten (duplicates are harmless).
+static void zxp_alloc_slots(const zxp_instr *in, uint32_t n_instr, std::vector<zxp_operand> &op, uint32_t &n_tmp1,
+                            uint32_t &n_tmp3)
+{
+    for (int pool = 0; pool < 2; pool++) {
+        const uint32_t kind = pool ? ZXP_TMP3 : ZXP_TMP1;
+        const uint32_t n_id = pool ? n_tmp3 : n_tmp1;
+        std::vector<uint32_t> first(n_id, UINT32_MAX), last(n_id, 0);
+        for (uint32_t k = 0; k < n_instr; k++) {
+            const uint32_t refs[3] = {in[k].dst, in[k].a, in[k].op == ZXP_COPY ? in[k].a : in[k].b};
+            for (uint32_t r : refs)
+                if (op[r].kind == kind) {
+                    const uint32_t id = op[r].a;
+                    first[id] = std::min(first[id], k);
+                    last[id] = std::max(last[id], k);
+                }
+        }
+        std::vector<uint32_t> order;
+        for (uint32_t id = 0; id < n_id; id++)
+            if (first[id] != UINT32_MAX) order.push_back(id);
+        std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return first[x] < first[y]; });
+        std::vector<uint32_t> slot_of(n_id, 0), slot_end;
+        for (uint32_t id : order) {
+            uint32_t s = 0;
+            while (s < slot_end.size() && slot_end[s] > first[id]) s++;
+            if (s == slot_end.size()) slot_end.push_back(0);
+            slot_end[s] = last[id];
+            slot_of[id] = s;
+        }
+        for (auto &o : op)
+            if (o.kind == kind) o.a = slot_of[o.a];
+        const uint32_t used = (uint32_t)std::max<size_t>(slot_end.size(), 1);
+        (pool ? n_tmp3 : n_tmp1) = used;
+    }
+}
+
 int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd, uint32_t n_tmp1,
                        uint32_t n_tmp3, const zkgpu_sections *sections, uint32_t log_dom, const uint64_t *challenges,
                        const uint64_t *publics, uint32_t n_publics, const uint64_t *evals, uint32_t n_evals,
@@ -582,6 +628,9 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
         }
         if (bad) return set_error(ZKGPU_ERR_ARG, "zxp: operand %u (kind %u) invalid", k, o.kind);
     }
+    std::vector<zxp_operand> opv(op, op + n_opnd);
+    zxp_alloc_slots(in, n_instr, opv, n_tmp1, n_tmp3);
+    opnd = opv.data();
     const uint32_t n_logz = extend_bits;
     const size_t zh = (size_t)1 << n_logz;
     size_t off_instr = 0, off_opnd = off_instr + ((n_instr * 16 + 15) & ~15ULL);

@@ -93,12 +93,13 @@ class Program:
 
 class SyntheticStark:
     def __init__(self, n_bits=10, blowup_bits=1, t=4, m=2, n_k=3, n_queries=16, fri_steps=None, n_publics=8,
-                 seed=0x5EED):
+                 seed=0x5EED, n_free=0):
         self.n_bits = n_bits
         self.n_bits_ext = n_bits + blowup_bits
         self.blowup_bits = blowup_bits
         self.t, self.m, self.n_k = t, m, n_k
-        self.n_cm1 = 3 * t
+        self.n_free = n_free  # extra free (unconstrained, random) committed columns
+        self.n_cm1 = 3 * t + n_free
         self.n_cm2 = 3 * m
         self.n_cm3 = 3 * m
         self.n_tmp = 6 * m
@@ -304,12 +305,12 @@ class SyntheticStark:
             "friSteps": self.fri_steps, "nCm1": self.n_cm1, "nCm2": self.n_cm2, "nCm3": self.n_cm3,
             "nCm4": self.n_cm4, "nTmp": self.n_tmp, "nConst": self.n_const, "nPublics": self.n_publics,
             "qDeg": self.q_deg, "qDim": self.q_dim, "lFirst": self.l_first, "seed": self.seed,
-            "randomCm1Cols": [c for c in range(self.n_cm1) if c % 3 != 2],
+            "randomCm1Cols": self.random_cm1_cols(),
             "zCtx": self.z_ctx, "evMap": self.evmap,
         }
 
     def random_cm1_cols(self):
-        return [c for c in range(self.n_cm1) if c % 3 != 2]
+        return [c for c in range(self.n_cm1) if c >= 3 * self.t or c % 3 != 2]
 
 
 # ---------------------------------------------------------------- PRNG
