@@ -69,6 +69,25 @@ int main()
     zkgpu::MerklehashGoldilocks::root(root, nodes.data(), ne);
     expect(memcmp(root, &nref[ne - 4], 32) == 0, "MerklehashGoldilocks::root");
 
+    // --- MerkleTreeGL as starks.hpp:186 builds it, getGroupProof as friProve.cpp queries
+    {
+        zkgpu::MerkleTreeGLT<Element> tree(H, W, src.data());
+        tree.merkelize();
+        Element r2[4];
+        tree.getRoot(r2);
+        expect(memcmp(r2, &nref[ne - 4], 32) == 0, "MerkleTreeGL::merkelize/getRoot");
+        const uint64_t plen = W + 4 * tree.MerkleProofSize();
+        std::vector<Element> pr(plen);
+        std::vector<uint64_t> prr(W + 4 * oc_merkle_proof_size(H));
+        bool ok = plen == prr.size();
+        for (uint64_t idx : {0ULL, 1ULL, 777ULL, (unsigned long long)H - 1}) {
+            tree.getGroupProof(pr.data(), idx);
+            oc_merkle_group_proof(prr.data(), nref.data(), (uint64_t *)src.data(), W, H, idx);
+            ok = ok && memcmp(pr.data(), prr.data(), plen * 8) == 0;
+        }
+        expect(ok, "MerkleTreeGL::getGroupProof");
+    }
+
     printf("%s\n", failures ? "FAILED" : "ALL OK");
     return failures ? 1 : 0;
 }

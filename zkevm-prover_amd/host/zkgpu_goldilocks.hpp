@@ -19,6 +19,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <string.h>
+
 #include <type_traits>
 
 #include "../../include/zkgpu.h"
@@ -157,6 +159,74 @@ struct MerklehashGoldilocks {
     static void root(E *out, E *tree, uint64_t numElementsTree)
     {
         for (int i = 0; i < 4; i++) out[i] = tree[numElementsTree - 4 + i];
+    }
+};
+
+// MerkleTreeGL -- merkleTreeGL.hpp:8-80 / merkleTreeGL.cpp:5-48.  Same members,
+// constructors and host-memory semantics (source row-major height x width,
+// nodes in the reference layout), so Starks (starks.hpp:186-190) and
+// FRIProve (friProve.cpp) use it unchanged; merkelize() runs on the GPU.
+template <typename E>
+class MerkleTreeGLT
+{
+public:
+    uint64_t height = 0;
+    uint64_t width = 0;
+    E *source = nullptr;
+    E *nodes = nullptr;
+    bool isSourceAllocated = false;
+    bool isNodesAllocated = false;
+
+    MerkleTreeGLT() {}
+    // constant-tree file image: [width, height, source..., nodes...]
+    explicit MerkleTreeGLT(E *tree)
+    {
+        width = u64p(tree)[0];
+        height = u64p(tree)[1];
+        source = &tree[2];
+        nodes = &tree[2 + height * width];
+    }
+    MerkleTreeGLT(uint64_t _height, uint64_t _width, E *_source) : height(_height), width(_width), source(_source)
+    {
+        if (source == nullptr) {
+            source = (E *)calloc(height * width, sizeof(E));
+            isSourceAllocated = true;
+        }
+        nodes = (E *)calloc(getTreeNumElements(), sizeof(E));
+        isNodesAllocated = true;
+    }
+    ~MerkleTreeGLT()
+    {
+        if (isSourceAllocated) free(source);
+        if (isNodesAllocated) free(nodes);
+    }
+    MerkleTreeGLT(const MerkleTreeGLT &) = delete;
+    MerkleTreeGLT &operator=(const MerkleTreeGLT &) = delete;
+
+    void copySource(E *_source) { memcpy(source, _source, height * width * sizeof(E)); }
+    void merkelize() { PoseidonGoldilocks::merkletree(nodes, source, width, height); }
+    uint64_t getTreeNumElements() { return height * 4 + (height - 1) * 4; }
+    void getRoot(E *root) { memcpy(root, &nodes[getTreeNumElements() - 4], 4 * sizeof(E)); }
+    // values of row idx followed by one sibling digest per level (leaves up)
+    void getGroupProof(E *proof, uint64_t idx)
+    {
+        memcpy(proof, &source[idx * width], width * sizeof(E));
+        E *p = proof + width;
+        uint64_t offset = 0, n = height * 4;  // elements on this level (genMerkleProof)
+        while (n > 4) {
+            memcpy(p, &nodes[offset + (idx ^ 1) * 4], 4 * sizeof(E));
+            p += 4;
+            const uint64_t next = ((n - 1) / 8 + 1) * 4;
+            offset += next * 2;
+            n = next;
+            idx >>= 1;
+        }
+    }
+    uint64_t MerkleProofSize()
+    {
+        uint64_t s = 0;
+        for (uint64_t n = 1; n < height; n <<= 1) s++;  // ceil(log2(height))
+        return s;
     }
 };
 
