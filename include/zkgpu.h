@@ -171,6 +171,17 @@ int zkgpu_ext_powers_dev(uint64_t *out, uint64_t ld, const uint64_t base[3], uin
 int zkgpu_qsplit_dev(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t q_deg,
                      uint64_t shift_in);
 
+/* plookup h1/h2 (Polinomial::calculateH1H2_opt1 / _opt3, polinomial.hpp:349-583,
+ * called at starks.cpp:104-127): f, t, h1, h2 are n-row columns of dimension
+ * dim (1, or 3 = three column-major components ld apart).  Every table row
+ * starts with multiplicity 1; each f value adds one to the LAST table row with
+ * the same (canonical) value; the multiset in table order is dealt
+ * alternately into h1 and h2.  An f value absent from t returns ZKGPU_ERR_ARG
+ * ("Number not included", the reference exits) with *missing_row = the first
+ * such f row; otherwise *missing_row = UINT64_MAX. */
+int zkgpu_h1h2_dev(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint64_t *f, uint64_t f_ld,
+                   const uint64_t *t, uint64_t t_ld, uint64_t n, uint32_t dim, uint64_t *missing_row);
+
 /* 3 ext columns (ld) -> interleaved n x 3 (the FRI polynomial layout, friProve.cpp) */
 int zkgpu_cols3_to_interleaved_dev(uint64_t *out, const uint64_t *cols, uint64_t ld, uint64_t n);
 

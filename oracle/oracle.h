@@ -112,6 +112,9 @@ void oc_powers(uint64_t *out, uint64_t start, uint64_t w, uint64_t n);
 
 /* ---- misc ---- */
 void oc_batch_inverse3(uint64_t *out, const uint64_t *in, uint64_t n); /* Polinomial::batchInverse */
+/* ---- plookup h1/h2 (h1h2.c): returns 0, or 1 + first f row not in t ---- */
+uint64_t oc_h1h2(uint64_t *h1, uint64_t h1s, uint64_t *h2, uint64_t h2s, const uint64_t *f, uint64_t fs,
+                 const uint64_t *t, uint64_t ts, uint64_t n, uint32_t dim);
 int oc_num_threads(void);
 void oc_set_num_threads(int n);
 

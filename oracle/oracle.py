@@ -70,6 +70,7 @@ def lib():
                                 ptr, u64, ctypes.c_uint32]),
             "oc_xdivxsub": (None, [ptr, ptr, ptr, u64, ptr, u64]),
             "oc_powers": (None, [ptr, u64, u64, u64]),
+            "oc_h1h2": (u64, [ptr, u64, ptr, u64, ptr, u64, ptr, u64, u64, ctypes.c_uint32]),
             "oc_num_threads": (ctypes.c_int, []),
             "oc_set_num_threads": (None, [ctypes.c_int]),
         }
@@ -111,6 +112,20 @@ def gl3_inv(a):
     o = np.zeros(3, np.uint64)
     lib().oc_gl3_inv(_p(o), _p(a))
     return o
+
+
+def h1h2(f, t):
+    """Plookup h1/h2 (calculateH1H2_opt1/opt3): f, t are (n,) or (n, 3).
+    Returns (h1, h2), or raises ValueError naming the first f row not in t."""
+    f, t = u64(f), u64(t)
+    n = t.shape[0]
+    dim = 1 if t.ndim == 1 else t.shape[1]
+    h1 = np.zeros_like(t)
+    h2 = np.zeros_like(t)
+    miss = lib().oc_h1h2(_p(h1), dim, _p(h2), dim, _p(f), dim, _p(t), dim, n, dim)
+    if miss:
+        raise ValueError("Number not included: w=%d" % (miss - 1))
+    return h1, h2
 
 
 # ---------------------------------------------------------------- NTT

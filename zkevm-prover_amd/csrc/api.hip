@@ -775,6 +775,20 @@ int zkgpu_qsplit_dev(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t 
     return qsplit(qq2, ld2, qq1, ld1, n, q_deg, shift_in, g_ctx.stream);
 }
 
+int zkgpu_h1h2_dev(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint64_t *f, uint64_t f_ld,
+                   const uint64_t *t, uint64_t t_ld, uint64_t n, uint32_t dim, uint64_t *missing_row)
+{
+    int rc;
+    if (missing_row) *missing_row = ~0ULL;
+    if ((rc = require_init())) return rc;
+    if (dim != 1 && dim != 3) return set_error(ZKGPU_ERR_ARG, "h1h2: dim must be 1 or 3");
+    if (n > 0x7FFFFFFFULL) return set_error(ZKGPU_ERR_ARG, "h1h2: n too large");
+    if (dim == 3 && (h1_ld < n || h2_ld < n || f_ld < n || t_ld < n))
+        return set_error(ZKGPU_ERR_ARG, "h1h2: ld < n");
+    if (!n) return 0;
+    return h1h2(h1, h1_ld, h2, h2_ld, f, f_ld, t, t_ld, n, dim, missing_row, g_ctx.stream);
+}
+
 int zkgpu_cols3_to_interleaved_dev(uint64_t *out, const uint64_t *cols, uint64_t ld, uint64_t n)
 {
     int rc;

@@ -1,0 +1,187 @@
+// Plookup h1/h2 columns on the GPU: Polinomial::calculateH1H2_opt1 (dim 1,
+// polinomial.hpp:349-463) / calculateH1H2_opt3 (dim 3, :465-583), called per
+// plookup from Starks::genProof stage 2 (starks.cpp:104-127).
+//
+// The reference builds a chained hash table of the table column t (each key
+// remembers its LAST row), counts every f value onto that row, and deals the
+// resulting multiset (t[j] repeated 1 + count_j times, in t order) alternately
+// into h1 and h2.  The same mapping, data-parallel:
+//   1. perm = stable radix sort of row indices by the canonical key
+//      (dim 3: three stable LSD passes, component 2 first, so the order is
+//      lexicographic (k0, k1, k2) with equal keys in ascending row order);
+//   2. one thread per f row: upper_bound in the sorted keys, step back one
+//      -> the last table row with that key; atomicAdd on its count
+//      (counts start at 1); a key that is absent records the smallest such
+//      row ("Number not included");
+//   3. exclusive scan of the counts = start position of each t row in the
+//      2N-long multiset;
+//   4. one thread per multiset slot s: j = upper_bound(start, s) - 1,
+//      h_{1 + (s & 1)}[s >> 1] = t[j]  (raw copy, like copyElement).
+// Columns are column-major: component c of a dim-3 column at ptr + c * ld.
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include "gl_device.hpp"
+#include "zkgpu_internal.hpp"
+
+namespace zk {
+
+static inline uint32_t nblk2(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
+
+__global__ void k_h12_iota(uint32_t *v, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = (uint32_t)i;
+}
+
+// out[r] = canon(col[perm[r]])  (perm = null: identity)
+__global__ void k_h12_gather(uint64_t *out, const uint64_t *col, const uint32_t *perm, uint64_t n)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n) out[r] = gl_canon(col[perm ? perm[r] : r]);
+}
+
+__global__ void k_h12_fill1(uint32_t *c, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) c[i] = 1;
+}
+
+template <int DIM>
+__device__ __forceinline__ int h12_cmp(const uint64_t *sk, uint64_t n, uint64_t r, const uint64_t *key)
+{
+#pragma unroll
+    for (int c = 0; c < DIM; c++) {
+        const uint64_t v = sk[c * n + r];
+        if (v < key[c]) return -1;
+        if (v > key[c]) return 1;
+    }
+    return 0;
+}
+
+// sk: DIM sorted key columns (ld n); perm: sorted position -> table row
+template <int DIM>
+__global__ void k_h12_count(const uint64_t *f, uint64_t f_ld, const uint64_t *sk, const uint32_t *perm, uint64_t n,
+                            uint32_t *cnt, unsigned long long *miss)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t key[DIM];
+#pragma unroll
+    for (int c = 0; c < DIM; c++) key[c] = gl_canon(f[c * f_ld + i]);
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (h12_cmp<DIM>(sk, n, mid, key) <= 0)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    if (lo == 0 || h12_cmp<DIM>(sk, n, lo - 1, key) != 0) {
+        atomicMin(miss, (unsigned long long)i);
+        return;
+    }
+    atomicAdd(&cnt[perm[lo - 1]], 1u);
+}
+
+template <int DIM>
+__global__ void k_h12_deal(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint64_t *t, uint64_t t_ld,
+                           const uint32_t *start, uint64_t n)
+{
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= 2 * n) return;
+    uint64_t lo = 0, hi = n;  // upper_bound(start, s)
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if ((uint64_t)start[mid] <= s)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    const uint64_t j = lo - 1;
+    uint64_t *h = (s & 1) ? h2 : h1;
+    const uint64_t ld = (s & 1) ? h2_ld : h1_ld;
+#pragma unroll
+    for (int c = 0; c < DIM; c++) h[c * ld + (s >> 1)] = t[c * t_ld + j];
+}
+
+int h1h2(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint64_t *f, uint64_t f_ld,
+         const uint64_t *t, uint64_t t_ld, uint64_t n, uint32_t dim, uint64_t *missing_row, hipStream_t s)
+{
+    // scratch: keys_in, keys_out (n u64 each), sk (dim n u64; sk[0] = keys_out
+    // of the last pass), perm_in, perm_out, cnt (n u32 each), miss (u64)
+    const size_t kb = n * sizeof(uint64_t), pb = n * sizeof(uint32_t);
+    const size_t need = 2 * kb + 2 * kb /* sk[1], sk[2] */ + 3 * pb + 16;
+    char *w = (char *)workspace(4, need);
+    if (!w) return ZKGPU_ERR_OOM;
+    uint64_t *keys_in = (uint64_t *)w;
+    uint64_t *keys_out = keys_in + n;
+    uint64_t *sk12 = keys_out + n;  // components 1, 2 of the sorted keys
+    uint32_t *perm_in = (uint32_t *)(sk12 + 2 * n);
+    uint32_t *perm_out = perm_in + n;
+    uint32_t *cnt = perm_out + n;
+    unsigned long long *miss = (unsigned long long *)(((uintptr_t)(cnt + n) + 7) & ~(uintptr_t)7);
+
+    // temp storage for the sort and the scan (sized once for both)
+    size_t sort_bytes = 0, scan_bytes = 0;
+    if (rocprim::radix_sort_pairs(nullptr, sort_bytes, keys_in, keys_out, perm_in, perm_out, (unsigned int)n, 0, 64, s) !=
+            hipSuccess ||
+        rocprim::exclusive_scan(nullptr, scan_bytes, cnt, perm_in, 0u, (size_t)n, rocprim::plus<uint32_t>(), s) !=
+            hipSuccess)
+        return set_error(ZKGPU_ERR_HIP, "h1h2: rocprim temp-size query failed");
+    void *tmp = workspace(5, sort_bytes > scan_bytes ? sort_bytes : scan_bytes);
+    if (!tmp) return ZKGPU_ERR_OOM;
+    size_t tmp_bytes = sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
+
+    const uint32_t B = 256;
+    prof_begin(s);
+    hipLaunchKernelGGL(k_h12_iota, dim3(nblk2(n, B)), dim3(B), 0, s, perm_in, n);
+    for (int c = (int)dim - 1; c >= 0; c--) {
+        hipLaunchKernelGGL(k_h12_gather, dim3(nblk2(n, B)), dim3(B), 0, s, keys_in, t + (uint64_t)c * t_ld,
+                           c == (int)dim - 1 ? (const uint32_t *)nullptr : perm_in, n);
+        size_t tb = tmp_bytes;
+        if (rocprim::radix_sort_pairs(tmp, tb, keys_in, keys_out, perm_in, perm_out, (unsigned int)n, 0, 64, s) !=
+            hipSuccess)
+            return set_error(ZKGPU_ERR_HIP, "h1h2: radix sort failed");
+        uint32_t *x = perm_in;
+        perm_in = perm_out;
+        perm_out = x;
+    }
+    // perm_in = sorted position -> table row; keys_out = component 0 sorted
+    for (uint32_t c = 1; c < dim; c++)
+        hipLaunchKernelGGL(k_h12_gather, dim3(nblk2(n, B)), dim3(B), 0, s, sk12 + (uint64_t)(c - 1) * n,
+                           t + (uint64_t)c * t_ld, perm_in, n);
+    // the count kernel indexes components as sk[c * n + r]: lay them out contiguously
+    uint64_t *sk = keys_out;  // keys_out, sk12[0..n), sk12[n..2n) are contiguous (keys_out + n == sk12)
+    hipLaunchKernelGGL(k_h12_fill1, dim3(nblk2(n, B)), dim3(B), 0, s, cnt, n);
+    (void)hipMemsetAsync(miss, 0xFF, 8, s);
+    if (dim == 1)
+        hipLaunchKernelGGL(k_h12_count<1>, dim3(nblk2(n, B)), dim3(B), 0, s, f, f_ld, sk, perm_in, n, cnt, miss);
+    else
+        hipLaunchKernelGGL(k_h12_count<3>, dim3(nblk2(n, B)), dim3(B), 0, s, f, f_ld, sk, perm_in, n, cnt, miss);
+    uint32_t *start = perm_out;  // free now
+    {
+        size_t tb = tmp_bytes;
+        if (rocprim::exclusive_scan(tmp, tb, cnt, start, 0u, (size_t)n, rocprim::plus<uint32_t>(), s) != hipSuccess)
+            return set_error(ZKGPU_ERR_HIP, "h1h2: scan failed");
+    }
+    unsigned long long mh = 0;
+    if (check_hip(hipMemcpyAsync(&mh, miss, 8, hipMemcpyDeviceToHost, s), "D2H") ||
+        check_hip(hipStreamSynchronize(s), "h1h2 sync"))
+        return ZKGPU_ERR_HIP;
+    if (mh != ~0ULL) {
+        if (missing_row) *missing_row = mh;
+        return set_error(ZKGPU_ERR_ARG, "calculateH1H2: Number not included: w=%llu", mh);
+    }
+    if (missing_row) *missing_row = ~0ULL;
+    if (dim == 1)
+        hipLaunchKernelGGL(k_h12_deal<1>, dim3(nblk2(2 * n, B)), dim3(B), 0, s, h1, h1_ld, h2, h2_ld, t, t_ld, start,
+                           n);
+    else
+        hipLaunchKernelGGL(k_h12_deal<3>, dim3(nblk2(2 * n, B)), dim3(B), 0, s, h1, h1_ld, h2, h2_ld, t, t_ld, start,
+                           n);
+    prof_end("k_h1h2", (double)dim * 8.0 * 4.0 * n, s);
+    return check_launch("h1h2");
+}
+
+}  // namespace zk

@@ -32,7 +32,7 @@ struct Ctx {
     uint64_t *post_lo = nullptr;
     uint64_t *post_hi = nullptr;
     // scratch workspaces
-    Workspace ws[4];
+    Workspace ws[6];  // 0-3 NTT / staging, 4 H1H2 scratch, 5 rocPRIM temp
     // Poseidon constants on device
     uint64_t *poseidon_rc = nullptr;
 };
@@ -107,6 +107,8 @@ int ext_powers(uint64_t *out, uint64_t ld, const uint64_t base[3], uint64_t n, h
 int qsplit(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t qdeg,
            uint64_t shift_in, hipStream_t s);
 int cols3_to_interleaved(uint64_t *out, const uint64_t *cols, uint64_t ld, uint64_t n, hipStream_t s);
+int h1h2(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint64_t *f, uint64_t f_ld,
+         const uint64_t *t, uint64_t t_ld, uint64_t n, uint32_t dim, uint64_t *missing_row, hipStream_t s);
 int merkle_open_strided(uint64_t *vals, uint64_t *sibs, const uint64_t *nodes, const uint64_t *src, uint64_t ncols,
                         uint64_t nrows, uint64_t row_stride, uint64_t col_stride, const uint64_t *idx, uint64_t nq,
                         hipStream_t s);

@@ -73,6 +73,7 @@ _SIGS = {
     "zkgpu_ext_powers_dev": (ctypes.c_int, [vp, u64, vp, u64]),
     "zkgpu_qsplit_dev": (ctypes.c_int, [vp, u64, vp, u64, u64, u32, u64]),
     "zkgpu_cols3_to_interleaved_dev": (ctypes.c_int, [vp, vp, u64, u64]),
+    "zkgpu_h1h2_dev": (ctypes.c_int, [vp, u64, vp, u64, vp, u64, vp, u64, u64, u32, pu64]),
     "zkgpu_gl_merkle_open_rows_dev": (ctypes.c_int, [vp, vp, vp, vp, u64, u64, vp, u64]),
     "zkgpu_prof_enable": (ctypes.c_int, [ctypes.c_int]),
     "zkgpu_prof_reset": (ctypes.c_int, []),
@@ -318,6 +319,18 @@ def zxp_eval_dev(prog, sections, log_dom, challenges, publics, evals=None, xdiv=
                                     max(nt3, 1), ctypes.byref(s), log_dom, ch.ctypes.data, pub.ctypes.data,
                                     pub.size if publics is not None else 0, ev.ctypes.data, ev.size // 3,
                                     _addr(xdiv), _addr(xdivw), extend_bits, x_start), "zkgpu_zxp_eval_dev")
+
+
+def h1h2_dev(h1, h1_ld, h2, h2_ld, f, f_ld, t, t_ld, n, dim):
+    """Plookup h1/h2 on device columns.  Returns None, or the first f row whose
+    value is not in t (the call then fails with "Number not included")."""
+    miss = ctypes.c_uint64(0)
+    rc = lib().zkgpu_h1h2_dev(_addr(h1), h1_ld, _addr(h2), h2_ld, _addr(f), f_ld, _addr(t), t_ld, n, dim,
+                              ctypes.byref(miss))
+    if rc != 0 and miss.value != (1 << 64) - 1:
+        return miss.value
+    _check(rc, "zkgpu_h1h2_dev")
+    return None
 
 
 def qsplit_dev(qq2, ld2, qq1, ld1, n, q_deg, shift_in):
