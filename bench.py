@@ -97,9 +97,12 @@ def stark_instance(log_n, blow, ncols, n_queries):
         steps.append(steps[-1] - 4)
     if steps[-1] > 5:
         steps.append(5)
-    t = ncols // 3
-    return SyntheticStark(n_bits=log_n, blowup_bits=blow, t=t, n_free=ncols - 3 * t, m=8, n_k=29,
-                          n_queries=n_queries, fri_steps=steps)
+    # cm1 = 3t constrained triples + free columns + 3 lookup columns (A, B, C);
+    # cm2 = 6 h groups (18) + plookup h1/h2 (3+3+1+1) = 26, cm3 = 18 + 2 plookup Z = 24,
+    # constants = 26 K + L_first + 3 tables = 30
+    t = (ncols - 3) // 3
+    return SyntheticStark(n_bits=log_n, blowup_bits=blow, t=t, n_free=ncols - 3 - 3 * t, m=6, n_k=26,
+                          n_queries=n_queries, fri_steps=steps, n_lookups=2)
 
 
 def cpu_baseline_stark(sample_bits, log_n, blow, ncols, n_queries):
@@ -244,9 +247,10 @@ def main():
                         % (args.log_n, C))
         else:
             workload = ("full STARK proof (genProof stages 1-5 + FRI + queries, starks.cpp:9-404), synthetic "
-                        "config-4 instance: 2^%d trace, blowup 2^%d, cm1/cm2/cm3/cm4 = %d/24/24/6, 30 constants, "
-                        "FRI steps %s, %d queries; one independent proof per GPU"
-                        % (args.log_n, args.blowup_bits, C, inst.fri_steps, args.queries))
+                        "config-4 instance: 2^%d trace, blowup 2^%d, cm1/cm2/cm3/cm4 = %d/%d/%d/%d, %d constants, "
+                        "2 plookups (dim 3 + dim 1), FRI steps %s, %d queries; one independent proof per GPU"
+                        % (args.log_n, args.blowup_bits, inst.n_cm1, inst.n_cm2, inst.n_cm3, inst.n_cm4,
+                           inst.n_const, inst.fri_steps, args.queries))
         res = {
             "metric": METRIC,
             "value": round(value, 4),

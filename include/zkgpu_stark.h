@@ -44,6 +44,17 @@ typedef struct {
     uint32_t n_ev;
     const uint32_t *ev; /* evMap (section_2ns, col, dim, prime) quads */
     zkgpu_zxp_prog step1, step2, step3prev, step42ns, step52ns;
+    /* constant polynomials (setup; the reference loads them from the
+     * zkevmConstPols file, starks.hpp:94-116): these columns are filled
+     * pseudo-randomly (n_random_const = 0: columns 0 .. n_k-1), l_first gets
+     * L_first, then step0 derives the rest on the N domain (may be empty) */
+    uint32_t n_random_const;
+    const uint32_t *random_const;
+    zkgpu_zxp_prog step0;
+    /* plookups (starkInfo.puCtx, starks.cpp:104-127): (f tmp col, t tmp col,
+     * h1 cm2 col, h2 cm2 col, dim) quintuples; h1/h2 are computed after step2 */
+    uint32_t n_pu;
+    const uint32_t *pu;
 } zkgpu_stark_info;
 
 /* allocate the HBM memory map, build the constant polynomials, their LDE and

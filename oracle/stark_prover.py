@@ -39,12 +39,9 @@ class OracleStark:
         S[4] = np.zeros((N, inst.n_const), np.uint64)
         self.S = S
         # constants (setup, like the reference's const pols + const tree files)
-        kcols = np.arange(inst.n_k, dtype=np.uint32)
-        L.oc_rand_cols(_p(S[4]), inst.n_const, _vp(kcols), inst.n_k, N, inst.seed, 1)
+        kcols = np.array(inst.random_const_cols(), dtype=np.uint32)
+        L.oc_rand_cols(_p(S[4]), inst.n_const, _vp(kcols), kcols.size, N, inst.seed, 1)
         S[4][0, inst.l_first] = 1
-        S[9] = oc.extend_pol(S[4], NE)
-        self.const_nodes = oc.merkletree(S[9])
-        self.verkey = self.const_nodes[-4:].copy()
         self.publics = np.array([L.oc_rand_u64(inst.seed, 2, k, 0) for k in range(inst.n_publics)], np.uint64)
         self.x_n = np.zeros(N, np.uint64)
         L.oc_powers(_p(self.x_n), 1, oc.gl_w(inst.n_bits), N)
@@ -54,6 +51,12 @@ class OracleStark:
         sn = pow(7, N, P)
         wE = oc.gl_w(self.eb)
         self.zhinv = np.array([pow((sn * pow(wE, i, P) - 1) % P, P - 2, P) for i in range(1 << self.eb)], np.uint64)
+        # derived constants (step0), then the constant LDE + tree -> verkey
+        if inst.programs["step0"].instr:
+            self.run(inst.programs["step0"], np.zeros(3 * 8, np.uint64), np.zeros(3, np.uint64))
+        S[9] = oc.extend_pol(S[4], NE)
+        self.const_nodes = oc.merkletree(S[9])
+        self.verkey = self.const_nodes[-4:].copy()
 
     # ------------------------------------------------------------ helpers
     def witness(self):
@@ -101,6 +104,13 @@ class OracleStark:
         ch[0] = t.get_field()
         ch[1] = t.get_field()
         self.run(inst.programs["step2"], ch, np.zeros(3, np.uint64))
+        # plookups: h1/h2 = calculateH1H2(f, t) (starks.cpp:104-127)
+        for f_c, t_c, h1_c, h2_c, d in inst.pu:
+            fcol = np.ascontiguousarray(S[3][:, f_c:f_c + d])
+            tcol = np.ascontiguousarray(S[3][:, t_c:t_c + d])
+            h1, h2 = oc.h1h2(fcol.reshape(-1) if d == 1 else fcol, tcol.reshape(-1) if d == 1 else tcol)
+            S[1][:, h1_c:h1_c + d] = h1.reshape(N, d)
+            S[1][:, h2_c:h2_c + d] = h2.reshape(N, d)
         S[6] = oc.extend_pol(S[1], NE)
         trees.append((oc.merkletree(S[6]), S[6]))
         roots.append(trees[-1][0][-4:].copy())

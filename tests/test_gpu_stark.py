@@ -58,6 +58,23 @@ def test_set_cm1_row_major_boundary(oracle, zkgpu):
     g.close()
 
 
+def test_lookup_value_not_in_table_fails_loudly(oracle, zkgpu):
+    """An f value outside the table stops the GPU prover with the reference's
+    "Number not included" error (polinomial.hpp:409-413)."""
+    from zkgpu.synthetic import SyntheticStark
+    from zkgpu.stark import GpuStark
+    from zkgpu import ZkgpuError
+    inst = SyntheticStark(n_bits=9, t=3, m=1, n_queries=8)
+    o, _ = oracle_proof(inst)
+    rows = o.S[0].copy()
+    rows[9, inst.cm1_lk[2]] = 12345
+    g = GpuStark(inst)
+    g.set_cm1(rows)
+    with pytest.raises(ZkgpuError, match="Number not included: w=9"):
+        g.prove()
+    g.close()
+
+
 def test_calculate_z_dev(oracle, zkgpu):
     import torch
     rng = np.random.default_rng(3)

@@ -79,6 +79,27 @@ def quotient_identity(inst, proof, ch):
         r = m3(m3(add3(E(S.SEC_CM2_2NS, 3 * j, 1), gamma), beta), E(S.SEC_CM3_2NS, 3 * j, 1))
         s = m3(m3(add3(E(S.SEC_CM2_2NS, 3 * j, 0), gamma), beta), E(S.SEC_CM3_2NS, 3 * j, 0))
         cons.append(sub3(r, s))
+    # plookups (pil-stark Plookup): L_first (Z - 1); Z' den - Z num
+    one = [1, 0, 0]
+    ob = add3(beta, one)
+    gb = m3(ob, gamma)
+    for k, lk in enumerate(inst.lookups):
+        cons.append(m3(sub3(E(S.SEC_CM3_2NS, lk["z"]), one), E(S.SEC_CONST_2NS, inst.l_first)))
+        d = lk["dim"]
+        if d == 3:
+            f = add3(E(S.SEC_CM1_2NS, inst.cm1_lk[0]), m3(u, E(S.SEC_CM1_2NS, inst.cm1_lk[1])))
+            t = add3(E(S.SEC_CONST_2NS, inst.c_t[0]), m3(u, E(S.SEC_CONST_2NS, inst.c_t[1])))
+            tn = add3(E(S.SEC_CONST_2NS, inst.c_t[0], 1), m3(u, E(S.SEC_CONST_2NS, inst.c_t[1], 1)))
+        else:
+            f = E(S.SEC_CM1_2NS, inst.cm1_lk[2])
+            t = E(S.SEC_CONST_2NS, inst.c_t[2])
+            tn = E(S.SEC_CONST_2NS, inst.c_t[2], 1)
+        h1, h2 = E(S.SEC_CM2_2NS, lk["h1"]), E(S.SEC_CM2_2NS, lk["h2"])
+        h1n = E(S.SEC_CM2_2NS, lk["h1"], 1)
+        num = m3(m3(ob, add3(f, gamma)), add3(add3(gb, t), m3(beta, tn)))
+        den = m3(add3(add3(gb, h1), m3(beta, h2)), add3(add3(gb, h2), m3(beta, h1n)))
+        z, zn = E(S.SEC_CM3_2NS, lk["z"]), E(S.SEC_CM3_2NS, lk["z"], 1)
+        cons.append(sub3(m3(zn, den), m3(z, num)))
     C = cons[0]
     for c in cons[1:]:
         C = add3(m3(C, alpha), c)
@@ -123,3 +144,16 @@ def test_tampered_trace_breaks_validity(oracle):
     coef = oracle.ntt(fp, True)
     deg_bound = (1 << inst.fri_steps[-1]) >> 1
     assert coef[deg_bound:].any() or not quotient_identity(inst, proof, ch)
+
+
+def test_lookup_value_not_in_table_is_rejected(oracle):
+    """calculateH1H2 refuses an f value absent from the table ("Number not
+    included", polinomial.hpp:409-413), like the reference."""
+    from zkgpu.synthetic import SyntheticStark
+    from oracle.stark_prover import OracleStark
+    inst = SyntheticStark(n_bits=8, blowup_bits=1, t=4, m=2, n_queries=8)
+    o = OracleStark(inst)
+    o.witness()
+    o.S[0][9, inst.cm1_lk[2]] = 12345  # not a T2 value
+    with pytest.raises(ValueError, match="Number not included: w=9"):
+        o.prove()

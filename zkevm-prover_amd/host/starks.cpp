@@ -149,9 +149,9 @@ class Starks
 {
 public:
     zkgpu_stark_info info;
-    std::vector<uint32_t> random_cols, zctx, ev;
+    std::vector<uint32_t> random_cols, zctx, ev, random_const, pu;
     std::vector<uint32_t> fri_steps;
-    Prog step1, step2, step3prev, step42ns, step52ns;
+    Prog step0, step1, step2, step3prev, step42ns, step52ns;
     uint64_t N = 0, NE = 0;
     uint32_t eb = 0;
     zkgpu_sections S;
@@ -186,6 +186,21 @@ public:
         zctx.assign(in->zctx, in->zctx + 3 * in->n_zctx);
         ev.assign(in->ev, in->ev + 4 * in->n_ev);
         fri_steps.assign(in->fri_steps, in->fri_steps + in->n_fri_steps);
+        if (in->n_random_const)
+            random_const.assign(in->random_const, in->random_const + in->n_random_const);
+        else
+            for (uint32_t k = 0; k < in->n_k; k++) random_const.push_back(k);
+        pu.assign(in->pu, in->pu + 5 * in->n_pu);
+        for (uint32_t k = 0; k < in->n_pu; k++) {
+            const uint32_t *q = &pu[5 * k];
+            const uint32_t d = q[4];
+            if ((d != 1 && d != 3) || q[0] + d > in->n_tmp || q[1] + d > in->n_tmp || q[2] + d > in->n_cm2 ||
+                q[3] + d > in->n_cm2)
+                return fail("stark_create: plookup %u out of range", k);
+        }
+        for (uint32_t c : random_const)
+            if (c >= in->n_const) return fail("stark_create: random const column %u out of range", c);
+        step0.set(in->step0);
         step1.set(in->step1);
         step2.set(in->step2);
         step3prev.set(in->step3prev);
@@ -229,13 +244,17 @@ public:
             if (dalloc(&fri_aux[si], len) || dalloc(&fri_nodes[si], zkgpu_gl_merkle_num_elements(1ULL << fri_steps[si])))
                 return -1;
         }
-        // constants (setup): K_k pseudo-random, L_first = [1, 0, ...]
-        std::vector<uint32_t> kc(in->n_k);
-        for (uint32_t k = 0; k < in->n_k; k++) kc[k] = k;
+        // constants (setup): pseudo-random columns, L_first = [1, 0, ...], then step0
         CK(zkgpu_memset_dev(S.sec[SEC_CONST_N], 0, (uint64_t)in->n_const * N * 8));
-        CK(zkgpu_rand_cols_dev(S.sec[SEC_CONST_N], N, kc.data(), in->n_k, N, in->seed, 1));
+        if (!random_const.empty())
+            CK(zkgpu_rand_cols_dev(S.sec[SEC_CONST_N], N, random_const.data(), (uint32_t)random_const.size(), N,
+                                   in->seed, 1));
         uint64_t one = 1;
         CK(zkgpu_memcpy_h2d(S.sec[SEC_CONST_N] + (uint64_t)in->l_first * N, &one, 8));
+        if (!step0.instr.empty()) {
+            uint64_t ch0[24] = {0}, ev0[3] = {0, 0, 0};
+            if (run(step0, false, ch0, ev0, 0)) return -1;
+        }
         CK(zkgpu_gl_extend_pol_dev(S.sec[SEC_CONST_2NS], NE, S.sec[SEC_CONST_N], N, NE, N, in->n_const));
         CK(zkgpu_gl_merkletree_dev(const_nodes, S.sec[SEC_CONST_2NS], NE, in->n_const, NE));
         CK(zkgpu_memcpy_d2h(verkey, const_nodes + tn - 4, 32));
@@ -332,6 +351,24 @@ public:
         tstart();
         if (run(step2, false, ch, evals.data(), 0)) return -1;
         if (tstop("STARK_STEP_2_CALCULATE_EXPS")) return -1;
+        if (info.n_pu) {
+            tstart();
+            for (uint32_t k = 0; k < info.n_pu; k++) {
+                const uint32_t *q = &pu[5 * k];
+                uint64_t miss = 0;
+                const int rc = zkgpu_h1h2_dev(S.sec[SEC_CM2_N] + (uint64_t)q[2] * N, N,
+                                              S.sec[SEC_CM2_N] + (uint64_t)q[3] * N, N,
+                                              S.sec[SEC_TMP_N] + (uint64_t)q[0] * N, N,
+                                              S.sec[SEC_TMP_N] + (uint64_t)q[1] * N, N, N, q[4], &miss);
+                if (rc) {
+                    if (miss != ~0ULL)
+                        return fail("Polinomial::calculateH1H2() Number not included: w=%llu plookup_number=%u",
+                                    (unsigned long long)miss, k);
+                    return fail("calculateH1H2: %s", zkgpu_last_error());
+                }
+            }
+            if (tstop("STARK_STEP_2_CALCULATEH1H2")) return -1;
+        }
         if (commit(1, SEC_CM2_N, SEC_CM2_2NS, info.n_cm2, tr, roots[1], "STARK_STEP_2_LDE", "STARK_STEP_2_MERKLETREE"))
             return -1;
         // STAGE 3 (:146-224)

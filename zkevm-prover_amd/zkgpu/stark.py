@@ -32,7 +32,9 @@ class _Info(ctypes.Structure):
                 ("n_random_cols", ctypes.c_uint32), ("random_cols", ctypes.c_void_p),
                 ("n_zctx", ctypes.c_uint32), ("zctx", ctypes.c_void_p),
                 ("n_ev", ctypes.c_uint32), ("ev", ctypes.c_void_p),
-                ("step1", _Prog), ("step2", _Prog), ("step3prev", _Prog), ("step42ns", _Prog), ("step52ns", _Prog)]
+                ("step1", _Prog), ("step2", _Prog), ("step3prev", _Prog), ("step42ns", _Prog), ("step52ns", _Prog),
+                ("n_random_const", ctypes.c_uint32), ("random_const", ctypes.c_void_p), ("step0", _Prog),
+                ("n_pu", ctypes.c_uint32), ("pu", ctypes.c_void_p)]
 
 
 _slib = None
@@ -85,11 +87,15 @@ class GpuStark:
         rc = np.array(inst.random_cm1_cols(), np.uint32)
         zc = np.array(inst.z_ctx, np.uint32).reshape(-1)
         ev = np.array(inst.evmap, np.uint32).reshape(-1)
-        self._keep += [rc, zc, ev]
+        rk = np.array(inst.random_const_cols(), np.uint32)
+        pu = np.array(inst.pu, np.uint32).reshape(-1)
+        self._keep += [rc, zc, ev, rk, pu]
+        info.n_random_const, info.random_const = rk.size, rk.ctypes.data
+        info.n_pu, info.pu = len(inst.pu), (pu.ctypes.data if pu.size else None)
         info.n_random_cols, info.random_cols = rc.size, rc.ctypes.data
         info.n_zctx, info.zctx = len(inst.z_ctx), zc.ctypes.data
         info.n_ev, info.ev = len(inst.evmap), ev.ctypes.data
-        for name in ("step1", "step2", "step3prev", "step42ns", "step52ns"):
+        for name in ("step0", "step1", "step2", "step3prev", "step42ns", "step52ns"):
             prog = inst.programs[name]
             ins, opn = prog.arrays()
             ins, opn = np.ascontiguousarray(ins), np.ascontiguousarray(opn)

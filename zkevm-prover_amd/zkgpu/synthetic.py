@@ -8,12 +8,20 @@ Starks::genProof (starks.cpp:9-404):
   constants  K_0..K_{nK-1} (pseudo-random), L_first (1 at row 0)
   stage 1    cm1 = 3t columns; a[3j], a[3j+1] pseudo-random,
              a[3j+2] = a[3j]*a[3j+1]*K_{j mod nK} + a[3j]             (degree 3)
+  lookups    n_lookups plookups (0..2) against constant tables:
+             #0 dim 3: (A, B) in (T0, T1) combined as f = A + u B, t = T0 + u T1
+             #1 dim 1: C in T2, T2 = T0 with row 0 replaced by T0[N/2] (a
+                duplicate value, so the "last table row" rule matters)
+             A, B, C are cm1 columns filled from the tables at shifted rows
   stage 2    challenges u = ch[0], defVal = ch[1];
-             m extension columns h_j = sum_k a[s_j+k] u^(k+1) + defVal (cm2, 3m cols)
+             m extension columns h_j = sum_k a[s_j+k] u^(k+1) + defVal (cm2, 3m cols);
+             plookup f/t into tmpExp, then h1/h2 = calculateH1H2(f, t) (cm2)
   stage 3    challenges gamma = ch[2], beta = ch[3];
              num_j = (h_j(x) + gamma) beta, den_j = (h_j(w x) + gamma) beta (tmpExp)
              Z_j = grand product of num_j/den_j (calculateZ, polinomial.hpp:586-607);
-             it closes because den is num shifted by one row (cm3, 3m cols)
+             it closes because den is num shifted by one row (cm3, 3m cols);
+             plookup Z: num = (1+beta)(gamma+f)(gamma(1+beta) + t + beta t'),
+             den = (gamma(1+beta) + h1 + beta h2)(gamma(1+beta) + h2 + beta h1')
   stage 4    alpha = ch[4]; C = Horner_alpha of all constraints; q = C / Z_H
              (step42ns semantics, op 69), split into qDeg = 2 pieces (cm4, 6 cols)
   stage 5    xi = ch[7]; evals (evmap); v1 = ch[5], v2 = ch[6];
@@ -93,18 +101,36 @@ class Program:
 
 class SyntheticStark:
     def __init__(self, n_bits=10, blowup_bits=1, t=4, m=2, n_k=3, n_queries=16, fri_steps=None, n_publics=8,
-                 seed=0x5EED, n_free=0):
+                 seed=0x5EED, n_free=0, n_lookups=2):
         self.n_bits = n_bits
         self.n_bits_ext = n_bits + blowup_bits
         self.blowup_bits = blowup_bits
         self.t, self.m, self.n_k = t, m, n_k
         self.n_free = n_free  # extra free (unconstrained, random) committed columns
-        self.n_cm1 = 3 * t + n_free
-        self.n_cm2 = 3 * m
-        self.n_cm3 = 3 * m
-        self.n_tmp = 6 * m
-        self.n_const = n_k + 1
+        assert 0 <= n_lookups <= 2
+        self.n_lookups = n_lookups
+        # constants: K_0..K_{nK-1}, L_first, then the lookup tables
         self.l_first = n_k  # const column index of L_first
+        self.c_t = [n_k + 1, n_k + 2, n_k + 3][:(2 if n_lookups >= 1 else 0) + (1 if n_lookups >= 2 else 0)]
+        self.n_const = n_k + 1 + len(self.c_t)
+        # cm1: 3t triples, n_free free columns, then lookup columns A, B, C
+        base = 3 * t + n_free
+        self.cm1_lk = list(range(base, base + len(self.c_t)))
+        self.n_cm1 = base + len(self.c_t)
+        # plookup contexts: dim, f/t tmp cols, h1/h2 cm2 cols, num/den tmp cols, Z cm3 col
+        self.lookups = []
+        cm2, tmp, cm3 = 3 * m, 6 * m, 3 * m
+        for k in range(n_lookups):
+            d = 3 if k == 0 else 1
+            lk = {"dim": d, "f": tmp, "t": tmp + d, "h1": cm2, "h2": cm2 + d, "num": tmp + 2 * d,
+                  "den": tmp + 2 * d + 3, "z": cm3}
+            self.lookups.append(lk)
+            cm2 += 2 * d
+            tmp += 2 * d + 6
+            cm3 += 3
+        self.n_cm2 = cm2
+        self.n_cm3 = cm3
+        self.n_tmp = tmp
         self.q_deg, self.q_dim = 2, 3
         self.n_cm4 = self.q_deg * self.q_dim
         self.n_queries = n_queries
@@ -121,8 +147,11 @@ class SyntheticStark:
         self.groups = [cols[j * size:(j + 1) * size] for j in range(m)]
         assert all(self.groups), "too many stage-2 groups for the cm1 width"
         self.z_ctx = [(6 * j, 6 * j + 3, 3 * j) for j in range(m)]  # (num tmp col, den tmp col, z cm3 col)
+        self.z_ctx += [(lk["num"], lk["den"], lk["z"]) for lk in self.lookups]
+        self.pu = [(lk["f"], lk["t"], lk["h1"], lk["h2"], lk["dim"]) for lk in self.lookups]
         self._build_evmap()
         self.programs = {
+            "step0": self._prog_step0(),
             "step1": self._prog_step1(),
             "step2": self._prog_step2(),
             "step3prev": self._prog_step3prev(),
@@ -139,20 +168,46 @@ class SyntheticStark:
             ev.append((SEC_CM1_2NS, c, 1, 0))
         for k in range(self.n_const):
             ev.append((SEC_CONST_2NS, k, 1, 0))
+        for c in self.c_t:
+            ev.append((SEC_CONST_2NS, c, 1, 1))  # t' in the plookup Z
         for j in range(self.m):
             ev.append((SEC_CM2_2NS, 3 * j, 3, 0))
             ev.append((SEC_CM2_2NS, 3 * j, 3, 1))
+        for lk in self.lookups:
+            ev.append((SEC_CM2_2NS, lk["h1"], lk["dim"], 0))
+            ev.append((SEC_CM2_2NS, lk["h1"], lk["dim"], 1))
+            ev.append((SEC_CM2_2NS, lk["h2"], lk["dim"], 0))
         for j in range(self.m):
             ev.append((SEC_CM3_2NS, 3 * j, 3, 0))
             ev.append((SEC_CM3_2NS, 3 * j, 3, 1))
+        for lk in self.lookups:
+            ev.append((SEC_CM3_2NS, lk["z"], 3, 0))
+            ev.append((SEC_CM3_2NS, lk["z"], 3, 1))
         for p in range(self.q_deg):
             ev.append((SEC_CM4_2NS, 3 * p, 3, 0))
         self.evmap = ev
         self.ev_index = {(s, c, pr): i for i, (s, c, d, pr) in enumerate(ev)}
 
     # ------------------------------------------------------------ programs
+    def _prog_step0(self):
+        """Constant derivation (setup): T2 = T0 with row 0 := T0[N/2]."""
+        p = Program(0)
+        if len(self.c_t) < 3:
+            return p
+        t = p.tmp1()
+        t0, lf = p.col(SEC_CONST_N, self.c_t[0]), p.col(SEC_CONST_N, self.l_first)
+        p.op(SUB, t, p.col(SEC_CONST_N, self.c_t[0], 1 << (self.n_bits - 1)), t0)
+        p.op(MUL, t, t, lf)
+        p.op(ADD, t, t, t0)
+        p.op(COPY, p.col(SEC_CONST_N, self.c_t[2]), t)
+        return p
+
+    # rows of the tables the lookup columns read: A, B at T[i+5] (row 0: T[11]), C at T2[i+7]
+    LK_SHIFT, LK_SHIFT0, LK_SHIFT_C = 5, 11, 7
+
     def _prog_step1(self):
-        """Trace derivation (executor stand-in): a[3j+2] = a[3j] a[3j+1] K_j + a[3j]."""
+        """Trace derivation (executor stand-in): a[3j+2] = a[3j] a[3j+1] K_j + a[3j];
+        lookup columns copied from table rows."""
         p = Program(0)
         t = p.tmp1()
         for j in range(self.t):
@@ -162,7 +217,57 @@ class SyntheticStark:
             p.op(MUL, t, t, kk)
             p.op(ADD, t, t, a0)
             p.op(COPY, a2, t)
+        lf = p.col(SEC_CONST_N, self.l_first)
+        for k, c in enumerate(self.cm1_lk[:2]):
+            tc = self.c_t[k]
+            p.op(SUB, t, p.col(SEC_CONST_N, tc, self.LK_SHIFT0), p.col(SEC_CONST_N, tc, self.LK_SHIFT))
+            p.op(MUL, t, t, lf)
+            p.op(ADD, t, t, p.col(SEC_CONST_N, tc, self.LK_SHIFT))
+            p.op(COPY, p.col(SEC_CM1_N, c), t)
+        if len(self.cm1_lk) > 2:
+            p.op(COPY, p.col(SEC_CM1_N, self.cm1_lk[2]), p.col(SEC_CONST_N, self.c_t[2], self.LK_SHIFT_C))
         return p
+
+    def _lk_ft(self, p, k, cm1_sec, const_sec, shift_t):
+        """(f, t') operands/temps of plookup k: f = A + u B | C, t = T0 + u T1 | T2 (row shift shift_t)."""
+        if self.lookups[k]["dim"] == 3:
+            u = p.chal(0)
+            f = p.tmp3()
+            p.op(MUL, f, u, p.col(cm1_sec, self.cm1_lk[1]))
+            p.op(ADD, f, f, p.col(cm1_sec, self.cm1_lk[0]))
+            t = p.tmp3()
+            p.op(MUL, t, u, p.col(const_sec, self.c_t[1], shift_t))
+            p.op(ADD, t, t, p.col(const_sec, self.c_t[0], shift_t))
+            return f, t
+        return p.col(cm1_sec, self.cm1_lk[2]), p.col(const_sec, self.c_t[2], shift_t)
+
+    def _lk_col(self, p, sec, c, dim, shift=0):
+        return p.col3(sec, c, shift) if dim == 3 else p.col(sec, c, shift)
+
+    def _emit_lk_num_den(self, p, lk, f, t, t_next, h1, h2, h1_next, num, den):
+        """num = (1+beta)(gamma+f)(gamma(1+beta) + t + beta t'),
+        den = (gamma(1+beta) + h1 + beta h2)(gamma(1+beta) + h2 + beta h1')."""
+        gamma, beta = p.chal(2), p.chal(3)
+        ob = p.tmp3()
+        p.op(ADD, ob, beta, p.lit(1))
+        gb = p.tmp3()
+        p.op(MUL, gb, ob, gamma)
+        x = p.tmp3()
+        y = p.tmp3()
+        p.op(ADD, x, f, gamma)
+        p.op(MUL, x, x, ob)
+        p.op(MUL, y, beta, t_next)
+        p.op(ADD, y, y, t)
+        p.op(ADD, y, y, gb)
+        p.op(MUL, num, x, y)
+        p.op(MUL, x, beta, h2)
+        p.op(ADD, x, x, h1)
+        p.op(ADD, x, x, gb)
+        p.op(MUL, y, beta, h1_next)
+        p.op(ADD, y, y, h2)
+        p.op(ADD, y, y, gb)
+        p.op(MUL, den, x, y)
+        return num, den
 
     def _emit_h(self, p, grp, sec, shift, dst3):
         """dst3 = sum_k a[s+k] u^(k+1) + defVal over the group's columns."""
@@ -182,6 +287,11 @@ class SyntheticStark:
         for j, grp in enumerate(self.groups):
             self._emit_h(p, grp, SEC_CM1_N, 0, h)
             p.op(COPY, p.col3(SEC_CM2_N, 3 * j), h)
+        # plookup f / t into tmpExp (transposeH1H2Columns reads them, starks.cpp:406-438)
+        for k, lk in enumerate(self.lookups):
+            f, t = self._lk_ft(p, k, SEC_CM1_N, SEC_CONST_N, 0)
+            p.op(COPY, self._lk_col(p, SEC_TMP_N, lk["f"], lk["dim"]), f)
+            p.op(COPY, self._lk_col(p, SEC_TMP_N, lk["t"], lk["dim"]), t)
         return p
 
     def _prog_step3prev(self):
@@ -194,6 +304,16 @@ class SyntheticStark:
             p.op(MUL, p.col3(SEC_TMP_N, num_c), t, beta)
             p.op(ADD, t, p.col3(SEC_CM2_N, 3 * j, 1), gamma)
             p.op(MUL, p.col3(SEC_TMP_N, den_c), t, beta)
+        for lk in self.lookups:
+            d = lk["dim"]
+            f = self._lk_col(p, SEC_TMP_N, lk["f"], d)
+            tt = self._lk_col(p, SEC_TMP_N, lk["t"], d)
+            tn = self._lk_col(p, SEC_TMP_N, lk["t"], d, 1)
+            h1 = self._lk_col(p, SEC_CM2_N, lk["h1"], d)
+            h2 = self._lk_col(p, SEC_CM2_N, lk["h2"], d)
+            h1n = self._lk_col(p, SEC_CM2_N, lk["h1"], d, 1)
+            self._emit_lk_num_den(p, lk, f, tt, tn, h1, h2, h1n, p.col3(SEC_TMP_N, lk["num"]),
+                                  p.col3(SEC_TMP_N, lk["den"]))
         return p
 
     def constraints(self, p, nxt):
@@ -238,6 +358,28 @@ class SyntheticStark:
                 p.op(SUB, r, r, s)
                 return r
             out.append(c_z)
+        for k, lk in enumerate(self.lookups):
+            def c_lk_first(lk=lk):
+                r = p.tmp3()
+                p.op(SUB, r, p.col3(SEC_CM3_2NS, lk["z"]), p.lit(1))
+                p.op(MUL, r, r, p.col(SEC_CONST_2NS, self.l_first))
+                return r
+
+            def c_lk_z(k=k, lk=lk):
+                d = lk["dim"]
+                f, t = self._lk_ft(p, k, SEC_CM1_2NS, SEC_CONST_2NS, 0)
+                _, tn = self._lk_ft(p, k, SEC_CM1_2NS, SEC_CONST_2NS, nxt)
+                h1 = self._lk_col(p, SEC_CM2_2NS, lk["h1"], d)
+                h2 = self._lk_col(p, SEC_CM2_2NS, lk["h2"], d)
+                h1n = self._lk_col(p, SEC_CM2_2NS, lk["h1"], d, nxt)
+                num, den = self._emit_lk_num_den(p, lk, f, t, tn, h1, h2, h1n, p.tmp3(), p.tmp3())
+                r = p.tmp3()
+                p.op(MUL, r, den, p.col3(SEC_CM3_2NS, lk["z"], nxt))
+                p.op(MUL, num, num, p.col3(SEC_CM3_2NS, lk["z"]))
+                p.op(SUB, r, r, num)
+                return r
+            out.append(c_lk_first)
+            out.append(c_lk_z)
         return out
 
     def _prog_step42ns(self):
@@ -261,7 +403,10 @@ class SyntheticStark:
         """(section, col, dim) of every committed polynomial, Horner order of f."""
         cols = [(SEC_CM1_2NS, c, 1) for c in range(self.n_cm1)]
         cols += [(SEC_CM2_2NS, 3 * j, 3) for j in range(self.m)]
+        for lk in self.lookups:
+            cols += [(SEC_CM2_2NS, lk["h1"], lk["dim"]), (SEC_CM2_2NS, lk["h2"], lk["dim"])]
         cols += [(SEC_CM3_2NS, 3 * j, 3) for j in range(self.m)]
+        cols += [(SEC_CM3_2NS, lk["z"], 3) for lk in self.lookups]
         cols += [(SEC_CM4_2NS, 3 * q, 3) for q in range(self.q_deg)]
         return cols
 
@@ -305,12 +450,16 @@ class SyntheticStark:
             "friSteps": self.fri_steps, "nCm1": self.n_cm1, "nCm2": self.n_cm2, "nCm3": self.n_cm3,
             "nCm4": self.n_cm4, "nTmp": self.n_tmp, "nConst": self.n_const, "nPublics": self.n_publics,
             "qDeg": self.q_deg, "qDim": self.q_dim, "lFirst": self.l_first, "seed": self.seed,
-            "randomCm1Cols": self.random_cm1_cols(),
-            "zCtx": self.z_ctx, "evMap": self.evmap,
+            "randomCm1Cols": self.random_cm1_cols(), "randomConst": self.random_const_cols(),
+            "zCtx": self.z_ctx, "puCtx": self.pu, "evMap": self.evmap,
         }
 
     def random_cm1_cols(self):
-        return [c for c in range(self.n_cm1) if c >= 3 * self.t or c % 3 != 2]
+        return [c for c in range(3 * self.t + self.n_free) if c >= 3 * self.t or c % 3 != 2]
+
+    def random_const_cols(self):
+        """K_k and the random tables T0, T1 (T2 is derived by step0)."""
+        return list(range(self.n_k)) + self.c_t[:2]
 
 
 # ---------------------------------------------------------------- PRNG
