@@ -1,0 +1,190 @@
+"""Translate the reference's generated per-row step code (the
+`<circuit>.chelpers.stepXX.cpp` files, e.g.
+src/starkpil/starkRecursive1/chelpers/recursive1.chelpers.step52ns.cpp) into a
+ZXP program (include/zkgpu_zxp.h).
+
+TEST INFRASTRUCTURE.  The reference's generated code is read as text at test
+time from /root/reference and turned into an in-memory program; nothing
+derived from it is stored in the repository.  The tests use it to pin the ZXP
+operation semantics (base/extension promotion, row shifts, challenges, evals,
+publics, x, zhInv, xDivXSub) against the reference's own code and golden
+proofs.
+
+Each statement of the `stepXX_first` body is one of
+    Goldilocks[3]::Element tmp_K;
+    Goldilocks[3]::{add,sub,mul}(dst, a, b);   Goldilocks[3]::copy(dst, a);
+with operands
+    tmp_K
+    params.pols[OFF + i*STRIDE]            params.pols[OFF + ((i + S)%M)*STRIDE]
+    params.pConstPols[2ns]->getElement(C,i)
+    params.challenges[K]  params.evals[K]  params.publicInputs[K]
+    Goldilocks::fromU64(V)   params.x_n[i] / x_2ns[i]   params.zi.zhInv(i)
+    params.xDivXSubXi[i] / xDivXSubWXi[i]  params.q_2ns[i * 3] / f_2ns[i * 3]
+A `(Goldilocks3::Element &)` cast on a pols operand marks a 3-wide column.
+`sections` maps a pols row STRIDE to (ZXP section, base offset).
+"""
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "zkevm-prover_amd")]
+
+from zkgpu.synthetic import (  # noqa: E402
+    ADD, SUB, MUL, COPY, TMP1, TMP3, COL, COL3, LIT, CHAL, PUB, X, EVAL, XDIV, XDIVW, ZI, Program,
+    SEC_CONST_N, SEC_CONST_2NS, SEC_Q_2NS, SEC_F_2NS)
+
+P = 0xFFFFFFFF00000001
+OPS = {"add": ADD, "sub": SUB, "mul": MUL, "copy": COPY}
+
+
+def function_body(text, name):
+    """Statements of `void <Class>::<name>(StepsParams &params, uint64_t i) { ... }`."""
+    m = re.search(r"void \w+::%s\(StepsParams &params, uint64_t i\)\s*\{" % re.escape(name), text)
+    if not m:
+        raise KeyError(name)
+    depth, j = 1, m.end()
+    while depth:
+        c = text[j]
+        depth += (c == "{") - (c == "}")
+        j += 1
+    return text[m.end():j - 1]
+
+
+def split_args(s):
+    out, depth, cur = [], 0, ""
+    for c in s:
+        if c in "([":
+            depth += 1
+        elif c in ")]":
+            depth -= 1
+        if c == "," and depth == 0:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += c
+    out.append(cur.strip())
+    return out
+
+
+class Translator:
+    def __init__(self, sections, domain_ext, nrows_ext=None):
+        self.p = Program(domain_ext)
+        self.sections = sections  # stride -> (section, base offset)
+        self.dim = {}
+        self.slot = {}
+        self.evals_used = set()
+
+    def tmp(self, name):
+        if name not in self.slot:
+            d = self.dim[name]
+            if d == 3:
+                self.slot[name] = self.p.tmp3()
+            else:
+                self.slot[name] = self.p.tmp1()
+        return self.slot[name]
+
+    def operand(self, s):
+        s = s.strip()
+        ext = False
+        cast = re.match(r"^\((Goldilocks3?)::Element\s*&\)\s*\*?\s*(.*)$", s)
+        if cast:
+            ext = cast.group(1) == "Goldilocks3"
+            s = cast.group(2).strip()
+        while s.startswith("(") and s.endswith(")"):
+            s = s[1:-1].strip()
+        if re.fullmatch(r"tmp_\d+", s):
+            return self.tmp(s)
+        m = re.fullmatch(r"params\.pols\[(\d+) \+ (?:i|\(\(i \+ (\d+)\)%(\d+)\))\*(\d+)\]", s)
+        if m:
+            off, shift, stride = int(m.group(1)), int(m.group(2) or 0), int(m.group(4))
+            sec, base = self.sections[stride]
+            return self.p.o(COL3 if ext else COL, sec, off - base, shift)
+        m = re.fullmatch(r"params\.pConstPols(2ns)?->getElement\((\d+),\s*i\)", s)
+        if m:
+            return self.p.o(COL, SEC_CONST_2NS if m.group(1) else SEC_CONST_N, int(m.group(2)), 0)
+        m = re.fullmatch(r"params\.challenges\[(\d+)\]", s)
+        if m:
+            return self.p.chal(int(m.group(1)))
+        m = re.fullmatch(r"params\.evals\[(\d+)\]", s)
+        if m:
+            self.evals_used.add(int(m.group(1)))
+            return self.p.ev(int(m.group(1)))
+        m = re.fullmatch(r"params\.publicInputs\[(\d+)\]", s)
+        if m:
+            return self.p.o(PUB, int(m.group(1)))
+        m = re.fullmatch(r"Goldilocks::fromU64\((\d+)ULL\)", s)
+        if m:
+            return self.p.lit(int(m.group(1)))
+        if re.fullmatch(r"params\.x_(n|2ns)\[i\]", s):
+            return self.p.o(X)
+        if s == "params.zi.zhInv(i)":
+            return self.p.o(ZI)
+        if s == "params.xDivXSubXi[i]":
+            return self.p.o(XDIV)
+        if s == "params.xDivXSubWXi[i]":
+            return self.p.o(XDIVW)
+        m = re.fullmatch(r"params\.(q|f)_2ns\[i \* 3\]", s)
+        if m:
+            return self.p.o(COL3, SEC_Q_2NS if m.group(1) == "q" else SEC_F_2NS, 0, 0)
+        raise ValueError("unsupported operand: %r" % s)
+
+    def translate(self, body):
+        for stmt in body.split(";"):
+            stmt = stmt.strip()
+            if not stmt:
+                continue
+            m = re.fullmatch(r"Goldilocks(3?)::Element (tmp_\d+)", stmt)
+            if m:
+                self.dim[m.group(2)] = 3 if m.group(1) else 1
+                continue
+            m = re.fullmatch(r"Goldilocks3?::(add|sub|mul|copy)\((.*)\)", stmt, re.S)
+            if not m:
+                raise ValueError("unsupported statement: %r" % stmt[:120])
+            args = [self.operand(a) for a in split_args(m.group(2))]
+            op = OPS[m.group(1)]
+            if op == COPY:
+                self.p.op(COPY, args[0], args[1])
+            else:
+                self.p.op(op, args[0], args[1], args[2])
+        return self.p
+
+
+def translate_file(path, func, sections, domain_ext):
+    with open(path) as f:
+        text = f.read()
+    tr = Translator(sections, domain_ext)
+    prog = tr.translate(function_body(text, func))
+    return prog, tr
+
+
+def evmap_from_step52ns(prog):
+    """Recover starkInfo.evMap from a translated step52ns: every
+    `pol - evals[k]` difference flows into either the xDivXSubXi product
+    (prime 0) or the xDivXSubWXi product (prime 1) (starks.cpp:336-366).
+    Returns {k: (section, col, dim, prime)}."""
+    ins = prog.instr
+    opn = prog.opnd
+    deps = {}  # operand index of a temp -> set of eval indices it carries
+    direct = {}  # eval k -> (section, col, dim)
+    res = {}
+    for op, dst, a, b in ins:
+        srcs = [a] if op == COPY else [a, b]
+        carried = set()
+        for s in srcs:
+            carried |= deps.get(s, set())
+        kinds = [opn[s][0] for s in srcs]
+        if op == SUB and EVAL in kinds:
+            col = srcs[kinds.index(EVAL) ^ 1]
+            k = opn[srcs[kinds.index(EVAL)]][1]
+            kind, sec, c, _ = opn[col]
+            direct[k] = (sec, c, 3 if kind == COL3 else 1)
+            carried.add(k)
+        if op == MUL and (XDIV in kinds or XDIVW in kinds):
+            prime = 0 if XDIV in kinds else 1
+            for k in carried:
+                res[k] = direct[k] + (prime,)
+            carried = set()
+        if opn[dst][0] in (TMP1, TMP3):
+            deps[dst] = carried if op != COPY else deps.get(a, set()) | carried
+    return res
