@@ -43,9 +43,11 @@ def parse():
     ap.add_argument("--blowup-bits", type=int, default=1)
     ap.add_argument("--cpu-sample-cols", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_COLS", "4")))
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--workload", choices=["lde", "merkle", "stark"], default="lde",
+    ap.add_argument("--workload", choices=["lde", "merkle", "stark", "commit"], default="lde",
                     help="lde = configs[1] (headline); merkle = configs[2] (2^23 x 100 Poseidon tree); "
-                         "stark = configs[3] (full synthetic STARK proof, 2^23 trace)")
+                         "stark = configs[3] (full synthetic STARK proof, 2^23 trace); "
+                         "commit = configs[4] (one trace column-sharded over the ranks: LDE + all-to-all + "
+                         "subtree Merkle + root, strong scaling)")
     ap.add_argument("--queries", type=int, default=128)
     ap.add_argument("--cpu-sample-bits", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_BITS", "16")))
     return ap.parse_args()
@@ -85,6 +87,24 @@ def cpu_baseline_merkle(log_n, ncols):
     return {"value": rows * ncols / dt / 1e9, "unit": "Gelem/s", "cores": threads, "kind": "port",
             "sample": "oracle merkletree 2^%d rows x %d cols, %.1f s, %d threads (%s)"
                       % (min(log_n, 16), ncols, dt, threads, _cpu_model())}
+
+
+def cpu_baseline_commit(log_n, blow, ncols, sample_bits):
+    """Oracle LDE + merkletree (OpenMP) of the same column count at 2^sample_bits rows."""
+    import numpy as np
+    from oracle import oracle as oc
+    oc.lib()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    oc.lib().oc_set_num_threads(threads)
+    rows = 1 << min(log_n, sample_bits)
+    rng = np.random.default_rng(0x5EED)
+    x = rng.integers(0, 2**63, size=(rows, ncols), dtype=np.uint64)
+    t0 = time.perf_counter()
+    oc.merkletree(oc.extend_pol(x, rows << blow))
+    dt = time.perf_counter() - t0
+    return {"value": (rows << blow) * ncols / dt / 1e9, "unit": "Gelem/s", "cores": threads, "kind": "port",
+            "sample": "oracle extendPol + merkletree 2^%d rows x %d cols, %.1f s, %d threads (%s)"
+                      % (min(log_n, sample_bits), ncols, dt, threads, _cpu_model())}
 
 
 def stark_instance(log_n, blow, ncols, n_queries):
@@ -161,7 +181,15 @@ def main():
     g.manual_seed(0x5EED + rank)
     # canonical Goldilocks values: uniform in [0, 2^63) < p
     gs = None
-    if args.workload == "stark":
+    if args.workload == "commit":
+        from zkgpu.sharded import ShardedCommit, col_range
+        lo, hi = col_range(C, world, rank)
+        trace = torch.randint(0, 2**63 - 1, (max(hi - lo, 1), n), dtype=torch.int64, device=dev, generator=g)
+        sc = ShardedCommit(args.log_n, args.blowup_bits, C, device=dev)
+
+        def step():
+            sc.commit(trace)
+    elif args.workload == "stark":
         from zkgpu.stark import GpuStark
         inst = stark_instance(args.log_n, args.blowup_bits, C, args.queries)
         gs = GpuStark(inst)  # setup: constants, constant LDE + tree (untimed, loaded from files in the reference)
@@ -217,7 +245,11 @@ def main():
     elapsed = float(t.item())
 
     if rank == 0:
-        if args.workload == "stark":
+        if args.workload == "commit":
+            total_elems = ne * C * args.steps  # one trace for the whole job
+            unit, metric_unit = "Gelem/s", "LDE elements committed (LDE + Merkle)"
+            alg_step = (8 * (n + ne) * C + 8 * ne * C + 32 * ne + 96 * ne) // world
+        elif args.workload == "stark":
             total_elems = world * args.steps
             unit, metric_unit = "s/proof", "proofs"
             alg_step = 8 * (n + ne) * (C + 48 + 6)
@@ -233,6 +265,8 @@ def main():
         if args.workload == "stark":
             value = elapsed / total_elems  # seconds per proof, whole job
         cpu = None
+        if world == 1 and not args.no_cpu and args.workload == "commit":
+            cpu = cpu_baseline_commit(args.log_n, args.blowup_bits, C, args.cpu_sample_bits)
         if world == 1 and not args.no_cpu and args.workload == "stark":
             cpu = cpu_baseline_stark(args.cpu_sample_bits, args.log_n, args.blowup_bits, C, args.queries)
         if world == 1 and not args.no_cpu and args.workload == "lde":
@@ -242,6 +276,10 @@ def main():
         if args.workload == "lde":
             workload = ("LDE 2^%d -> 2^%d rows x %d cols per GPU (extendPol, starks.cpp:53), column-major in HBM"
                         % (args.log_n, args.log_n + args.blowup_bits, C))
+        elif args.workload == "commit":
+            workload = ("column-sharded commit of one 2^%d-row x %d-col trace over %d rank(s): LDE 2^%d -> 2^%d, "
+                        "all-to-all column->row blocks, per-rank Merkle subtree, sub-root gather + top levels "
+                        "(starks.cpp:53-57)" % (args.log_n, C, world, args.log_n, args.log_n + args.blowup_bits))
         elif args.workload == "merkle":
             workload = ("Poseidon-GL Merkle tree over 2^%d rows x %d cols per GPU (merkelize, merkleTreeGL.cpp:37-44)"
                         % (args.log_n, C))
@@ -261,15 +299,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": args.workload != "stark",
-            "scaling": "weak",
+            "scaling": "strong" if args.workload == "commit" else "weak",
             "vs_baseline": None,
             "dtype": "u64 (Goldilocks)" if args.workload != "stark" else "u64 (Goldilocks) + F_p^3",
             "data": "synthetic (uniform canonical Goldilocks, torch generator seed 0x5EED+rank)",
             "config": {
                 "workload": workload,
                 "log_n": args.log_n, "blowup_bits": args.blowup_bits, "ncols_per_gpu": C,
-                "parallelism": ("column-sharded x%d (no data-path collective)" % world) if args.workload != "stark"
-                else "replicas x%d (one independent proof per GPU)" % world,
+                "parallelism": {"stark": "replicas x%d (one independent proof per GPU)" % world,
+                                "commit": "column-sharded x%d, RCCL all-to-all column->row blocks" % world}.get(
+                    args.workload, "column-sharded x%d (no data-path collective)" % world),
             },
             "roofline": {
                 "kernel": dom,

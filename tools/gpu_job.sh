@@ -61,6 +61,12 @@ for step in "$@"; do
         ok_or_stop $? "bench stark"
         cat gpurun_out/bench_stark.json
         ;;
+    commit)
+        timeout -k 10 600 python bench.py --workload commit --steps 3 --warmup 1 \
+            > gpurun_out/bench_commit.json 2> gpurun_out/bench_commit.err
+        ok_or_stop $? "bench commit"
+        cat gpurun_out/bench_commit.json
+        ;;
     starkprof)
         cd /tmp
         timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_stark" -o run \
