@@ -5,85 +5,18 @@
 // transcript.cpp:23,46, build_const_tree.cpp:582) and MerkleTreeGL's
 // getGroupProof (merkleTreeGL.cpp:12-35).
 //
-// Permutation: t = 12, 4 + 22 + 4 rounds, S-box x^7, MDS = circ(17,15,41,16,
-// 2,28,13,13,39,18,34,20) + diag(8,0,...) -- the reference's own form at
-// poseidon_g_executor.cpp:201-231 / .hpp:29-51.  Integer VALU-bound: one
-// thread per permutation, the 12-lane state in VGPRs, round constants in
-// constant memory (wave-uniform -> scalar loads), the MDS as 32x32->64
-// multiply-adds on the 32-bit halves of each lane (the MDS entries are < 64).
+// Permutation: poseidon_perm.hpp (perm_fast) -- bit-identical to the
+// reference's form at poseidon_g_executor.cpp:201-231 / .hpp:29-51, evaluated
+// with folded round constants and the partial rounds as block dot products.
+// Integer VALU-bound: one thread per permutation, the 12-lane state in VGPRs,
+// table coefficients as wave-uniform scalar loads.
 //
 // Leaves: one thread per row; a column-major (SoA) source makes each of the
 // ceil(ncols/8) absorption steps a fully coalesced 8-column read.
-#include "gl_device.hpp"
-#include "poseidon_gl_constants.h"
+#include "poseidon_perm.hpp"
 #include "zkgpu_internal.hpp"
 
 namespace zk {
-
-__constant__ uint64_t c_rc[360];
-
-__device__ __forceinline__ uint64_t pow7(uint64_t x)
-{
-    uint64_t x2 = gl_mul(x, x);
-    uint64_t x3 = gl_mul(x2, x);
-    uint64_t x4 = gl_mul(x2, x2);
-    return gl_mul(x3, x4);
-}
-
-// state' = M * state ; M[x][y] = MCIRC[(y - x) mod 12] + (x == y) * MDIAG[x]
-__device__ __forceinline__ void mds(uint64_t st[12])
-{
-    constexpr uint32_t MC[12] = {17, 15, 41, 16, 2, 28, 13, 13, 39, 18, 34, 20};
-    uint32_t lo[12], hi[12];
-#pragma unroll
-    for (int y = 0; y < 12; y++) {
-        lo[y] = (uint32_t)st[y];
-        hi[y] = (uint32_t)(st[y] >> 32);
-    }
-    uint64_t out[12];
-#pragma unroll
-    for (int x = 0; x < 12; x++) {
-        uint64_t sl = 0, sh = 0;
-#pragma unroll
-        for (int y = 0; y < 12; y++) {
-            uint32_t m = MC[(y - x + 12) % 12] + (x == y && x == 0 ? 8u : 0u);
-            sl += (uint64_t)lo[y] * m;
-            sh += (uint64_t)hi[y] * m;
-        }
-        // value = sl + sh * 2^32  (< 2^75)
-        uint64_t l = sl + (sh << 32);
-        uint64_t c = (l < sl) ? 1ULL : 0ULL;
-        uint64_t h = (sh >> 32) + c;
-        out[x] = gl_reduce128(l, h);
-    }
-#pragma unroll
-    for (int x = 0; x < 12; x++) st[x] = out[x];
-}
-
-__device__ __forceinline__ void full_round(uint64_t st[12], int r)
-{
-#pragma unroll
-    for (int s = 0; s < 12; s++) st[s] = pow7(gl_add(st[s], c_rc[r * 12 + s]));
-    mds(st);
-}
-
-__device__ __forceinline__ void partial_round(uint64_t st[12], int r)
-{
-#pragma unroll
-    for (int s = 0; s < 12; s++) st[s] = gl_add(st[s], c_rc[r * 12 + s]);
-    st[0] = pow7(st[0]);
-    mds(st);
-}
-
-__device__ void poseidon_perm(uint64_t st[12])
-{
-#pragma unroll 1
-    for (int r = 0; r < 4; r++) full_round(st, r);
-#pragma unroll 1
-    for (int r = 4; r < 26; r++) partial_round(st, r);
-#pragma unroll 1
-    for (int r = 26; r < 30; r++) full_round(st, r);
-}
 
 // ---------------------------------------------------------------- kernels
 __global__ void k_poseidon_batch(uint64_t *out, const uint64_t *in, uint64_t n, int full)
@@ -196,10 +129,11 @@ __global__ void k_merkle_open(uint64_t *vals, uint64_t *sibs, const uint64_t *no
 // ---------------------------------------------------------------- host side
 static inline uint32_t blocks_for(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
 
+// The permutation's tables are compile-time constants (poseidon_perm.hpp); nothing to upload.
 int upload_poseidon_constants(Ctx &c)
 {
     (void)c;
-    return check_hip(hipMemcpyToSymbol(HIP_SYMBOL(c_rc), ZKGPU_POSEIDON_RC, sizeof(uint64_t) * 360), "poseidon rc");
+    return 0;
 }
 
 int poseidon_batch(uint64_t *out, const uint64_t *in, uint64_t n, int full, hipStream_t s)
