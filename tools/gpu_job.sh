@@ -102,6 +102,25 @@ for step in "$@"; do
         cd "$GRAFT_REPO_ROOT"
         ok_or_stop $rc "rocprofv3 pmc WRITE_SIZE"
         ;;
+    zxpsweep)
+        for r in 1 2 4; do
+            ZKGPU_ZXP_ROWS=$r timeout -k 10 300 python bench.py --workload stark --steps 2 --warmup 1 --no-cpu \
+                > gpurun_out/zxp_r$r.json 2>> gpurun_out/zxp_sweep.err
+            ok_or_stop $? "stark zxp rows=$r"
+            echo "rows=$r $(python -c "import json;d=json.load(open('gpurun_out/zxp_r$r.json'));print(d['ms_per_step'],'ms', d['kernels']['k_zxp_eval'])")"
+        done
+        ;;
+    sqpmc)
+        # VALU/SALU/SMEM issue and wave-state counters for every kernel of a 2^20 STARK proof
+        cd /tmp
+        timeout -s KILL 120 rocprofv3 -L > "$GRAFT_REPO_ROOT/gpurun_out/rocprof_counters.txt" 2>&1
+        timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
+            -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_sq" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" \
+            --workload stark --log-n 20 --no-cpu --steps 1 --warmup 0 > /dev/null 2> "$GRAFT_REPO_ROOT/gpurun_out/pmc_sq.err"
+        rc=$?
+        cd "$GRAFT_REPO_ROOT"
+        ok_or_stop $rc "rocprofv3 pmc SQ"
+        ;;
     *)
         echo "unknown step $step"
         ;;

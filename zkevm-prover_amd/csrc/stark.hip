@@ -17,6 +17,8 @@
 //   k_qsplit        quotient split (starks.cpp:264-281)
 // F_p^3 arithmetic is associative/commutative and exact, so any reduction
 // order gives the reference's values bit for bit.
+#include <stdlib.h>
+
 #include "gl_device.hpp"
 #include "zkgpu_internal.hpp"
 #include "../../include/zkgpu_zxp.h"
@@ -122,17 +124,19 @@ struct Val {
     int dim;
 };
 
-__device__ __forceinline__ Val zxp_load(const ZxpEnv &e, const zxp_operand &o, const uint64_t *lds, int lane,
-                                        uint64_t i)
+// Temp slot s of virtual row vl lives at lds[s * VL + vl] (VL = 64 * R rows
+// per workgroup), so each LDS access of a wave is 64 consecutive u64.
+template <int VL>
+__device__ __forceinline__ Val zxp_load(const ZxpEnv &e, const zxp_operand &o, const uint64_t *lds, int vl, uint64_t i)
 {
     Val r;
     r.dim = 1;
     r.v.v[1] = r.v.v[2] = 0;
     switch (o.kind) {
-    case ZXP_TMP1: r.v.v[0] = lds[o.a * ZXP_THREADS + lane]; break;
+    case ZXP_TMP1: r.v.v[0] = lds[o.a * VL + vl]; break;
     case ZXP_TMP3: {
-        const uint64_t *p = lds + (e.tmp3_base + 3 * o.a) * ZXP_THREADS + lane;
-        r.v = gl3{{p[0], p[ZXP_THREADS], p[2 * ZXP_THREADS]}};
+        const uint64_t *p = lds + (e.tmp3_base + 3 * o.a) * VL + vl;
+        r.v = gl3{{p[0], p[VL], p[2 * VL]}};
         r.dim = 3;
         break;
     }
@@ -167,62 +171,84 @@ __device__ __forceinline__ Val zxp_load(const ZxpEnv &e, const zxp_operand &o, c
     return r;
 }
 
+// One wave per workgroup, R rows per thread (rows i0 + 64 r): an instruction
+// is decoded once (wave-uniform scalar loads) and applied to R rows whose
+// operand loads are all issued before any arithmetic.  R > 1 was meant to
+// hide decode/load latency (SQ_WAIT_ANY 0.57 at R = 1) but measured slower
+// (more VGPRs, fewer waves), so the default is R = 1.
+template <int R>
 __global__ void __launch_bounds__(ZXP_THREADS) k_zxp_eval(ZxpEnv e)
 {
+    constexpr int VL = ZXP_THREADS * R;
     extern __shared__ __attribute__((aligned(16))) uint64_t zlds[];
     const int lane = threadIdx.x;
-    const uint64_t i = (uint64_t)blockIdx.x * ZXP_THREADS + lane;  // dom is a multiple of 64 or padded
+    const uint64_t i0 = (uint64_t)blockIdx.x * VL + lane;
     const uint64_t dom = 1ULL << e.logdom;
-    const bool active = i < dom;
     for (uint32_t k = 0; k < e.n_instr; k++) {
         const zxp_instr in = e.instr[k];
         const zxp_operand oa = e.opnd[in.a];
-        Val a = zxp_load(e, oa, zlds, lane, active ? i : 0);
-        Val r;
-        if (in.op == ZXP_COPY) {
-            r = a;
-        } else {
-            const zxp_operand ob = e.opnd[in.b];
-            Val b = zxp_load(e, ob, zlds, lane, active ? i : 0);
-            r.dim = (a.dim == 3 || b.dim == 3) ? 3 : 1;
-            if (in.op == ZXP_MUL) {
-                if (a.dim == 3 && b.dim == 3)
-                    r.v = gl3_mul(a.v, b.v);
-                else if (a.dim == 3)
-                    r.v = gl3_mul1(a.v, b.v.v[0]);
-                else if (b.dim == 3)
-                    r.v = gl3_mul1(b.v, a.v.v[0]);
-                else
-                    r.v = gl3{{gl_mul(a.v.v[0], b.v.v[0]), 0, 0}};
-            } else if (in.op == ZXP_ADD) {
-                r.v = gl3_add(a.v, b.v);  // base operands carry zeros in components 1, 2
-            } else {
-                r.v = gl3_sub(a.v, b.v);
+        const zxp_operand ob = e.opnd[in.op == ZXP_COPY ? in.a : in.b];
+        const zxp_operand od = e.opnd[in.dst];
+        Val a[R], b[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const uint64_t i = i0 + (uint64_t)(ZXP_THREADS * r);
+            a[r] = zxp_load<VL>(e, oa, zlds, lane + ZXP_THREADS * r, i < dom ? i : 0);
+        }
+        if (in.op != ZXP_COPY) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const uint64_t i = i0 + (uint64_t)(ZXP_THREADS * r);
+                b[r] = zxp_load<VL>(e, ob, zlds, lane + ZXP_THREADS * r, i < dom ? i : 0);
             }
         }
-        const zxp_operand od = e.opnd[in.dst];
-        switch (od.kind) {
-        case ZXP_TMP1: zlds[od.a * ZXP_THREADS + lane] = r.v.v[0]; break;
-        case ZXP_TMP3: {
-            uint64_t *p = zlds + (e.tmp3_base + 3 * od.a) * ZXP_THREADS + lane;
-            p[0] = r.v.v[0];
-            p[ZXP_THREADS] = r.dim == 3 ? r.v.v[1] : 0;
-            p[2 * ZXP_THREADS] = r.dim == 3 ? r.v.v[2] : 0;
-            break;
-        }
-        case ZXP_COL:
-        case ZXP_COL3:
-            if (active) {
-                const uint64_t ld = e.ld[od.a];
-                uint64_t *p = e.sec[od.a] + (uint64_t)od.b * ld + i;
-                p[0] = gl_canon(r.v.v[0]);
-                if (od.kind == ZXP_COL3) {
-                    p[ld] = r.dim == 3 ? gl_canon(r.v.v[1]) : 0;
-                    p[2 * ld] = r.dim == 3 ? gl_canon(r.v.v[2]) : 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const uint64_t i = i0 + (uint64_t)(ZXP_THREADS * r);
+            const int vl = lane + ZXP_THREADS * r;
+            Val res;
+            if (in.op == ZXP_COPY) {
+                res = a[r];
+            } else {
+                res.dim = (a[r].dim == 3 || b[r].dim == 3) ? 3 : 1;
+                if (in.op == ZXP_MUL) {
+                    if (a[r].dim == 3 && b[r].dim == 3)
+                        res.v = gl3_mul(a[r].v, b[r].v);
+                    else if (a[r].dim == 3)
+                        res.v = gl3_mul1(a[r].v, b[r].v.v[0]);
+                    else if (b[r].dim == 3)
+                        res.v = gl3_mul1(b[r].v, a[r].v.v[0]);
+                    else
+                        res.v = gl3{{gl_mul(a[r].v.v[0], b[r].v.v[0]), 0, 0}};
+                } else if (in.op == ZXP_ADD) {
+                    res.v = gl3_add(a[r].v, b[r].v);  // base operands carry zeros in components 1, 2
+                } else {
+                    res.v = gl3_sub(a[r].v, b[r].v);
                 }
             }
-            break;
-        default: break;
+            switch (od.kind) {
+            case ZXP_TMP1: zlds[od.a * VL + vl] = res.v.v[0]; break;
+            case ZXP_TMP3: {
+                uint64_t *p = zlds + (e.tmp3_base + 3 * od.a) * VL + vl;
+                p[0] = res.v.v[0];
+                p[VL] = res.dim == 3 ? res.v.v[1] : 0;
+                p[2 * VL] = res.dim == 3 ? res.v.v[2] : 0;
+                break;
+            }
+            case ZXP_COL:
+            case ZXP_COL3:
+                if (i < dom) {
+                    const uint64_t ld = e.ld[od.a];
+                    uint64_t *p = e.sec[od.a] + (uint64_t)od.b * ld + i;
+                    p[0] = gl_canon(res.v.v[0]);
+                    if (od.kind == ZXP_COL3) {
+                        p[ld] = res.dim == 3 ? gl_canon(res.v.v[1]) : 0;
+                        p[2 * ld] = res.dim == 3 ? gl_canon(res.v.v[2]) : 0;
+                    }
+                }
+                break;
+            default: break;
+            }
         }
     }
 }
@@ -545,11 +571,29 @@ int zxp_eval(const ZxpLaunch &L, hipStream_t s)
     e.x_start = L.x_start;
     e.tw_lo = c.tw_lo[0];
     e.tw_hi = c.tw_hi[0];
-    size_t lds = (size_t)(e.n_slots ? e.n_slots : 1) * ZXP_THREADS * sizeof(uint64_t);
+    // rows per thread: the most that keeps >= 2 waves per SIMD (8 x 20 KB of LDS per CU)
+    const uint64_t slots = e.n_slots ? e.n_slots : 1;
+    static const int R_max = [] {
+        // tuning override (1, 2 or 4); measured on MI355X, config-4 STARK: the
+        // one-row form is fastest (28.3 ms vs 37.5 / 44.9 ms per launch)
+        const char *v = getenv("ZKGPU_ZXP_ROWS");
+        const int r = v ? atoi(v) : 1;
+        return r >= 4 ? 4 : (r >= 2 ? 2 : 1);
+    }();
+    int R = R_max;
+    while (R > 1 && slots * R * ZXP_THREADS * sizeof(uint64_t) > 20 * 1024) R >>= 1;
+    const uint64_t dom = 1ULL << L.logdom;
+    while (R > 1 && dom < (uint64_t)ZXP_THREADS * R) R >>= 1;
+    size_t lds = (size_t)slots * R * ZXP_THREADS * sizeof(uint64_t);
     if (lds > 160 * 1024) return set_error(ZKGPU_ERR_ARG, "zxp: %u temp slots exceed LDS", e.n_slots);
-    uint64_t dom = 1ULL << L.logdom;
     prof_begin(s);
-    hipLaunchKernelGGL(k_zxp_eval, dim3(nblk(dom, ZXP_THREADS)), dim3(ZXP_THREADS), lds, s, e);
+    const dim3 grid(nblk(dom, ZXP_THREADS * R));
+    if (R == 4)
+        hipLaunchKernelGGL(k_zxp_eval<4>, grid, dim3(ZXP_THREADS), lds, s, e);
+    else if (R == 2)
+        hipLaunchKernelGGL(k_zxp_eval<2>, grid, dim3(ZXP_THREADS), lds, s, e);
+    else
+        hipLaunchKernelGGL(k_zxp_eval<1>, grid, dim3(ZXP_THREADS), lds, s, e);
     prof_end("k_zxp_eval", L.bytes, s);
     return check_launch("k_zxp_eval");
 }
