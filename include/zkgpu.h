@@ -96,6 +96,28 @@ int zkgpu_gl_merkletree(uint64_t *nodes, const uint64_t *src, uint64_t ncols, ui
 int zkgpu_gl_merkletree_dev(uint64_t *nodes, const uint64_t *src, uint64_t ld, uint64_t ncols, uint64_t nrows);
 /* device-resident, row-major source (FRI trees: friProve.cpp:117-121) */
 int zkgpu_gl_merkletree_rows_dev(uint64_t *nodes, const uint64_t *src, uint64_t ncols, uint64_t nrows);
+/* ---- constant tree (tools/starkpil/bctree) -----------------------------
+ * Element count of a const-tree file: header 2 + nPols*nExt + tree
+ * (build_const_tree.cpp:566-569). */
+uint64_t zkgpu_const_tree_num_elements(uint64_t n_pols, uint32_t n_bits_ext);
+/* build_const_tree.cpp:553-603 (GL hash): interpolate (extendPol of the
+ * row-major N x nPols constant pols to nExt rows) + PoseidonGoldilocks::
+ * merkletree, written in the file layout [nPols, nExt, LDE row-major,
+ * tree nodes]; the verkey constRoot is the last 4 elements.  Host pointers. */
+int zkgpu_build_const_tree(uint64_t *tree_out, const uint64_t *const_pols, uint64_t n_pols, uint32_t n_bits,
+                           uint32_t n_bits_ext);
+
+/* ---- executor hand-off ------------------------------------------------
+ * Load a host row-major section (the committed-pols buffer the executor
+ * fills, CommitPols stride = width, commit_pols.hpp:18,1735-1737; read by
+ * prover.cpp:94-116) into device column-major storage (column c at
+ * cols + c*ld), streamed in row blocks: each block's H2D copy runs on a copy
+ * stream while the previous block is transposed, so a pinned (registered)
+ * source moves at link speed.  register_host = 1 page-locks `rows` for the
+ * duration of the call (hipHostRegister). */
+int zkgpu_load_rows_dev(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint64_t nrows, uint64_t ncols,
+                        uint64_t block_rows, int register_host);
+
 /* MerkleTreeGL::getGroupProof(Element *proof, uint64_t idx) for nq queries at
  * once -- merkleTreeGL.cpp:12-35, friProve.cpp:195-232.
  * vals_out: nq x ncols, sibs_out: nq x log2(nrows) x 4 (host pointers);

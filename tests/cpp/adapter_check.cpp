@@ -88,6 +88,27 @@ int main()
         expect(ok, "MerkleTreeGL::getGroupProof");
     }
 
+    // --- bctree: const tree image, loaded back through MerkleTreeGL(E *tree)
+    {
+        const uint32_t nb = 11, nbe = 12;
+        const uint64_t n = 1ULL << nb, nx = 1ULL << nbe, np = 6;
+        std::vector<Element> cp(n * np);
+        for (auto &e : cp) e.fe = rng() % P;
+        std::vector<Element> img = zkgpu::buildConstTree(cp.data(), np, nb, nbe);
+        std::vector<uint64_t> lde(nx * np), cn(oc_merkle_num_elements(nx));
+        oc_extend_pol(lde.data(), (uint64_t *)cp.data(), nx, n, np);
+        oc_merkletree(cn.data(), lde.data(), np, nx);
+        bool ok = img.size() == 2 + np * nx + cn.size() && img[0].fe == np && img[1].fe == nx &&
+                  memcmp(&img[2], lde.data(), lde.size() * 8) == 0 &&
+                  memcmp(&img[2 + np * nx], cn.data(), cn.size() * 8) == 0;
+        expect(ok, "bctree buildConstTree image");
+        zkgpu::MerkleTreeGLT<Element> ct(img.data());
+        Element r3[4];
+        ct.getRoot(r3);
+        expect(ct.width == np && ct.height == nx && memcmp(r3, &cn[cn.size() - 4], 32) == 0,
+               "MerkleTreeGL(constTree) root");
+    }
+
     printf("%s\n", failures ? "FAILED" : "ALL OK");
     return failures ? 1 : 0;
 }

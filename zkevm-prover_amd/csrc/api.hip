@@ -478,6 +478,105 @@ int zkgpu_gl_merkle_open_dev(uint64_t *vals_out, uint64_t *sibs_out, const uint6
     return check_hip(hipStreamSynchronize(c.stream), "merkle_open sync");
 }
 
+// ---------------------------------------------------------------- const tree
+uint64_t zkgpu_const_tree_num_elements(uint64_t n_pols, uint32_t n_bits_ext)
+{
+    const uint64_t n_ext = 1ULL << n_bits_ext;
+    return 2 + n_pols * n_ext + zkgpu_gl_merkle_num_elements(n_ext);
+}
+
+int zkgpu_build_const_tree(uint64_t *tree_out, const uint64_t *const_pols, uint64_t n_pols, uint32_t n_bits,
+                           uint32_t n_bits_ext)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (n_bits_ext < n_bits || n_bits_ext > TW_MAX_LOG)
+        return set_error(ZKGPU_ERR_ARG, "const_tree: bad nBits %u / nBitsExt %u", n_bits, n_bits_ext);
+    Ctx &c = g_ctx;
+    const uint64_t n = 1ULL << n_bits, n_ext = 1ULL << n_bits_ext;
+    const uint64_t n_nodes = zkgpu_gl_merkle_num_elements(n_ext);
+    tree_out[0] = n_pols;  // Goldilocks::fromU64(nPols), fromU64(nExt)
+    tree_out[1] = n_ext;
+    const size_t in_bytes = n * n_pols * sizeof(uint64_t), out_bytes = n_ext * n_pols * sizeof(uint64_t);
+    uint64_t *rows = workspace(2, out_bytes + 8);
+    uint64_t *cols = workspace(3, out_bytes + in_bytes + n_nodes * sizeof(uint64_t) + 8);
+    if (!rows || !cols) return ZKGPU_ERR_OOM;
+    uint64_t *cin = cols + n_ext * n_pols;
+    uint64_t *nodes = cin + n * n_pols;
+    if (n_pols) {
+        if ((rc = check_hip(hipMemcpyAsync(rows, const_pols, in_bytes, hipMemcpyHostToDevice, c.stream), "H2D")))
+            return rc;
+        rows_to_cols(rows, cin, n, n_pols, n, c.stream);
+        if ((rc = extend_pol_dev(cols, n_ext, cin, n, n_ext, n, n_pols))) return rc;  // interpolate()
+    }
+    if ((rc = merkle_leaves_cols(nodes, cols, n_pols, n_ext, n_ext, c.stream))) return rc;
+    if ((rc = merkle_levels(nodes, n_ext, c.stream))) return rc;
+    if (n_pols) {
+        cols_to_rows(cols, rows, n_ext, n_pols, n_ext, c.stream);
+        if ((rc = check_hip(hipMemcpyAsync(tree_out + 2, rows, out_bytes, hipMemcpyDeviceToHost, c.stream), "D2H")))
+            return rc;
+    }
+    if ((rc = check_hip(hipMemcpyAsync(tree_out + 2 + n_ext * n_pols, nodes, n_nodes * sizeof(uint64_t),
+                                       hipMemcpyDeviceToHost, c.stream),
+                        "D2H")))
+        return rc;
+    return check_hip(hipStreamSynchronize(c.stream), "const_tree sync");
+}
+
+// ---------------------------------------------------------------- executor hand-off
+int zkgpu_load_rows_dev(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint64_t nrows, uint64_t ncols,
+                        uint64_t block_rows, int register_host)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!nrows || !ncols) return 0;
+    if (ld < nrows) return set_error(ZKGPU_ERR_ARG, "load_rows: ld %llu < nrows", (unsigned long long)ld);
+    Ctx &c = g_ctx;
+    if (!block_rows) block_rows = std::max<uint64_t>(1, (64ULL << 20) / (ncols * sizeof(uint64_t)));  // ~64 MB
+    block_rows = std::min(block_rows, nrows);
+    const size_t blk_bytes = block_rows * ncols * sizeof(uint64_t);
+    uint64_t *stage = workspace(2, 2 * blk_bytes);
+    if (!stage) return ZKGPU_ERR_OOM;
+    const size_t total = nrows * ncols * sizeof(uint64_t);
+    bool registered = false;
+    if (register_host) {
+        if ((rc = check_hip(hipHostRegister((void *)rows, total, hipHostRegisterDefault), "hipHostRegister")))
+            return rc;
+        registered = true;
+    }
+    hipStream_t cs = nullptr;
+    hipEvent_t copied[2] = {nullptr, nullptr}, freed[2] = {nullptr, nullptr};
+    rc = check_hip(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "copy stream");
+    for (int k = 0; k < 2 && !rc; k++) {
+        rc = check_hip(hipEventCreateWithFlags(&copied[k], hipEventDisableTiming), "event");
+        if (!rc) rc = check_hip(hipEventCreateWithFlags(&freed[k], hipEventDisableTiming), "event");
+    }
+    const uint64_t nblocks = (nrows + block_rows - 1) / block_rows;
+    for (uint64_t b = 0; b < nblocks && !rc; b++) {
+        const int k = (int)(b & 1);
+        const uint64_t r0 = b * block_rows, nr = std::min(block_rows, nrows - r0);
+        uint64_t *buf = stage + (size_t)k * block_rows * ncols;
+        if (b >= 2 && (rc = check_hip(hipStreamWaitEvent(cs, freed[k], 0), "wait"))) break;
+        if ((rc = check_hip(hipMemcpyAsync(buf, rows + r0 * ncols, nr * ncols * sizeof(uint64_t),
+                                           hipMemcpyHostToDevice, cs),
+                            "H2D")))
+            break;
+        if ((rc = check_hip(hipEventRecord(copied[k], cs), "record"))) break;
+        if ((rc = check_hip(hipStreamWaitEvent(c.stream, copied[k], 0), "wait"))) break;
+        rows_to_cols(buf, cols + r0, nr, ncols, ld, c.stream);
+        if ((rc = check_hip(hipEventRecord(freed[k], c.stream), "record"))) break;
+    }
+    if (!rc) rc = check_hip(hipStreamSynchronize(c.stream), "load_rows sync");
+    (void)hipStreamSynchronize(cs);
+    for (int k = 0; k < 2; k++) {
+        if (copied[k]) (void)hipEventDestroy(copied[k]);
+        if (freed[k]) (void)hipEventDestroy(freed[k]);
+    }
+    if (cs) (void)hipStreamDestroy(cs);
+    if (registered) (void)hipHostUnregister((void *)rows);
+    return rc ? rc : check_launch("rows_to_cols");
+}
+
 // ---------------------------------------------------------------- device memory
 int zkgpu_dev_malloc(void **ptr, uint64_t bytes)
 {

@@ -15,6 +15,7 @@
 // process (zklog.error + exitProcess(), exit_process.cpp:7); install a
 // different handler with zkgpu::set_error_handler.
 #pragma once
+#include <vector>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -229,5 +230,29 @@ public:
         return s;
     }
 };
+
+// bctree (tools/starkpil/bctree/build_const_tree.cpp:536-603, GL hash):
+// interpolate + merkletree in one GPU call; returns the whole const-tree file
+// image [nPols, nExt, LDE row-major, nodes] that MerkleTreeGLT(E *tree) and
+// Starks (starks.hpp:193-223) load.  The verkey constRoot is image[size-4..].
+template <typename E>
+inline std::vector<E> buildConstTree(const E *constPols, uint64_t nPols, uint32_t nBits, uint32_t nBitsExt)
+{
+    ensure_init();
+    std::vector<E> image(zkgpu_const_tree_num_elements(nPols, nBitsExt));
+    check(zkgpu_build_const_tree(u64p(image.data()), u64p(constPols), nPols, nBits, nBitsExt), "buildConstTree");
+    return image;
+}
+
+// Executor hand-off (prover.cpp:94-116, commit_pols.hpp:18): stream the
+// committed-pols buffer the executor filled (row-major, stride = width) into a
+// device column-major section without an intermediate host transpose.
+template <typename E>
+inline void loadCommittedPols(uint64_t *devCols, uint64_t ld, const E *rows, uint64_t nRows, uint64_t width,
+                              bool pinSource = true)
+{
+    ensure_init();
+    check(zkgpu_load_rows_dev(devCols, ld, u64p(rows), nRows, width, 0, pinSource ? 1 : 0), "loadCommittedPols");
+}
 
 }  // namespace zkgpu

@@ -52,6 +52,9 @@ _SIGS = {
     "zkgpu_gl_poseidon_batch_dev": (ctypes.c_int, [vp, vp, u64, ctypes.c_int]),
     "zkgpu_gl_merkle_num_elements": (u64, [u64]),
     "zkgpu_gl_merkletree": (ctypes.c_int, [vp, vp, u64, u64]),
+    "zkgpu_const_tree_num_elements": (u64, [u64, u32]),
+    "zkgpu_build_const_tree": (ctypes.c_int, [vp, vp, u64, u32, u32]),
+    "zkgpu_load_rows_dev": (ctypes.c_int, [vp, u64, vp, u64, u64, u64, ctypes.c_int]),
     "zkgpu_gl_merkletree_dev": (ctypes.c_int, [vp, vp, u64, u64, u64]),
     "zkgpu_gl_merkletree_rows_dev": (ctypes.c_int, [vp, vp, u64, u64]),
     "zkgpu_gl_merkle_open_dev": (ctypes.c_int, [vp, vp, vp, vp, u64, u64, u64, vp, u64]),
@@ -215,7 +218,29 @@ def merkletree(src):
     return nodes
 
 
+def build_const_tree(const_pols, n_bits_ext):
+    """bctree: [nPols, nExt, LDE row-major, Merkle nodes] (build_const_tree.cpp:553-603)."""
+    x = _np(const_pols)
+    n = x.shape[0]
+    n_pols = x.shape[1] if x.ndim == 2 else 1
+    n_bits = n.bit_length() - 1
+    assert 1 << n_bits == n, "rows must be a power of two"
+    out = np.zeros(lib().zkgpu_const_tree_num_elements(n_pols, n_bits_ext), np.uint64)
+    buf = x if x.size else np.zeros(1, np.uint64)
+    _check(lib().zkgpu_build_const_tree(out.ctypes.data, buf.ctypes.data, n_pols, n_bits, n_bits_ext),
+           "zkgpu_build_const_tree")
+    return out
+
+
 # ---------------------------------------------------------------- device
+def load_rows_dev(cols, ld, rows, block_rows=0, register_host=False):
+    """Executor hand-off: host row-major (nrows x ncols) -> device column-major."""
+    rows = np.ascontiguousarray(rows, dtype=np.uint64)
+    nrows, ncols = rows.shape
+    _check(lib().zkgpu_load_rows_dev(_addr(cols), ld, rows.ctypes.data, nrows, ncols, block_rows,
+                                     int(register_host)), "zkgpu_load_rows_dev")
+
+
 def ntt_dev(dst, ld_dst, src, ld_src, n, ncols, inverse=False):
     _check(lib().zkgpu_gl_ntt_dev(_addr(dst), ld_dst, _addr(src), ld_src, n, ncols, int(inverse)), "zkgpu_gl_ntt_dev")
 
