@@ -732,17 +732,14 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
     opnd = opv.data();
     const uint32_t n_logz = extend_bits;
     const size_t zh = (size_t)1 << n_logz;
-    size_t off_instr = 0, off_opnd = off_instr + ((n_instr * 16 + 15) & ~15ULL);
-    size_t off_ch = off_opnd + ((n_opnd * 16 + 15) & ~15ULL);
-    size_t off_pub = off_ch + 8 * 24;
-    size_t off_ev = off_pub + ((n_publics * 8 + 15) & ~15ULL);
-    size_t off_zh = off_ev + ((n_evals * 24 + 15) & ~15ULL);
+    if (zh > 64) return set_error(ZKGPU_ERR_ARG, "zxp: extend bits > 6");
+    size_t off_prog = 0;
+    size_t off_zh = off_prog + (size_t)n_instr * sizeof(ZOp);
     size_t total = off_zh + zh * 8 + 16;
     char *p = param_buf(total);
     if (!p) return set_error(ZKGPU_ERR_OOM, "param buffer");
     // zhInv[j] = 1/(7^N * W[eb]^j - 1)  (zhInv.cpp:7-31), N = 2^(log_dom - eb)
     uint64_t zhv[64];
-    if (zh > 64) return set_error(ZKGPU_ERR_ARG, "zxp: extend bits > 6");
     {
         uint64_t sn = h_pow(7, 1ULL << (log_dom - extend_bits));
         uint64_t we = h_w(extend_bits), w = 1;
@@ -752,13 +749,63 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
             w = h_mul(w, we);
         }
     }
+    const uint64_t *zh_dev = (const uint64_t *)(p + off_zh);
+    // pre-decode: resolve every operand to (kind, pointer, shift/slot, stride, immediate)
+    std::vector<ZOp> prog(n_instr);
+    auto decode = [&](const zxp_operand &o, uint32_t &kind, const uint64_t *&ptr, int32_t &ii, uint32_t &ld,
+                      uint64_t *imm) {
+        ptr = nullptr;
+        ii = 0;
+        ld = 0;
+        imm[0] = imm[1] = imm[2] = 0;
+        switch (o.kind) {
+        case ZXP_TMP1: kind = DK_T1; ii = (int32_t)(o.a * 64); break;
+        case ZXP_TMP3: kind = DK_T3; ii = (int32_t)((n_tmp1 + 3 * o.a) * 64); break;
+        case ZXP_COL:
+        case ZXP_COL3:
+            kind = o.kind == ZXP_COL ? DK_C1 : DK_C3;
+            ptr = sections->sec[o.a] + (uint64_t)o.b * sections->ld[o.a];
+            ii = (int32_t)o.c;
+            ld = (uint32_t)sections->ld[o.a];
+            break;
+        case ZXP_LIT: kind = DK_IMM1; imm[0] = ((uint64_t)o.a | ((uint64_t)o.b << 32)) % HP; break;
+        case ZXP_PUB: kind = DK_IMM1; imm[0] = publics[o.a] % HP; break;
+        case ZXP_CHAL:
+            kind = DK_IMM3;
+            for (int t = 0; t < 3; t++) imm[t] = challenges[3 * o.a + t] % HP;
+            break;
+        case ZXP_EVAL:
+            kind = DK_IMM3;
+            for (int t = 0; t < 3; t++) imm[t] = evals[3 * o.a + t] % HP;
+            break;
+        case ZXP_X: kind = DK_X; break;
+        case ZXP_XDIV: kind = DK_I3; ptr = xdiv; break;
+        case ZXP_XDIVW: kind = DK_I3; ptr = xdivw; break;
+        case ZXP_ZI: kind = DK_ZI; ptr = zh_dev; ii = (int32_t)(zh - 1); break;
+        default: kind = DK_IMM1; break;
+        }
+    };
+    for (uint32_t k = 0; k < n_instr; k++) {
+        ZOp &z = prog[k];
+        memset(&z, 0, sizeof(z));
+        z.op = in[k].op;
+        decode(opv[in[k].a], z.ka, z.pa, z.ia, z.lda, z.ima);
+        if (in[k].op != ZXP_COPY) decode(opv[in[k].b], z.kb, z.pb, z.ib, z.ldb, z.imb);
+        const uint64_t *pd;
+        uint64_t dimm[3];
+        decode(opv[in[k].dst], z.kd, pd, z.id, z.ldd, dimm);
+        z.pd = const_cast<uint64_t *>(pd);
+        if (z.kd != DK_T1 && z.kd != DK_T3 && z.kd != DK_C1 && z.kd != DK_C3)
+            return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u writes a read-only operand", k);
+        if ((z.kd == DK_C1 || z.kd == DK_C3) && z.id != 0)
+            return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u writes a shifted column", k);
+    }
+    for (uint32_t k = 0; k < n_opnd; k++)
+        if ((op[k].kind == ZXP_COL || op[k].kind == ZXP_COL3) && sections->ld[op[k].a] > 0xFFFFFFFFULL)
+            return set_error(ZKGPU_ERR_ARG, "zxp: section %u stride exceeds 2^32", op[k].a);
     hipStream_t s = g_ctx.stream;
-    if ((rc = check_hip(hipMemcpyAsync(p + off_instr, instr, n_instr * 16, hipMemcpyHostToDevice, s), "H2D")) ||
-        (rc = check_hip(hipMemcpyAsync(p + off_opnd, opnd, n_opnd * 16, hipMemcpyHostToDevice, s), "H2D")) ||
-        (rc = check_hip(hipMemcpyAsync(p + off_ch, challenges, 8 * 24, hipMemcpyHostToDevice, s), "H2D")) ||
-        (n_publics &&
-         (rc = check_hip(hipMemcpyAsync(p + off_pub, publics, n_publics * 8, hipMemcpyHostToDevice, s), "H2D"))) ||
-        (n_evals && (rc = check_hip(hipMemcpyAsync(p + off_ev, evals, n_evals * 24, hipMemcpyHostToDevice, s), "H2D"))) ||
+    if ((rc = check_hip(hipMemcpyAsync(p + off_prog, prog.data(), n_instr * sizeof(ZOp), hipMemcpyHostToDevice, s),
+                        "H2D")) ||
         (rc = check_hip(hipMemcpyAsync(p + off_zh, zhv, zh * 8, hipMemcpyHostToDevice, s), "H2D")))
         return rc;
     // the sources are pageable host memory (zhv lives on this stack): the
@@ -769,18 +816,17 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
         L.sec[k] = sections->sec[k];
         L.ld[k] = sections->ld[k];
     }
-    L.instr = (const zxp_instr *)(p + off_instr);
-    L.opnd = (const zxp_operand *)(p + off_opnd);
+    L.prog = (const ZOp *)(p + off_prog);
     L.n_instr = n_instr;
     L.n_tmp1 = n_tmp1;
     L.n_tmp3 = n_tmp3;
     L.logdom = log_dom;
-    L.challenges = (const uint64_t *)(p + off_ch);
-    L.publics = (const uint64_t *)(p + off_pub);
-    L.evals = (const uint64_t *)(p + off_ev);
+    L.challenges = nullptr;
+    L.publics = nullptr;
+    L.evals = nullptr;
     L.xdiv = xdiv;
     L.xdivw = xdivw;
-    L.zhinv = (const uint64_t *)(p + off_zh);
+    L.zhinv = zh_dev;
     L.zhinv_mask = (uint32_t)(zh - 1);
     L.x_start = x_start % HP;
     // algorithmic bytes: every distinct column operand read once per row + written columns

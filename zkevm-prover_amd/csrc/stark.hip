@@ -17,8 +17,6 @@
 //   k_qsplit        quotient split (starks.cpp:264-281)
 // F_p^3 arithmetic is associative/commutative and exact, so any reduction
 // order gives the reference's values bit for bit.
-#include <stdlib.h>
-
 #include "gl_device.hpp"
 #include "zkgpu_internal.hpp"
 #include "../../include/zkgpu_zxp.h"
@@ -97,22 +95,10 @@ __global__ void k_rand_cols(uint64_t *base, uint64_t ld, const uint32_t *cols, u
 
 // ---------------------------------------------------------------- ZXP interpreter
 struct ZxpEnv {
-    uint64_t *sec[SEC_COUNT];
-    uint64_t ld[SEC_COUNT];
-    const zxp_instr *instr;
-    const zxp_operand *opnd;
+    const ZOp *prog;
     uint32_t n_instr;
-    uint32_t n_slots;  // LDS slots per thread (tmp1 + 3*tmp3)
-    uint32_t tmp3_base;
     uint32_t logdom;
-    const uint64_t *challenges;  // device, 3 per challenge
-    const uint64_t *publics;
-    const uint64_t *evals;
-    const uint64_t *xdiv;  // dom x 3 interleaved
-    const uint64_t *xdivw;
-    const uint64_t *zhinv;  // 2^eb entries
-    uint32_t zhinv_mask;
-    uint64_t x_start;     // x_i = x_start * omega_dom^i
+    uint64_t x_start;       // x_i = x_start * omega_dom^i
     const uint64_t *tw_lo;  // forward big twiddles (omega_2^28)
     const uint64_t *tw_hi;
 };
@@ -124,131 +110,107 @@ struct Val {
     int dim;
 };
 
-// Temp slot s of virtual row vl lives at lds[s * VL + vl] (VL = 64 * R rows
-// per workgroup), so each LDS access of a wave is 64 consecutive u64.
-template <int VL>
-__device__ __forceinline__ Val zxp_load(const ZxpEnv &e, const zxp_operand &o, const uint64_t *lds, int vl, uint64_t i)
+// Temp slot s of lane l lives at lds[s * 64 + l] (each wave access = 64
+// consecutive u64); the host pre-multiplies slot indices by 64.
+__device__ __forceinline__ Val zxp_load(const ZxpEnv &e, uint32_t kind, const uint64_t *ptr, int32_t ii, uint32_t ld,
+                                        const uint64_t *imm, const uint64_t *lds, int lane, uint64_t i)
 {
     Val r;
     r.dim = 1;
     r.v.v[1] = r.v.v[2] = 0;
-    switch (o.kind) {
-    case ZXP_TMP1: r.v.v[0] = lds[o.a * VL + vl]; break;
-    case ZXP_TMP3: {
-        const uint64_t *p = lds + (e.tmp3_base + 3 * o.a) * VL + vl;
-        r.v = gl3{{p[0], p[VL], p[2 * VL]}};
+    switch (kind) {
+    case DK_T1: r.v.v[0] = lds[ii + lane]; break;
+    case DK_T3: {
+        const uint64_t *p = lds + ii + lane;
+        r.v = gl3{{p[0], p[ZXP_THREADS], p[2 * ZXP_THREADS]}};
         r.dim = 3;
         break;
     }
-    case ZXP_COL:
-    case ZXP_COL3: {
-        const uint64_t dom_mask = (1ULL << e.logdom) - 1;
-        const uint64_t row = (i + (uint64_t)(int64_t)(int32_t)o.c) & dom_mask;
-        const uint64_t ld = e.ld[o.a];
-        const uint64_t *p = e.sec[o.a] + (uint64_t)o.b * ld + row;
-        r.v.v[0] = p[0];
-        if (o.kind == ZXP_COL3) {
-            r.v.v[1] = p[ld];
-            r.v.v[2] = p[2 * ld];
-            r.dim = 3;
-        }
+    case DK_C1: r.v.v[0] = ptr[(i + (uint64_t)(int64_t)ii) & ((1ULL << e.logdom) - 1)]; break;
+    case DK_C3: {
+        const uint64_t *p = ptr + ((i + (uint64_t)(int64_t)ii) & ((1ULL << e.logdom) - 1));
+        r.v = gl3{{p[0], p[ld], p[2 * (uint64_t)ld]}};
+        r.dim = 3;
         break;
     }
-    case ZXP_LIT: r.v.v[0] = (uint64_t)o.a | ((uint64_t)o.b << 32); break;
-    case ZXP_CHAL: r.v = gl3{{e.challenges[3 * o.a], e.challenges[3 * o.a + 1], e.challenges[3 * o.a + 2]}}; r.dim = 3; break;
-    case ZXP_PUB: r.v.v[0] = e.publics[o.a]; break;
-    case ZXP_X: {
+    case DK_IMM1: r.v.v[0] = imm[0]; break;
+    case DK_IMM3: r.v = gl3{{imm[0], imm[1], imm[2]}}; r.dim = 3; break;
+    case DK_X: {
         uint64_t ex = i << (TW_MAX_LOG - e.logdom);
         r.v.v[0] = gl_mul(e.x_start, gl_mul(e.tw_lo[ex & (TW_LEVEL_SIZE - 1)], e.tw_hi[ex >> TW_LEVEL_BITS]));
         break;
     }
-    case ZXP_EVAL: r.v = gl3{{e.evals[3 * o.a], e.evals[3 * o.a + 1], e.evals[3 * o.a + 2]}}; r.dim = 3; break;
-    case ZXP_XDIV: r.v = gl3{{e.xdiv[3 * i], e.xdiv[3 * i + 1], e.xdiv[3 * i + 2]}}; r.dim = 3; break;
-    case ZXP_XDIVW: r.v = gl3{{e.xdivw[3 * i], e.xdivw[3 * i + 1], e.xdivw[3 * i + 2]}}; r.dim = 3; break;
-    case ZXP_ZI: r.v.v[0] = e.zhinv[i & e.zhinv_mask]; break;
+    case DK_I3: r.v = gl3{{ptr[3 * i], ptr[3 * i + 1], ptr[3 * i + 2]}}; r.dim = 3; break;
+    case DK_ZI: r.v.v[0] = ptr[i & (uint32_t)ii]; break;
     default: break;
     }
     return r;
 }
 
-// One wave per workgroup, R rows per thread (rows i0 + 64 r): an instruction
-// is decoded once (wave-uniform scalar loads) and applied to R rows whose
-// operand loads are all issued before any arithmetic.  R > 1 was meant to
-// hide decode/load latency (SQ_WAIT_ANY 0.57 at R = 1) but measured slower
-// (more VGPRs, fewer waves), so the default is R = 1.
-template <int R>
+// One wave per workgroup, one row per lane.  Instruction k is one pre-decoded
+// 128-byte ZOp record read with scalar loads; operands, op and destination
+// are all wave-uniform branches.
 __global__ void __launch_bounds__(ZXP_THREADS) k_zxp_eval(ZxpEnv e)
 {
-    constexpr int VL = ZXP_THREADS * R;
     extern __shared__ __attribute__((aligned(16))) uint64_t zlds[];
     const int lane = threadIdx.x;
-    const uint64_t i0 = (uint64_t)blockIdx.x * VL + lane;
+    const uint64_t i = (uint64_t)blockIdx.x * ZXP_THREADS + lane;
     const uint64_t dom = 1ULL << e.logdom;
+    const bool active = i < dom;
+    const uint64_t ir = active ? i : 0;
     for (uint32_t k = 0; k < e.n_instr; k++) {
-        const zxp_instr in = e.instr[k];
-        const zxp_operand oa = e.opnd[in.a];
-        const zxp_operand ob = e.opnd[in.op == ZXP_COPY ? in.a : in.b];
-        const zxp_operand od = e.opnd[in.dst];
-        Val a[R], b[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            const uint64_t i = i0 + (uint64_t)(ZXP_THREADS * r);
-            a[r] = zxp_load<VL>(e, oa, zlds, lane + ZXP_THREADS * r, i < dom ? i : 0);
-        }
-        if (in.op != ZXP_COPY) {
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                const uint64_t i = i0 + (uint64_t)(ZXP_THREADS * r);
-                b[r] = zxp_load<VL>(e, ob, zlds, lane + ZXP_THREADS * r, i < dom ? i : 0);
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            const uint64_t i = i0 + (uint64_t)(ZXP_THREADS * r);
-            const int vl = lane + ZXP_THREADS * r;
-            Val res;
-            if (in.op == ZXP_COPY) {
-                res = a[r];
+        const ZOp &z = e.prog[k];
+        const uint32_t op = z.op;
+        Val a = zxp_load(e, z.ka, z.pa, z.ia, z.lda, z.ima, zlds, lane, ir);
+        Val r;
+        if (op == ZXP_COPY) {
+            r = a;
+        } else {
+            Val b = zxp_load(e, z.kb, z.pb, z.ib, z.ldb, z.imb, zlds, lane, ir);
+            r.dim = (a.dim == 3 || b.dim == 3) ? 3 : 1;
+            r.v.v[1] = r.v.v[2] = 0;
+            if (op == ZXP_MUL) {
+                if (a.dim == 3 && b.dim == 3)
+                    r.v = gl3_mul(a.v, b.v);
+                else if (a.dim == 3)
+                    r.v = gl3_mul1(a.v, b.v.v[0]);
+                else if (b.dim == 3)
+                    r.v = gl3_mul1(b.v, a.v.v[0]);
+                else
+                    r.v = gl3{{gl_mul(a.v.v[0], b.v.v[0]), 0, 0}};
+            } else if (op == ZXP_ADD) {
+                if (r.dim == 3)
+                    r.v = gl3_add(a.v, b.v);  // a base operand carries zeros in components 1, 2
+                else
+                    r.v.v[0] = gl_add(a.v.v[0], b.v.v[0]);
             } else {
-                res.dim = (a[r].dim == 3 || b[r].dim == 3) ? 3 : 1;
-                if (in.op == ZXP_MUL) {
-                    if (a[r].dim == 3 && b[r].dim == 3)
-                        res.v = gl3_mul(a[r].v, b[r].v);
-                    else if (a[r].dim == 3)
-                        res.v = gl3_mul1(a[r].v, b[r].v.v[0]);
-                    else if (b[r].dim == 3)
-                        res.v = gl3_mul1(b[r].v, a[r].v.v[0]);
-                    else
-                        res.v = gl3{{gl_mul(a[r].v.v[0], b[r].v.v[0]), 0, 0}};
-                } else if (in.op == ZXP_ADD) {
-                    res.v = gl3_add(a[r].v, b[r].v);  // base operands carry zeros in components 1, 2
-                } else {
-                    res.v = gl3_sub(a[r].v, b[r].v);
+                if (r.dim == 3)
+                    r.v = gl3_sub(a.v, b.v);
+                else
+                    r.v.v[0] = gl_sub(a.v.v[0], b.v.v[0]);
+            }
+        }
+        switch (z.kd) {
+        case DK_T1: zlds[z.id + lane] = r.v.v[0]; break;
+        case DK_T3: {
+            uint64_t *p = zlds + z.id + lane;
+            p[0] = r.v.v[0];
+            p[ZXP_THREADS] = r.dim == 3 ? r.v.v[1] : 0;
+            p[2 * ZXP_THREADS] = r.dim == 3 ? r.v.v[2] : 0;
+            break;
+        }
+        case DK_C1:
+        case DK_C3:
+            if (active) {
+                uint64_t *p = z.pd + i;
+                p[0] = gl_canon(r.v.v[0]);
+                if (z.kd == DK_C3) {
+                    p[z.ldd] = r.dim == 3 ? gl_canon(r.v.v[1]) : 0;
+                    p[2 * (uint64_t)z.ldd] = r.dim == 3 ? gl_canon(r.v.v[2]) : 0;
                 }
             }
-            switch (od.kind) {
-            case ZXP_TMP1: zlds[od.a * VL + vl] = res.v.v[0]; break;
-            case ZXP_TMP3: {
-                uint64_t *p = zlds + (e.tmp3_base + 3 * od.a) * VL + vl;
-                p[0] = res.v.v[0];
-                p[VL] = res.dim == 3 ? res.v.v[1] : 0;
-                p[2 * VL] = res.dim == 3 ? res.v.v[2] : 0;
-                break;
-            }
-            case ZXP_COL:
-            case ZXP_COL3:
-                if (i < dom) {
-                    const uint64_t ld = e.ld[od.a];
-                    uint64_t *p = e.sec[od.a] + (uint64_t)od.b * ld + i;
-                    p[0] = gl_canon(res.v.v[0]);
-                    if (od.kind == ZXP_COL3) {
-                        p[ld] = res.dim == 3 ? gl_canon(res.v.v[1]) : 0;
-                        p[2 * ld] = res.dim == 3 ? gl_canon(res.v.v[2]) : 0;
-                    }
-                }
-                break;
-            default: break;
-            }
+            break;
+        default: break;
         }
     }
 }
@@ -551,49 +513,18 @@ int zxp_eval(const ZxpLaunch &L, hipStream_t s)
 {
     Ctx &c = ctx();
     ZxpEnv e;
-    for (int k = 0; k < SEC_COUNT; k++) {
-        e.sec[k] = L.sec[k];
-        e.ld[k] = L.ld[k];
-    }
-    e.instr = L.instr;
-    e.opnd = L.opnd;
+    e.prog = L.prog;
     e.n_instr = L.n_instr;
-    e.n_slots = L.n_tmp1 + 3 * L.n_tmp3;
-    e.tmp3_base = L.n_tmp1;
     e.logdom = L.logdom;
-    e.challenges = L.challenges;
-    e.publics = L.publics;
-    e.evals = L.evals;
-    e.xdiv = L.xdiv;
-    e.xdivw = L.xdivw;
-    e.zhinv = L.zhinv;
-    e.zhinv_mask = L.zhinv_mask;
     e.x_start = L.x_start;
     e.tw_lo = c.tw_lo[0];
     e.tw_hi = c.tw_hi[0];
-    // rows per thread: the most that keeps >= 2 waves per SIMD (8 x 20 KB of LDS per CU)
-    const uint64_t slots = e.n_slots ? e.n_slots : 1;
-    static const int R_max = [] {
-        // tuning override (1, 2 or 4); measured on MI355X, config-4 STARK: the
-        // one-row form is fastest (28.3 ms vs 37.5 / 44.9 ms per launch)
-        const char *v = getenv("ZKGPU_ZXP_ROWS");
-        const int r = v ? atoi(v) : 1;
-        return r >= 4 ? 4 : (r >= 2 ? 2 : 1);
-    }();
-    int R = R_max;
-    while (R > 1 && slots * R * ZXP_THREADS * sizeof(uint64_t) > 20 * 1024) R >>= 1;
+    const uint64_t slots = (uint64_t)L.n_tmp1 + 3ULL * L.n_tmp3;
+    size_t lds = (size_t)(slots ? slots : 1) * ZXP_THREADS * sizeof(uint64_t);
+    if (lds > 160 * 1024) return set_error(ZKGPU_ERR_ARG, "zxp: %llu temp slots exceed LDS", (unsigned long long)slots);
     const uint64_t dom = 1ULL << L.logdom;
-    while (R > 1 && dom < (uint64_t)ZXP_THREADS * R) R >>= 1;
-    size_t lds = (size_t)slots * R * ZXP_THREADS * sizeof(uint64_t);
-    if (lds > 160 * 1024) return set_error(ZKGPU_ERR_ARG, "zxp: %u temp slots exceed LDS", e.n_slots);
     prof_begin(s);
-    const dim3 grid(nblk(dom, ZXP_THREADS * R));
-    if (R == 4)
-        hipLaunchKernelGGL(k_zxp_eval<4>, grid, dim3(ZXP_THREADS), lds, s, e);
-    else if (R == 2)
-        hipLaunchKernelGGL(k_zxp_eval<2>, grid, dim3(ZXP_THREADS), lds, s, e);
-    else
-        hipLaunchKernelGGL(k_zxp_eval<1>, grid, dim3(ZXP_THREADS), lds, s, e);
+    hipLaunchKernelGGL(k_zxp_eval, dim3(nblk(dom, ZXP_THREADS)), dim3(ZXP_THREADS), lds, s, e);
     prof_end("k_zxp_eval", L.bytes, s);
     return check_launch("k_zxp_eval");
 }

@@ -80,11 +80,26 @@ int fri_fold(uint64_t *out, const uint64_t *pol, uint32_t pol_bits, uint32_t out
 int fri_transpose(uint64_t *aux, const uint64_t *pol, uint64_t degree, uint32_t tbits, hipStream_t s);
 
 // ---- stark.hip
+// Pre-decoded ZXP instruction (built on the host by zkgpu_zxp_eval_dev): every
+// operand is resolved to a source kind plus a ready pointer / shift / stride /
+// immediate, so the kernel fetches one 128-byte record per instruction with
+// wave-uniform scalar loads and no dependent descriptor or section lookups.
+enum { DK_T1 = 0, DK_T3, DK_C1, DK_C3, DK_IMM1, DK_IMM3, DK_X, DK_I3, DK_ZI };
+struct alignas(16) ZOp {
+    uint32_t op, ka, kb, kd;
+    const uint64_t *pa, *pb;
+    uint64_t *pd;
+    int32_t ia, ib, id;  // T*: slot offset (slot * 64); C*: row shift; ZI: index mask
+    uint32_t lda, ldb, ldd;
+    uint64_t ima[3], imb[3];
+    uint64_t pad[2];
+};
+static_assert(sizeof(ZOp) == 128, "ZOp is two 64-byte scalar loads");
+
 struct ZxpLaunch {
     uint64_t *sec[SEC_COUNT];
     uint64_t ld[SEC_COUNT];
-    const zxp_instr *instr;  // device
-    const zxp_operand *opnd; // device
+    const ZOp *prog;  // device, n_instr records
     uint32_t n_instr, n_tmp1, n_tmp3;
     uint32_t logdom;
     const uint64_t *challenges, *publics, *evals;  // device
