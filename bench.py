@@ -147,6 +147,37 @@ def cpu_baseline_stark(sample_bits, log_n, blow, ncols, n_queries):
                       % (sample_bits, ncols, n_queries, dt, threads, _cpu_model(), log_n)}
 
 
+VALU_PEAK_WAVE_INSTR_S = 256 * 4 * 2.4e9 / 4  # 256 CUs x 4 SIMDs, one wave64 VALU op per 4 clk @ 2.4 GHz
+
+
+def pmc_for(kernel, args, avg_ms):
+    """HBM traffic and VALU issue for the dominant kernel from the committed
+    PMC summary (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py
+    from separate rocprofv3 --pmc passes of this same default command).
+    Returns (traffic bytes per launch or None, valu dict or None)."""
+    import glob
+    if args.workload != "lde" or args.log_n != 23 or args.ncols != 100 or args.blowup_bits != 1:
+        return None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        try:
+            lab = json.load(open(f)).get("bench_labels", {}).get(kernel)
+        except (OSError, ValueError):
+            continue
+        if not lab:
+            continue
+        traffic = lab.get("hbm_bytes_per_launch")
+        valu = None
+        if lab.get("valu_wave_instr_per_launch"):
+            rate = lab["valu_wave_instr_per_launch"] / (avg_ms * 1e-3)
+            valu = {"kernel": kernel, "wave_instr_per_launch": lab["valu_wave_instr_per_launch"],
+                    "achieved": round(rate / 1e9, 1), "peak": VALU_PEAK_WAVE_INSTR_S / 1e9,
+                    "unit": "G wave-instr/s", "frac": round(rate / VALU_PEAK_WAVE_INSTR_S, 4),
+                    "source": os.path.basename(f)}
+        return traffic, valu
+    return None, None
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -238,6 +269,7 @@ def main():
     launches, ms, by = kernels[dom]
     avg_ms = ms / launches
     achieved = (by / launches) / (avg_ms * 1e-3) / 1e9
+    traffic, valu = pmc_for(dom, args, avg_ms)
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -310,6 +342,7 @@ def main():
                                 "commit": "column-sharded x%d, RCCL all-to-all column->row blocks" % world}.get(
                     args.workload, "column-sharded x%d (no data-path collective)" % world),
             },
+            "valu": valu,
             "roofline": {
                 "kernel": dom,
                 "bound": "hbm",
@@ -317,7 +350,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic,
                 "avg_launch_ms": round(avg_ms, 4),
                 "alg_bytes_per_launch": by / launches,
                 "step_frac": round(alg_step / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),

@@ -101,6 +101,13 @@ for step in "$@"; do
         rc=$?
         cd "$GRAFT_REPO_ROOT"
         ok_or_stop $rc "rocprofv3 pmc WRITE_SIZE"
+        cd /tmp
+        timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_sqb" -o run \
+            --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu --steps 2 --warmup 1 \
+            > /dev/null 2> "$GRAFT_REPO_ROOT/gpurun_out/pmc_sqb.err"
+        rc=$?
+        cd "$GRAFT_REPO_ROOT"
+        ok_or_stop $rc "rocprofv3 pmc SQ_INSTS_VALU"
         ;;
     zxpsweep)
         for r in 1 2 4; do

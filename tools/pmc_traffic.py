@@ -9,6 +9,7 @@ traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
 Usage: tools/pmc_traffic.py <gpurun_out dir> <round tag, e.g. r01>
 """
 import csv
+import re
 import json
 import os
 import shutil
@@ -24,6 +25,26 @@ def per_kernel(path, counter):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
+def bench_label(name):
+    """rocprof kernel name -> the label bench.py / zkgpu_prof_* use."""
+    base = name.split("(")[0].replace("void ", "").replace("zk::", "").strip()
+    m = re.match(r"k_ntt_pass<(\d+), (\d+), \w+>", base)
+    if m:
+        return "k_ntt_pass<%d>" % (int(m.group(1)) + int(m.group(2)))
+    return base
+
+
+def launches(path):
+    n = {}
+    seen = set()
+    for r in csv.DictReader(open(path)):
+        key = (r["Dispatch_Id"], r["Kernel_Name"])
+        if key not in seen:
+            seen.add(key)
+            n[r["Kernel_Name"]] = n.get(r["Kernel_Name"], 0) + 1
+    return n
+
+
 def main():
     src, tag = sys.argv[1], sys.argv[2]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -36,9 +57,31 @@ def main():
         if k in write:
             out[k] = {"FETCH_SIZE_KiB": fetch[k], "WRITE_SIZE_KiB": write[k],
                       "hbm_bytes_per_launch": (2 * fetch[k] + write[k]) * 1024.0}
+    # per bench label, launch-weighted
+    cnt = launches(os.path.join(src, "pmc_write/run_counter_collection.csv"))
+    by_label = {}
+    for k, v in out.items():
+        lab = bench_label(k)
+        b = by_label.setdefault(lab, {"launches": 0, "hbm_bytes": 0.0})
+        b["launches"] += cnt.get(k, 1)
+        b["hbm_bytes"] += v["hbm_bytes_per_launch"] * cnt.get(k, 1)
+    sq = os.path.join(src, "pmc_sqb/run_counter_collection.csv")
+    valu = {}
+    if os.path.exists(sq):
+        vi = per_kernel(sq, "SQ_INSTS_VALU")
+        vc = launches(sq)
+        for k, v in vi.items():
+            lab = bench_label(k)
+            b = valu.setdefault(lab, [0, 0.0])
+            b[0] += vc.get(k, 1)
+            b[1] += v * vc.get(k, 1)
+    labels = {lab: {"hbm_bytes_per_launch": b["hbm_bytes"] / b["launches"]} for lab, b in by_label.items()}
+    for lab, (n, tot) in valu.items():
+        labels.setdefault(lab, {})["valu_wave_instr_per_launch"] = tot / n
     meta = {"_doc": "per-launch HBM traffic = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE half-count "
                     "correction, MI355X_MICROARCH.md HBM); separate --pmc passes of `python3 bench.py --no-cpu "
-                    "--steps 2 --warmup 1`", "kernels": out}
+                    "--steps 2 --warmup 1`; valu_wave_instr_per_launch = SQ_INSTS_VALU (wave instructions) from a separate SQ pass",
+            "kernels": out, "bench_labels": labels}
     with open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w") as f:
         json.dump(meta, f, indent=1)
     shutil.copy(os.path.join(src, "prof/run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
