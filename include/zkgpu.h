@@ -24,6 +24,7 @@
 #define ZKGPU_H
 
 #include <stdint.h>
+#include "zkgpu_zxp.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -167,6 +168,17 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
                        uint32_t n_tmp3, const zkgpu_sections *sections, uint32_t log_dom, const uint64_t *challenges,
                        const uint64_t *publics, uint32_t n_publics, const uint64_t *evals, uint32_t n_evals,
                        const uint64_t *xdiv, const uint64_t *xdivw, uint32_t extend_bits, uint64_t x_start);
+
+/* Host-only compiler behind zkgpu_zxp_eval_dev (include/zkgpu_zxp.h,
+ * "compiled programs"): folds the row-constant operands (challenges 8 x 3,
+ * publics, evals n_evals x 3, literals) into linear-combination instructions
+ * with at most max_terms terms each (0 = default 64, cap 256) and packs the
+ * temporaries.  The output arrays stay valid until the next call on the same
+ * thread.  No GPU needed; used by the tests to check the compiled program
+ * against the source program on the CPU oracle. */
+int zkgpu_zxp_compile(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd, uint32_t n_tmp1,
+                      uint32_t n_tmp3, const uint64_t *challenges, const uint64_t *publics, uint32_t n_publics,
+                      const uint64_t *evals, uint32_t n_evals, uint32_t max_terms, zxp_compiled *out);
 
 /* Polinomial::calculateZ(z, num, den) (polinomial.hpp:586-607), F_p^3 columns
  * (3 consecutive columns of ld each).  *closes = 1 iff z[n-1]*num[n-1]/den[n-1] == 1

@@ -72,6 +72,47 @@ typedef struct {
     uint32_t op, dst, a, b;
 } zxp_instr;
 
+/* ---- compiled programs (zkgpu_zxp_compile, include/zkgpu.h) ---------------
+ * The device does not interpret the producer's op list directly: the host
+ * compiles it first.  Every value is tracked as an affine form
+ * cst + sum_t coef_t * src_t over base-field row values src_t (columns, temps)
+ * with row-constant F_p^3 coefficients (challenges, evals, publics, literals
+ * and their products).  Additions, subtractions, copies and products by a
+ * row-constant operand fold into the form on the host; a form is emitted as
+ * ONE linear-combination instruction only where a row-varying product, a
+ * column store or the term cap needs its value.  Horner chains such as the
+ * reference's FRI polynomial (step52ns: acc = acc*v1 + pol_k) and constraint
+ * combination (step42ns: acc = acc*alpha + C_k) become dot products with
+ * precomputed challenge powers.  Field arithmetic is exact, so the compiled
+ * program computes the same values as the source program.
+ * Compiled instruction ops add:
+ *   ZXP_DOT1 / ZXP_DOT3  dst = sum over terms [a, a+b) of coef * src
+ *                        (result dimension 1 / 3)
+ * and operand kinds add:
+ *   ZXP_IMM   a = index into the constant table (3 u64 per entry), b = dim.
+ * Temporaries are SSA values packed into slots (liveness linear scan). */
+enum { ZXP_DOT1 = 4, ZXP_DOT3 = 5 };
+enum { ZXP_IMM = 12 };
+#define ZXP_TERM_ONE 0xFFFFFFFFu /* term source "1": the form's constant */
+
+typedef struct {
+    uint32_t src;  /* operand index (COL / TMP1 / TMP3) or ZXP_TERM_ONE */
+    uint32_t comp; /* component of a TMP3 source */
+    uint64_t coef[3];
+} zxp_term;
+
+typedef struct {
+    const zxp_instr *instr;
+    uint32_t n_instr;
+    const zxp_operand *opnd;
+    uint32_t n_opnd;
+    const zxp_term *term;
+    uint32_t n_term;
+    const uint64_t *cst; /* n_cst x 3 */
+    uint32_t n_cst;
+    uint32_t n_tmp1, n_tmp3;
+} zxp_compiled;
+
 typedef struct {
     const zxp_instr *instr;
     uint32_t n_instr;

@@ -102,6 +102,10 @@ void oc_zxp_eval(const void *instr, uint32_t n_instr, const void *opnd, uint32_t
                  uint64_t **sec, const uint64_t *stride, uint64_t dom, const uint64_t *challenges,
                  const uint64_t *publics, const uint64_t *evals, const uint64_t *x, const uint64_t *xdiv,
                  const uint64_t *xdivw, const uint64_t *zhinv, uint64_t zhinv_size);
+void oc_zxc_eval(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_tmp1, uint32_t n_tmp3,
+                 const void *term, const uint64_t *cst, uint64_t **sec, const uint64_t *stride, uint64_t dom,
+                 const uint64_t *challenges, const uint64_t *publics, const uint64_t *evals, const uint64_t *x,
+                 const uint64_t *xdiv, const uint64_t *xdivw, const uint64_t *zhinv, uint64_t zhinv_size);
 int oc_calculate_z(uint64_t *z, uint64_t zs, const uint64_t *num, uint64_t ns, const uint64_t *den, uint64_t ds,
                    uint64_t n);
 void oc_evmap(uint64_t *evals, const uint64_t *const *pols, const uint64_t *strides, const uint32_t *dims,

@@ -65,6 +65,9 @@ def lib():
             "oc_zxp_eval": (None, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                    ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, u64, ptr, ptr, ptr, ptr,
                                    ptr, ptr, ptr, u64]),
+            "oc_zxc_eval": (None, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                   ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_void_p, u64, ptr, ptr, ptr, ptr, ptr, ptr, ptr, u64]),
             "oc_calculate_z": (ctypes.c_int, [ptr, u64, ptr, u64, ptr, u64, u64]),
             "oc_evmap": (None, [ptr, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, u64, ptr,
                                 ptr, u64, ctypes.c_uint32]),

@@ -52,6 +52,8 @@ typedef struct {
     const uint64_t *xdiv, *xdivw; /* dom x 3 (2n domain only) */
     const uint64_t *zhinv; /* 2^eb entries */
     uint64_t zhinv_mask;
+    const uint64_t *cst;   /* compiled programs: ZXP_IMM constants (3 each) */
+    const zxp_term *term;  /* compiled programs: DOT terms */
 } env_t;
 
 static inline val load(const env_t *e, const zxp_operand *o, const uint64_t *t1, const uint64_t *t3, uint64_t i)
@@ -80,7 +82,25 @@ static inline val load(const env_t *e, const zxp_operand *o, const uint64_t *t1,
     case ZXP_XDIV: memcpy(r.v, e->xdiv + 3 * i, 24); r.dim = 3; break;
     case ZXP_XDIVW: memcpy(r.v, e->xdivw + 3 * i, 24); r.dim = 3; break;
     case ZXP_ZI: r.v[0] = e->zhinv[i & e->zhinv_mask]; break;
+    case ZXP_IMM: memcpy(r.v, e->cst + 3 * o->a, 24); r.dim = (int)o->b; break;
     default: break;
+    }
+    return r;
+}
+
+/* compiled DOT (include/zkgpu_zxp.h): sum of coef * (base source value) */
+static inline val dot(const env_t *e, const zxp_operand *opnd, const zxp_instr *in, const uint64_t *t1,
+                      const uint64_t *t3, uint64_t i)
+{
+    val r = {{0, 0, 0}, in->op == ZXP_DOT3 ? 3 : 1};
+    for (uint32_t k = in->a; k < in->a + in->b; k++) {
+        const zxp_term *t = &e->term[k];
+        uint64_t x = 1;
+        if (t->src != ZXP_TERM_ONE) {
+            val s = load(e, &opnd[t->src], t1, t3, i);
+            x = s.v[t->comp];
+        }
+        for (int c = 0; c < 3; c++) r.v[c] = gl_add(r.v[c], gl_mul(t->coef[c], x));
     }
     return r;
 }
@@ -132,14 +152,16 @@ static inline val binop(uint32_t op, const val *a, const val *b)
     return r;
 }
 
-void oc_zxp_eval(const void *instr_v, uint32_t n_instr, const void *opnd_v, uint32_t n_tmp1,
-                 uint32_t n_tmp3, uint64_t **sec, const uint64_t *stride, uint64_t dom, const uint64_t *challenges,
-                 const uint64_t *publics, const uint64_t *evals, const uint64_t *x, const uint64_t *xdiv,
-                 const uint64_t *xdivw, const uint64_t *zhinv, uint64_t zhinv_size)
+static void zxp_run(const void *instr_v, uint32_t n_instr, const void *opnd_v, uint32_t n_tmp1, uint32_t n_tmp3,
+                    uint64_t **sec, const uint64_t *stride, uint64_t dom, const uint64_t *challenges,
+                    const uint64_t *publics, const uint64_t *evals, const uint64_t *x, const uint64_t *xdiv,
+                    const uint64_t *xdivw, const uint64_t *zhinv, uint64_t zhinv_size, const uint64_t *cst,
+                    const zxp_term *term)
 {
     const zxp_instr *instr = (const zxp_instr *)instr_v;
     const zxp_operand *opnd = (const zxp_operand *)opnd_v;
-    env_t e = {sec, stride, dom, challenges, publics, evals, x, xdiv, xdivw, zhinv, zhinv_size ? zhinv_size - 1 : 0};
+    env_t e = {sec, stride, dom, challenges, publics, evals, x, xdiv, xdivw, zhinv, zhinv_size ? zhinv_size - 1 : 0,
+               cst, term};
 #pragma omp parallel
     {
         uint64_t *t1 = (uint64_t *)calloc(n_tmp1 + 1, sizeof(uint64_t));
@@ -148,9 +170,12 @@ void oc_zxp_eval(const void *instr_v, uint32_t n_instr, const void *opnd_v, uint
         for (uint64_t i = 0; i < dom; i++) {
             for (uint32_t k = 0; k < n_instr; k++) {
                 const zxp_instr *in = &instr[k];
-                val a = load(&e, &opnd[in->a], t1, t3, i);
+                val a = {{0, 0, 0}, 1};
+                if (in->op <= ZXP_COPY) a = load(&e, &opnd[in->a], t1, t3, i);
                 val r;
-                if (in->op == ZXP_COPY) {
+                if (in->op == ZXP_DOT1 || in->op == ZXP_DOT3) {
+                    r = dot(&e, opnd, in, t1, t3, i);
+                } else if (in->op == ZXP_COPY) {
                     r = a;
                 } else {
                     val b = load(&e, &opnd[in->b], t1, t3, i);
@@ -162,6 +187,26 @@ void oc_zxp_eval(const void *instr_v, uint32_t n_instr, const void *opnd_v, uint
         free(t1);
         free(t3);
     }
+}
+
+void oc_zxp_eval(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_tmp1, uint32_t n_tmp3,
+                 uint64_t **sec, const uint64_t *stride, uint64_t dom, const uint64_t *challenges,
+                 const uint64_t *publics, const uint64_t *evals, const uint64_t *x, const uint64_t *xdiv,
+                 const uint64_t *xdivw, const uint64_t *zhinv, uint64_t zhinv_size)
+{
+    zxp_run(instr, n_instr, opnd, n_tmp1, n_tmp3, sec, stride, dom, challenges, publics, evals, x, xdiv, xdivw, zhinv,
+            zhinv_size, NULL, NULL);
+}
+
+/* a compiled program (zkgpu_zxp_compile output): checks the compiler against
+ * the source program on the same inputs */
+void oc_zxc_eval(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_tmp1, uint32_t n_tmp3,
+                 const void *term, const uint64_t *cst, uint64_t **sec, const uint64_t *stride, uint64_t dom,
+                 const uint64_t *challenges, const uint64_t *publics, const uint64_t *evals, const uint64_t *x,
+                 const uint64_t *xdiv, const uint64_t *xdivw, const uint64_t *zhinv, uint64_t zhinv_size)
+{
+    zxp_run(instr, n_instr, opnd, n_tmp1, n_tmp3, sec, stride, dom, challenges, publics, evals, x, xdiv, xdivw, zhinv,
+            zhinv_size, cst, (const zxp_term *)term);
 }
 
 /* Polinomial::calculateZ: z[0] = 1, z[i] = z[i-1] * num[i-1] / den[i-1];

@@ -178,3 +178,57 @@ def test_step42ns_stage(oracle, zkgpu, n_bits, blow):
     zkgpu.ntt_dev(cm4, NE, qq2, NE, NE, inst.q_deg * 3)
     torch.cuda.synchronize()
     assert np.array_equal(zkgpu.from_device(cm4).T, o.S[8])
+
+
+@pytest.mark.parametrize("name", ["step1", "step2", "step3prev", "step42ns", "step52ns"])
+@pytest.mark.parametrize("mode", [("1", "0"), ("1", "3"), ("0", "0")])
+def test_zxp_programs_vs_oracle(oracle, zkgpu, name, mode, monkeypatch):
+    """Each synthetic program on random sections: the GPU (compiled with
+    linear-combination fusion at the default / a tiny term cap, and the
+    unfused source program) equals the oracle's evaluation of the SOURCE
+    program, bit for bit."""
+    import ctypes
+    import torch
+    from zkgpu.synthetic import SyntheticStark
+    monkeypatch.setenv("ZKGPU_ZXP_FUSE", mode[0])
+    monkeypatch.setenv("ZKGPU_ZXP_MAX_TERMS", mode[1])
+    inst = SyntheticStark(n_bits=9, blowup_bits=1, t=8, m=3, n_free=4, n_lookups=2, n_queries=8)
+    prog = inst.programs[name]
+    eb = inst.blowup_bits
+    logd = inst.n_bits_ext if prog.domain_ext else inst.n_bits
+    dom = 1 << logd
+    rng = np.random.default_rng(sum(map(ord, name)))
+    widths = {0: inst.n_cm1, 1: inst.n_cm2, 2: inst.n_cm3, 3: inst.n_tmp, 4: inst.n_const, 5: inst.n_cm1,
+              6: inst.n_cm2, 7: inst.n_cm3, 8: inst.n_cm4, 9: inst.n_const, 10: 3, 11: 3}
+    S = {k: rand_gl(rng, (dom, w)) for k, w in widths.items()}
+    chal = rand_gl(rng, (8, 3))
+    pub = rand_gl(rng, inst.n_publics)
+    evals = rand_gl(rng, (len(inst.evmap), 3))
+    xdiv = rand_gl(rng, (dom, 3))
+    xdivw = rand_gl(rng, (dom, 3))
+    x_start = 7 if prog.domain_ext else 1
+    x = np.zeros(dom, np.uint64)
+    oracle.lib().oc_powers(oracle._p(x), x_start, oracle.gl_w(logd), dom)
+    n = dom >> eb if prog.domain_ext else dom
+    wE = oracle.gl_w(eb)
+    zh = np.array([pow((pow(7, n, P) * pow(wE, i, P) - 1) % P, P - 2, P) for i in range(1 << eb)], np.uint64)
+    # device copies (column-major) before the oracle writes its outputs
+    secs = {k: (zkgpu.to_device(np.ascontiguousarray(a.T)), dom, a.shape[1]) for k, a in S.items()}
+    dx = zkgpu.to_device(xdiv)
+    dxw = zkgpu.to_device(xdivw)
+    ins, opn = prog.arrays()
+    sp = (ctypes.c_void_p * 12)()
+    strides = np.zeros(12, np.uint64)
+    for k, a in S.items():
+        sp[k] = a.ctypes.data
+        strides[k] = a.shape[1]
+    p = oracle._p
+    oracle.lib().oc_zxp_eval(ctypes.c_void_p(ins.ctypes.data), ins.shape[0], ctypes.c_void_p(opn.ctypes.data),
+                             max(prog.n_tmp1, 1), max(prog.n_tmp3, 1), ctypes.cast(sp, ctypes.c_void_p),
+                             ctypes.c_void_p(strides.ctypes.data), dom, p(chal), p(pub), p(evals), p(x), p(xdiv),
+                             p(xdivw), p(zh), zh.size)
+    zkgpu.zxp_eval_dev(prog, secs, logd, chal, pub, evals, dx if prog.domain_ext else None,
+                       dxw if prog.domain_ext else None, extend_bits=eb, x_start=x_start)
+    torch.cuda.synchronize()
+    for k, (t, _, _) in secs.items():
+        assert np.array_equal(zkgpu.from_device(t).T, S[k]), "section %d" % k

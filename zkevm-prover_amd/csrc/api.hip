@@ -645,6 +645,25 @@ int zkgpu_rand_cols_dev(uint64_t *base, uint64_t ld, const uint32_t *cols, uint3
     return rand_cols(base, ld, (const uint32_t *)p, ncols, nrows, seed, stream, g_ctx.stream);
 }
 
+// Dot3 limbs of coefficient c (canonical): 22/21/21-bit limbs of c and of
+// c * 2^32 mod p (csrc/gl_device.hpp Dot3::term)
+static void zxp_limbs6(uint64_t c, uint32_t out[6])
+{
+    const uint64_t cs = h_mul(c, 1ULL << 32);
+    const uint64_t v[2] = {c, cs};
+    for (int h = 0; h < 2; h++) {
+        out[3 * h] = (uint32_t)(v[h] & ((1u << 22) - 1));
+        out[3 * h + 1] = (uint32_t)((v[h] >> 22) & ((1u << 21) - 1));
+        out[3 * h + 2] = (uint32_t)(v[h] >> 43);
+    }
+}
+
+static inline uint64_t h_add(uint64_t a, uint64_t b)
+{
+    const uint64_t s = a + b;  // a, b < p
+    return (s < a || s >= HP) ? s - HP : s;
+}
+
 // Temp-slot allocation for a ZXP program.  Program producers (the synthetic
 // builder, a chelpers converter) may give every intermediate its own temp;
 // the LDS footprint per workgroup is (slots x 64 rows x 8 B), which bounds
@@ -727,14 +746,45 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
         }
         if (bad) return set_error(ZKGPU_ERR_ARG, "zxp: operand %u (kind %u) invalid", k, o.kind);
     }
-    std::vector<zxp_operand> opv(op, op + n_opnd);
-    zxp_alloc_slots(in, n_instr, opv, n_tmp1, n_tmp3);
-    opnd = opv.data();
+    // compile (csrc/zxp_compile.cpp): linear-combination fusion + SSA slots.
+    // ZKGPU_ZXP_FUSE=0 runs the source program as is (slot packing only).
+    const char *env_fuse = getenv("ZKGPU_ZXP_FUSE");
+    const char *env_terms = getenv("ZKGPU_ZXP_MAX_TERMS");
+    const int fuse = env_fuse ? atoi(env_fuse) : 1;
+    const uint32_t max_terms = env_terms ? (uint32_t)atoi(env_terms) : 0u;
+    std::vector<zxp_operand> opv;
+    const zxp_instr *pin = in;
+    const zxp_term *terms = nullptr;
+    const uint64_t *csts = nullptr;
+    uint32_t n_terms = 0;
+    if (fuse) {
+        zxp_compiled cp;
+        if ((rc = zkgpu_zxp_compile(instr, n_instr, opnd, n_opnd, n_tmp1, n_tmp3, challenges, publics, n_publics,
+                                    evals, n_evals, max_terms, &cp)))
+            return rc;
+        pin = cp.instr;
+        n_instr = cp.n_instr;
+        opv.assign(cp.opnd, cp.opnd + cp.n_opnd);
+        terms = cp.term;
+        n_terms = cp.n_term;
+        csts = cp.cst;
+        n_tmp1 = cp.n_tmp1;
+        n_tmp3 = cp.n_tmp3;
+    } else {
+        opv.assign(op, op + n_opnd);
+        zxp_alloc_slots(in, n_instr, opv, n_tmp1, n_tmp3);
+    }
+    const uint32_t n_dot_terms = [&] {
+        uint32_t c = 0;
+        for (uint32_t t = 0; t < n_terms; t++) c += terms[t].src != ZXP_TERM_ONE;
+        return c;
+    }();
     const uint32_t n_logz = extend_bits;
     const size_t zh = (size_t)1 << n_logz;
     if (zh > 64) return set_error(ZKGPU_ERR_ARG, "zxp: extend bits > 6");
     size_t off_prog = 0;
-    size_t off_zh = off_prog + (size_t)n_instr * sizeof(ZOp);
+    size_t off_terms = off_prog + (size_t)std::max<uint32_t>(n_instr, 1) * sizeof(ZOp);
+    size_t off_zh = off_terms + (size_t)n_dot_terms * sizeof(ZTerm);
     size_t total = off_zh + zh * 8 + 16;
     char *p = param_buf(total);
     if (!p) return set_error(ZKGPU_ERR_OOM, "param buffer");
@@ -778,6 +828,10 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
             kind = DK_IMM3;
             for (int t = 0; t < 3; t++) imm[t] = evals[3 * o.a + t] % HP;
             break;
+        case ZXP_IMM:
+            kind = o.b == 3 ? DK_IMM3 : DK_IMM1;
+            for (int t = 0; t < 3; t++) imm[t] = csts[3 * o.a + t];
+            break;
         case ZXP_X: kind = DK_X; break;
         case ZXP_XDIV: kind = DK_I3; ptr = xdiv; break;
         case ZXP_XDIVW: kind = DK_I3; ptr = xdivw; break;
@@ -785,20 +839,64 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
         default: kind = DK_IMM1; break;
         }
     };
+    std::vector<ZTerm> zterms;
+    zterms.reserve(n_dot_terms);
     for (uint32_t k = 0; k < n_instr; k++) {
         ZOp &z = prog[k];
         memset(&z, 0, sizeof(z));
-        z.op = in[k].op;
-        decode(opv[in[k].a], z.ka, z.pa, z.ia, z.lda, z.ima);
-        if (in[k].op != ZXP_COPY) decode(opv[in[k].b], z.kb, z.pb, z.ib, z.ldb, z.imb);
+        z.op = pin[k].op;
+        if (z.op == ZXP_DOT1 || z.op == ZXP_DOT3) {
+            uint64_t c0[3] = {0, 0, 0};
+            z.ia = (int32_t)zterms.size();
+            for (uint32_t t = pin[k].a; t < pin[k].a + pin[k].b; t++) {
+                const zxp_term &tm = terms[t];
+                if (tm.src == ZXP_TERM_ONE) {
+                    for (int j = 0; j < 3; j++) c0[j] = h_add(c0[j], tm.coef[j] % HP);
+                    continue;
+                }
+                ZTerm zt;
+                memset(&zt, 0, sizeof(zt));
+                const zxp_operand &o = opv[tm.src];
+                if (o.kind == ZXP_COL) {
+                    zt.kind = DK_C1;
+                    zt.ptr = sections->sec[o.a] + (uint64_t)o.b * sections->ld[o.a];
+                    zt.ii = (int32_t)o.c;
+                } else if (o.kind == ZXP_TMP1) {
+                    zt.kind = DK_T1;
+                    zt.ii = (int32_t)(o.a * 64);
+                } else if (o.kind == ZXP_TMP3) {
+                    zt.kind = DK_T1;
+                    zt.ii = (int32_t)((n_tmp1 + 3 * o.a + tm.comp) * 64);
+                } else {
+                    return set_error(ZKGPU_ERR_ARG, "zxp: DOT term source kind %u", o.kind);
+                }
+                for (int j = 0; j < 3; j++) zxp_limbs6(tm.coef[j] % HP, zt.c[j]);
+                zterms.push_back(zt);
+            }
+            z.ib = (int32_t)(zterms.size() - (size_t)z.ia);
+            uint32_t *kl = reinterpret_cast<uint32_t *>(z.ima);  // 9 u32 over ima/imb
+            for (int j = 0; j < 3; j++) {
+                kl[3 * j] = (uint32_t)(c0[j] & ((1u << 22) - 1));
+                kl[3 * j + 1] = (uint32_t)((c0[j] >> 22) & ((1u << 21) - 1));
+                kl[3 * j + 2] = (uint32_t)(c0[j] >> 43);
+            }
+        } else {
+            decode(opv[pin[k].a], z.ka, z.pa, z.ia, z.lda, z.ima);
+            if (pin[k].op != ZXP_COPY) decode(opv[pin[k].b], z.kb, z.pb, z.ib, z.ldb, z.imb);
+        }
         const uint64_t *pd;
         uint64_t dimm[3];
-        decode(opv[in[k].dst], z.kd, pd, z.id, z.ldd, dimm);
+        decode(opv[pin[k].dst], z.kd, pd, z.id, z.ldd, dimm);
         z.pd = const_cast<uint64_t *>(pd);
         if (z.kd != DK_T1 && z.kd != DK_T3 && z.kd != DK_C1 && z.kd != DK_C3)
             return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u writes a read-only operand", k);
         if ((z.kd == DK_C1 || z.kd == DK_C3) && z.id != 0)
             return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u writes a shifted column", k);
+    }
+    {
+        const uint64_t slots = (uint64_t)n_tmp1 + 3ULL * n_tmp3;
+        if (slots * 64 * 8 > 160 * 1024)
+            return set_error(ZKGPU_ERR_ARG, "zxp: %llu temp slots exceed LDS", (unsigned long long)slots);
     }
     for (uint32_t k = 0; k < n_opnd; k++)
         if ((op[k].kind == ZXP_COL || op[k].kind == ZXP_COL3) && sections->ld[op[k].a] > 0xFFFFFFFFULL)
@@ -806,6 +904,10 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
     hipStream_t s = g_ctx.stream;
     if ((rc = check_hip(hipMemcpyAsync(p + off_prog, prog.data(), n_instr * sizeof(ZOp), hipMemcpyHostToDevice, s),
                         "H2D")) ||
+        (zterms.size() &&
+         (rc = check_hip(hipMemcpyAsync(p + off_terms, zterms.data(), zterms.size() * sizeof(ZTerm),
+                                        hipMemcpyHostToDevice, s),
+                         "H2D"))) ||
         (rc = check_hip(hipMemcpyAsync(p + off_zh, zhv, zh * 8, hipMemcpyHostToDevice, s), "H2D")))
         return rc;
     // the sources are pageable host memory (zhv lives on this stack): the
@@ -817,6 +919,7 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
         L.ld[k] = sections->ld[k];
     }
     L.prog = (const ZOp *)(p + off_prog);
+    L.terms = (const ZTerm *)(p + off_terms);
     L.n_instr = n_instr;
     L.n_tmp1 = n_tmp1;
     L.n_tmp3 = n_tmp3;

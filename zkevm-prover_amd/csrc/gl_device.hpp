@@ -154,4 +154,40 @@ __device__ __forceinline__ gl3 gl3_mul(const gl3 &a, const gl3 &b)
     return r;
 }
 
+// ---------------------------------------------------------------- dot products
+// Dot product of lazy lanes with table coefficients, one reduction at the end.
+// Coefficient c is stored as 22/21/21-bit limbs of c and of c*2^32 mod p
+// (tools/gen_poseidon_sparse.py limbs6; api.hip zxp_limbs6 for ZXP_DOT), so
+// a = a0 + a1*2^32 contributes a0*c_k + a1*c'_k to accumulator k (weights
+// 2^0, 2^22, 2^43): six carry-free 32x32->64 multiply-adds per term, each
+// term adding < 2^55 (< 2^61 for <= 34 terms, < 2^63 for <= 250).
+struct Dot3 {
+    uint64_t A0, A1, A2;
+    __device__ __forceinline__ explicit Dot3(const uint32_t *k) : A0(k[0]), A1(k[1]), A2(k[2]) {}
+    __device__ __forceinline__ void term(uint64_t a, const uint32_t *c)
+    {
+        const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);
+        A0 += (uint64_t)a0 * c[0];
+        A1 += (uint64_t)a0 * c[1];
+        A2 += (uint64_t)a0 * c[2];
+        A0 += (uint64_t)a1 * c[3];
+        A1 += (uint64_t)a1 * c[4];
+        A2 += (uint64_t)a1 * c[5];
+    }
+    // coefficient 1: a0 -> A0, a1 * 2^32 = a1 * 2^10 * 2^22 -> A1
+    __device__ __forceinline__ void lane(uint64_t a)
+    {
+        A0 += (uint32_t)a;
+        A1 += (uint64_t)(uint32_t)(a >> 32) << 10;
+    }
+    __device__ __forceinline__ uint64_t fin() const
+    {
+        uint64_t l1, l2;
+        const uint32_t c1 = __builtin_add_overflow(A0, A1 << 22, &l1) ? 1u : 0u;
+        const uint32_t c2 = __builtin_add_overflow(l1, A2 << 43, &l2) ? 1u : 0u;
+        const uint64_t h = (A1 >> 42) + (A2 >> 21) + c1 + c2;  // < 2^41
+        return gl_reduce128(l2, h);
+    }
+};
+
 }  // namespace zk

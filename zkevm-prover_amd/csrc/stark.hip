@@ -96,6 +96,7 @@ __global__ void k_rand_cols(uint64_t *base, uint64_t ld, const uint32_t *cols, u
 // ---------------------------------------------------------------- ZXP interpreter
 struct ZxpEnv {
     const ZOp *prog;
+    const ZTerm *terms;
     uint32_t n_instr;
     uint32_t logdom;
     uint64_t x_start;       // x_i = x_start * omega_dom^i
@@ -158,11 +159,41 @@ __global__ void __launch_bounds__(ZXP_THREADS) k_zxp_eval(ZxpEnv e)
     const uint64_t dom = 1ULL << e.logdom;
     const bool active = i < dom;
     const uint64_t ir = active ? i : 0;
+    const uint64_t dmask = dom - 1;
     for (uint32_t k = 0; k < e.n_instr; k++) {
         const ZOp &z = e.prog[k];
         const uint32_t op = z.op;
-        Val a = zxp_load(e, z.ka, z.pa, z.ia, z.lda, z.ima, zlds, lane, ir);
         Val r;
+        if (op >= ZXP_DOT1) {
+            // linear combination (csrc/zxp_compile.cpp): sum of coef * source,
+            // carry-free limb accumulation, one reduction per component
+            const uint32_t *k0 = reinterpret_cast<const uint32_t *>(z.ima);
+            Dot3 d0(k0), d1(k0 + 3), d2(k0 + 6);
+            const ZTerm *T = e.terms + z.ia;
+            const int nt = z.ib;
+            if (op == ZXP_DOT3) {
+                for (int t = 0; t < nt; t++) {
+                    const ZTerm &tt = T[t];
+                    const uint64_t a =
+                        tt.kind == DK_T1 ? zlds[tt.ii + lane] : tt.ptr[(ir + (uint64_t)(int64_t)tt.ii) & dmask];
+                    d0.term(a, tt.c[0]);
+                    d1.term(a, tt.c[1]);
+                    d2.term(a, tt.c[2]);
+                }
+                r.v = gl3{{d0.fin(), d1.fin(), d2.fin()}};
+                r.dim = 3;
+            } else {
+                for (int t = 0; t < nt; t++) {
+                    const ZTerm &tt = T[t];
+                    const uint64_t a =
+                        tt.kind == DK_T1 ? zlds[tt.ii + lane] : tt.ptr[(ir + (uint64_t)(int64_t)tt.ii) & dmask];
+                    d0.term(a, tt.c[0]);
+                }
+                r.v = gl3{{d0.fin(), 0, 0}};
+                r.dim = 1;
+            }
+        } else {
+        Val a = zxp_load(e, z.ka, z.pa, z.ia, z.lda, z.ima, zlds, lane, ir);
         if (op == ZXP_COPY) {
             r = a;
         } else {
@@ -189,6 +220,7 @@ __global__ void __launch_bounds__(ZXP_THREADS) k_zxp_eval(ZxpEnv e)
                 else
                     r.v.v[0] = gl_sub(a.v.v[0], b.v.v[0]);
             }
+        }
         }
         switch (z.kd) {
         case DK_T1: zlds[z.id + lane] = r.v.v[0]; break;
@@ -514,6 +546,7 @@ int zxp_eval(const ZxpLaunch &L, hipStream_t s)
     Ctx &c = ctx();
     ZxpEnv e;
     e.prog = L.prog;
+    e.terms = L.terms;
     e.n_instr = L.n_instr;
     e.logdom = L.logdom;
     e.x_start = L.x_start;

@@ -90,16 +90,29 @@ struct alignas(16) ZOp {
     const uint64_t *pa, *pb;
     uint64_t *pd;
     int32_t ia, ib, id;  // T*: slot offset (slot * 64); C*: row shift; ZI: index mask
+                         // DOT: ia = first term, ib = term count; ima/imb = constant limbs (9 u32)
     uint32_t lda, ldb, ldd;
     uint64_t ima[3], imb[3];
     uint64_t pad[2];
 };
 static_assert(sizeof(ZOp) == 128, "ZOp is two 64-byte scalar loads");
 
+// ZXP_DOT term: source (a column at a row shift, or an LDS temp slot
+// component) and its F_p^3 coefficient as Dot3 limbs (3 components x 6).
+struct alignas(16) ZTerm {
+    uint32_t kind;  // DK_C1 or DK_T1
+    int32_t ii;     // C1: row shift; T1: LDS offset (slot * 64)
+    const uint64_t *ptr;
+    uint32_t c[3][6];
+    uint32_t pad[2];
+};
+static_assert(sizeof(ZTerm) == 96, "ZTerm is 96 bytes");
+
 struct ZxpLaunch {
     uint64_t *sec[SEC_COUNT];
     uint64_t ld[SEC_COUNT];
     const ZOp *prog;  // device, n_instr records
+    const ZTerm *terms;  // device, DOT terms
     uint32_t n_instr, n_tmp1, n_tmp3;
     uint32_t logdom;
     const uint64_t *challenges, *publics, *evals;  // device

@@ -70,6 +70,7 @@ _SIGS = {
     "zkgpu_rand_cols_dev": (ctypes.c_int, [vp, u64, vp, u32, u64, u64, u64]),
     "zkgpu_zxp_eval_dev": (ctypes.c_int, [vp, u32, vp, u32, u32, u32, vp, u32, vp, vp, u32, vp, u32, vp, vp, u32,
                                           u64]),
+    "zkgpu_zxp_compile": (ctypes.c_int, [vp, u32, vp, u32, u32, u32, vp, vp, u32, vp, u32, u32, vp]),
     "zkgpu_calculate_z_dev": (ctypes.c_int, [vp, u64, vp, u64, vp, u64, u64, ctypes.POINTER(ctypes.c_int)]),
     "zkgpu_evmap_dev": (ctypes.c_int, [vp, vp, vp, vp, vp, u32, vp, vp, u64, u64, u32]),
     "zkgpu_xdivxsub_dev": (ctypes.c_int, [vp, vp, vp, u32, u32]),
@@ -344,6 +345,44 @@ def zxp_eval_dev(prog, sections, log_dom, challenges, publics, evals=None, xdiv=
                                     max(nt3, 1), ctypes.byref(s), log_dom, ch.ctypes.data, pub.ctypes.data,
                                     pub.size if publics is not None else 0, ev.ctypes.data, ev.size // 3,
                                     _addr(xdiv), _addr(xdivw), extend_bits, x_start), "zkgpu_zxp_eval_dev")
+
+
+class ZxpCompiled(ctypes.Structure):
+    """zxp_compiled (include/zkgpu_zxp.h)."""
+    _fields_ = [("instr", vp), ("n_instr", u32), ("opnd", vp), ("n_opnd", u32), ("term", vp), ("n_term", u32),
+                ("cst", vp), ("n_cst", u32), ("n_tmp1", u32), ("n_tmp3", u32)]
+
+
+ZXP_TERM_DTYPE = np.dtype([("src", np.uint32), ("comp", np.uint32), ("coef", np.uint64, 3)])
+
+
+def zxp_compile(prog, challenges, publics, evals=None, max_terms=0):
+    """Host-only compile of a ZXP program (zkgpu_zxp_compile, no GPU needed).
+    Returns dict(instr, opnd, term, cst, n_tmp1, n_tmp3) of numpy copies."""
+    ins, opn = prog.arrays()
+    ins = np.ascontiguousarray(ins, np.uint32)
+    opn = np.ascontiguousarray(opn, np.uint32)
+    ch = np.zeros(24, np.uint64)
+    c = _np(challenges).reshape(-1)
+    ch[:c.size] = c
+    pub = _np(publics if publics is not None else np.zeros(1, np.uint64))
+    ev = _np(evals if evals is not None else np.zeros(3, np.uint64)).reshape(-1)
+    out = ZxpCompiled()
+    _check(lib().zkgpu_zxp_compile(ins.ctypes.data, ins.shape[0], opn.ctypes.data, opn.shape[0],
+                                   max(prog.n_tmp1, 1), max(prog.n_tmp3, 1), ch.ctypes.data, pub.ctypes.data,
+                                   pub.size if publics is not None else 0, ev.ctypes.data, ev.size // 3, max_terms,
+                                   ctypes.byref(out)), "zkgpu_zxp_compile")
+
+    def grab(ptr, n, dtype, width):
+        if n == 0:
+            return np.zeros((0, width) if width else 0, dtype)
+        nbytes = n * (width or 1) * np.dtype(dtype).itemsize
+        a = np.frombuffer(ctypes.string_at(ptr, nbytes), dtype=dtype).copy()
+        return a.reshape(n, width) if width else a
+
+    return {"instr": grab(out.instr, out.n_instr, np.uint32, 4), "opnd": grab(out.opnd, out.n_opnd, np.uint32, 4),
+            "term": grab(out.term, out.n_term, ZXP_TERM_DTYPE, 0), "cst": grab(out.cst, out.n_cst, np.uint64, 3),
+            "n_tmp1": out.n_tmp1, "n_tmp3": out.n_tmp3}
 
 
 def h1h2_dev(h1, h1_ld, h2, h2_ld, f, f_ld, t, t_ld, n, dim):
