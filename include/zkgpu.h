@@ -180,6 +180,15 @@ int zkgpu_zxp_compile(const void *instr, uint32_t n_instr, const void *opnd, uin
                       uint32_t n_tmp3, const uint64_t *challenges, const uint64_t *publics, uint32_t n_publics,
                       const uint64_t *evals, uint32_t n_evals, uint32_t max_terms, zxp_compiled *out);
 
+/* Diagnostics for the run-time compiled expression kernels (csrc/zxp_jit.hip):
+ * compile a program exactly as zkgpu_zxp_eval_dev does and write the
+ * generated straight-line HIP kernel source into buf (truncated to buflen);
+ * with rtc_check != 0 also compile it for gfx950 with hiprtc.  No GPU needed.
+ * Returns the source length (>= 0) or an error code. */
+int zkgpu_zxp_jit_source(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd, uint32_t n_tmp1,
+                         uint32_t n_tmp3, const uint64_t *challenges, const uint64_t *publics, uint32_t n_publics,
+                         const uint64_t *evals, uint32_t n_evals, char *buf, uint64_t buflen, int rtc_check);
+
 /* Polinomial::calculateZ(z, num, den) (polinomial.hpp:586-607), F_p^3 columns
  * (3 consecutive columns of ld each).  *closes = 1 iff z[n-1]*num[n-1]/den[n-1] == 1
  * (the reference's zkassert). */

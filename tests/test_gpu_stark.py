@@ -181,17 +181,19 @@ def test_step42ns_stage(oracle, zkgpu, n_bits, blow):
 
 
 @pytest.mark.parametrize("name", ["step1", "step2", "step3prev", "step42ns", "step52ns"])
-@pytest.mark.parametrize("mode", [("1", "0"), ("1", "3"), ("0", "0")])
+@pytest.mark.parametrize("mode", [("1", "0", "2"), ("1", "0", "0"), ("1", "3", "0"), ("0", "0", "0")])
 def test_zxp_programs_vs_oracle(oracle, zkgpu, name, mode, monkeypatch):
-    """Each synthetic program on random sections: the GPU (compiled with
-    linear-combination fusion at the default / a tiny term cap, and the
-    unfused source program) equals the oracle's evaluation of the SOURCE
-    program, bit for bit."""
+    """Each synthetic program on random sections: the GPU -- the run-time
+    compiled straight-line kernel, the interpreter on the compiled program at
+    the default / a tiny term cap, and the interpreter on the unfused source
+    program -- equals the oracle's evaluation of the SOURCE program, bit for
+    bit."""
     import ctypes
     import torch
     from zkgpu.synthetic import SyntheticStark
     monkeypatch.setenv("ZKGPU_ZXP_FUSE", mode[0])
     monkeypatch.setenv("ZKGPU_ZXP_MAX_TERMS", mode[1])
+    monkeypatch.setenv("ZKGPU_ZXP_JIT", mode[2])
     inst = SyntheticStark(n_bits=9, blowup_bits=1, t=8, m=3, n_free=4, n_lookups=2, n_queries=8)
     prog = inst.programs[name]
     eb = inst.blowup_bits
@@ -232,3 +234,19 @@ def test_zxp_programs_vs_oracle(oracle, zkgpu, name, mode, monkeypatch):
     torch.cuda.synchronize()
     for k, (t, _, _) in secs.items():
         assert np.array_equal(zkgpu.from_device(t).T, S[k]), "section %d" % k
+
+
+def test_full_proof_bit_exact_jit(oracle, zkgpu, monkeypatch):
+    """The whole proof with every expression program as a run-time compiled
+    straight-line kernel (csrc/zxp_jit.hip) equals the oracle's proof."""
+    from zkgpu.synthetic import SyntheticStark
+    from zkgpu.stark import GpuStark
+    monkeypatch.setenv("ZKGPU_ZXP_JIT", "2")
+    inst = SyntheticStark(n_bits=10, blowup_bits=1, t=6, m=3, n_queries=16)
+    o, ref = oracle_proof(inst)
+    g = GpuStark(inst)
+    g.witness()
+    got = g.prove()
+    for k in ref:
+        assert got[k] == ref[k], k
+    g.close()

@@ -166,3 +166,20 @@ def test_reference_step_code(oracle, zkgpu_host, which):
     n_pub = int(opn[opn[:, 0] == 6][:, 1].max()) + 1 if (opn[:, 0] == 6).any() else 1
     comp = _check_program(oracle, zkgpu_host, prog, widths, 64, n_pub, n_ev, 0, seed=11)
     assert len(comp["instr"]) < len(prog.instr)
+
+
+@pytest.mark.parametrize("name", ["step1", "step42ns", "step52ns"])
+def test_jit_source_compiles_for_gfx950(zkgpu_host, name):
+    """The straight-line kernel printed for a compiled program (csrc/zxp_jit.hip)
+    compiles with hiprtc for gfx950 (no GPU needed); pointers and
+    challenge-dependent values are not in the source."""
+    from zkgpu.synthetic import SyntheticStark
+    inst = SyntheticStark(n_bits=5, t=6, m=2, n_free=5, n_lookups=2, n_queries=4)
+    prog = inst.programs[name]
+    rng = np.random.default_rng(5)
+    ch = _rand(rng, (8, 3))
+    ev = _rand(rng, (len(inst.evmap), 3))
+    src = zkgpu_host.zxp_jit_source(prog, ch, np.zeros(8, np.uint64), ev, rtc_check=True)
+    assert "zxp_jit" in src
+    src2 = zkgpu_host.zxp_jit_source(prog, _rand(rng, (8, 3)), np.zeros(8, np.uint64), _rand(rng, ev.shape))
+    assert src == src2  # same structure -> same kernel (cached per process)

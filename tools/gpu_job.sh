@@ -117,6 +117,15 @@ for step in "$@"; do
             echo "rows=$r $(python -c "import json;d=json.load(open('gpurun_out/zxp_r$r.json'));print(d['ms_per_step'],'ms', d['kernels']['k_zxp_eval'])")"
         done
         ;;
+    jitsweep)
+        for cfg in "8 0" "1000 0" "8 4" "4 0"; do
+            set -- $cfg
+            ZKGPU_ZXP_JIT_DOTLOOP=$1 ZKGPU_ZXP_JIT_WAVES=$2 timeout -k 10 300 python bench.py --workload stark --steps 2 --warmup 1 --no-cpu \
+                > gpurun_out/jit_$1_$2.json 2>> gpurun_out/jit_sweep.err
+            ok_or_stop $? "stark jit loop=$1 waves=$2"
+            echo "loop=$1 waves=$2 $(python -c "import json;d=json.load(open('gpurun_out/jit_$1_$2.json'));s=d['stages_ms'];print(d['ms_per_step'],'ms q',s['STARK_STEP_4_CALCULATE_EXPS_2NS'],'f',s['STARK_STEP_5_CALCULATE_EXPS'],'s2',s['STARK_STEP_2_CALCULATE_EXPS'],'s3',s['STARK_STEP_3_CALCULATE_EXPS'])")"
+        done
+        ;;
     sqpmc)
         # VALU/SALU/SMEM issue and wave-state counters for every kernel of a 2^20 STARK proof
         cd /tmp

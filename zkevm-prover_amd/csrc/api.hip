@@ -645,19 +645,6 @@ int zkgpu_rand_cols_dev(uint64_t *base, uint64_t ld, const uint32_t *cols, uint3
     return rand_cols(base, ld, (const uint32_t *)p, ncols, nrows, seed, stream, g_ctx.stream);
 }
 
-// Dot3 limbs of coefficient c (canonical): 22/21/21-bit limbs of c and of
-// c * 2^32 mod p (csrc/gl_device.hpp Dot3::term)
-static void zxp_limbs6(uint64_t c, uint32_t out[6])
-{
-    const uint64_t cs = h_mul(c, 1ULL << 32);
-    const uint64_t v[2] = {c, cs};
-    for (int h = 0; h < 2; h++) {
-        out[3 * h] = (uint32_t)(v[h] & ((1u << 22) - 1));
-        out[3 * h + 1] = (uint32_t)((v[h] >> 22) & ((1u << 21) - 1));
-        out[3 * h + 2] = (uint32_t)(v[h] >> 43);
-    }
-}
-
 static inline uint64_t h_add(uint64_t a, uint64_t b)
 {
     const uint64_t s = a + b;  // a, b < p
@@ -939,6 +926,39 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
         else if (op[k].kind == ZXP_COL3) cols += 3;
         else if (op[k].kind == ZXP_XDIV || op[k].kind == ZXP_XDIVW) cols += 3;
     L.bytes = 8.0 * cols * (double)(1ULL << log_dom);
+    // The compiled program runs as a run-time compiled straight-line kernel
+    // (csrc/zxp_jit.hip, compiled once per program per process) on domains of
+    // 2^16 rows and more, where it pays for its ~1-2 s compile; smaller
+    // domains use the interpreter.  ZKGPU_ZXP_JIT=0 never, =2 always.
+    const char *env_jit = getenv("ZKGPU_ZXP_JIT");
+    const int jit_mode = env_jit ? atoi(env_jit) : 1;
+    if (fuse && (jit_mode == 2 || (jit_mode == 1 && log_dom >= 16))) {
+        ZxpJitIn J;
+        J.ins = pin;
+        J.n_instr = n_instr;
+        J.opnd = opv.data();
+        J.terms = terms;
+        J.csts = csts;
+        J.n_tmp1 = n_tmp1;
+        J.n_tmp3 = n_tmp3;
+        J.sections = sections;
+        J.log_dom = log_dom;
+        J.challenges = challenges;
+        J.publics = publics;
+        J.evals = evals;
+        J.xdiv = xdiv;
+        J.xdivw = xdivw;
+        J.zh_dev = zh_dev;
+        J.zmask = (uint32_t)(zh - 1);
+        J.x_start = x_start % HP;
+        J.bytes = L.bytes;
+        const char *env_loop = getenv("ZKGPU_ZXP_JIT_DOTLOOP");
+        const char *env_waves = getenv("ZKGPU_ZXP_JIT_WAVES");
+        J.dot_loop_min = env_loop ? (uint32_t)atoi(env_loop) : 8u;
+        J.waves_per_eu = env_waves ? (uint32_t)atoi(env_waves) : 0u;
+        rc = zxp_jit_run(J, s);
+        if (rc <= 0) return rc;  // launched, or an error; 1 = shape unsupported
+    }
     return zxp_eval(L, s);
 }
 

@@ -15,9 +15,17 @@
 //
 // Semantics match the reference's Goldilocks/Goldilocks3 API (submodule,
 // used e.g. at polinomial.hpp:178-207) after canonicalisation.
+#ifndef __HIPCC_RTC__
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#else
+// run-time compiled expression kernels (csrc/zxp_jit.hip) embed this file
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+using __hip_internal::int64_t;
+using __hip_internal::int32_t;
+#endif
 
 #define ZK_P 0xFFFFFFFF00000001ULL
 #define ZK_EPS 0xFFFFFFFFULL  // 2^64 mod p
@@ -152,6 +160,14 @@ __device__ __forceinline__ gl3 gl3_mul(const gl3 &a, const gl3 &b)
     r.v[1] = gl_sub(gl_sub(gl_sub(gl_add(A, C), E), E), D);
     r.v[2] = gl_sub(B, G);
     return r;
+}
+
+// F_p^3 op F_p (the base operand sits in component 0)
+__device__ __forceinline__ gl3 gl3_add1(const gl3 &a, uint64_t b) { return gl3{{gl_add(a.v[0], b), a.v[1], a.v[2]}}; }
+__device__ __forceinline__ gl3 gl3_sub1(const gl3 &a, uint64_t b) { return gl3{{gl_sub(a.v[0], b), a.v[1], a.v[2]}}; }
+__device__ __forceinline__ gl3 gl3_rsub1(uint64_t a, const gl3 &b)
+{
+    return gl3{{gl_sub(a, b.v[0]), gl_neg(b.v[1]), gl_neg(b.v[2])}};
 }
 
 // ---------------------------------------------------------------- dot products

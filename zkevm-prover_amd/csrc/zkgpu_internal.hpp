@@ -122,6 +122,38 @@ struct ZxpLaunch {
     uint64_t x_start;
     double bytes;  // algorithmic bytes for profiling
 };
+// ---- zxp_jit.hip: run-time compiled straight-line expression kernels
+struct ZxpJitIn {
+    const zxp_instr *ins;  // compiled program (zkgpu_zxp_compile)
+    uint32_t n_instr;
+    const zxp_operand *opnd;
+    const zxp_term *terms;
+    const uint64_t *csts;
+    uint32_t n_tmp1, n_tmp3;
+    const zkgpu_sections *sections;
+    uint32_t log_dom;
+    const uint64_t *challenges, *publics, *evals;  // host
+    const uint64_t *xdiv, *xdivw, *zh_dev;         // device
+    uint32_t zmask;
+    uint64_t x_start;
+    double bytes;
+    uint32_t dot_loop_min;  // DOTs with at least this many column terms loop over a table
+    uint32_t waves_per_eu;  // occupancy hint for the compiler (0: none)
+};
+// 0 launched, 1 shape unsupported (run the interpreter), < 0 error
+int zxp_jit_run(const ZxpJitIn &in, hipStream_t s);
+// Dot3 limbs of a canonical coefficient c: 22/21/21-bit limbs of c and of
+// c * 2^32 mod p (csrc/gl_device.hpp Dot3::term)
+inline void zxp_limbs6(uint64_t c, uint32_t out[6])
+{
+    const uint64_t v[2] = {c, h_mul(c, 1ULL << 32)};
+    for (int h = 0; h < 2; h++) {
+        out[3 * h] = (uint32_t)(v[h] & ((1u << 22) - 1));
+        out[3 * h + 1] = (uint32_t)((v[h] >> 22) & ((1u << 21) - 1));
+        out[3 * h + 2] = (uint32_t)(v[h] >> 43);
+    }
+}
+
 int rand_cols(uint64_t *base, uint64_t ld, const uint32_t *cols_dev, uint32_t ncols, uint64_t nrows, uint64_t seed,
               uint64_t stream, hipStream_t s);
 int zxp_eval(const ZxpLaunch &L, hipStream_t s);

@@ -1,0 +1,662 @@
+// Run-time compiled expression kernels for ZXP programs.
+//
+// The reference ships its constraint/FRI expressions as generated C++ compiled
+// into the prover (src/starkpil/*/chelpers/*.step42ns.cpp, step52ns.cpp: one
+// straight-line function per circuit).  This is the GPU equivalent: the
+// compiled program (csrc/zxp_compile.cpp: fused DOT instructions, SSA temps
+// packed into slots) is printed as one straight-line HIP kernel -- temporaries
+// in registers, every column read a coalesced load the compiler can schedule
+// freely, column stores deferred to the end of the row -- and compiled for
+// gfx950 with hiprtc on first use.  Only the program STRUCTURE is in the
+// source (column slots, row shifts, table offsets); challenge-dependent
+// values (DOT coefficient limbs, F_p^3 constants) and pointers are kernel
+// inputs, so one compiled kernel serves every proof of a circuit (cached per
+// process by source text).  csrc/gl_device.hpp is embedded verbatim, so the
+// field arithmetic is the same code the interpreter (k_zxp_eval) runs.
+//
+// Unsupported shapes (a program that reads a column it writes at a nonzero
+// row shift) return 1 and the caller runs the interpreter.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "zkgpu_internal.hpp"
+
+namespace zk {
+
+static const char *k_gl_device_src =
+#include "../build/gl_device_src.inc"
+    ;
+
+namespace {
+
+constexpr int JIT_THREADS = 256;
+
+// column term of a looped DOT (device table; layout shared with k_kernel_head)
+struct JitTerm {
+    const uint64_t *ptr;
+    int64_t sh;
+    uint32_t c[3][6];
+    uint32_t pad[2];
+};
+static_assert(sizeof(JitTerm) == 96, "JitTerm");
+
+struct JitParams {
+    const uint64_t *const *cp;  // column base pointers (slot j)
+    const uint64_t *kc;         // F_p / F_p^3 constants
+    const uint32_t *kl;         // DOT limbs (unrolled terms)
+    const JitTerm *zt;          // DOT column terms (looped)
+    const uint64_t *xdiv, *xdivw, *zh, *tw_lo, *tw_hi;
+    uint64_t x_start;
+    uint32_t logdom, zmask;
+};
+
+const char *k_kernel_head = R"(
+using namespace zk;
+struct JitTerm {
+    const uint64_t *ptr;
+    int64_t sh;
+    uint32_t c[3][6];
+    uint32_t pad[2];
+};
+struct JitParams {
+    const uint64_t *const *cp;
+    const uint64_t *kc;
+    const uint32_t *kl;
+    const JitTerm *zt;
+    const uint64_t *xdiv, *xdivw, *zh, *tw_lo, *tw_hi;
+    uint64_t x_start;
+    uint32_t logdom, zmask;
+};
+// long column runs of a DOT: a loop over table terms, 4 loads in flight
+template <int D>
+__device__ __forceinline__ void dot_cols(Dot3 &d0, Dot3 &d1, Dot3 &d2, const JitTerm *t, int n, uint64_t i,
+                                         uint64_t m)
+{
+    int k = 0;
+    for (; k + 4 <= n; k += 4) {
+        uint64_t a[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) a[u] = t[k + u].ptr[(i + (uint64_t)t[k + u].sh) & m];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            d0.term(a[u], t[k + u].c[0]);
+            if (D == 3) {
+                d1.term(a[u], t[k + u].c[1]);
+                d2.term(a[u], t[k + u].c[2]);
+            }
+        }
+    }
+    for (; k < n; k++) {
+        const uint64_t a = t[k].ptr[(i + (uint64_t)t[k].sh) & m];
+        d0.term(a, t[k].c[0]);
+        if (D == 3) {
+            d1.term(a, t[k].c[1]);
+            d2.term(a, t[k].c[2]);
+        }
+    }
+}
+extern "C" __global__ void __launch_bounds__(256) ZKJIT_WAVES zxp_jit(const JitParams p)
+{
+    const uint64_t m = (1ULL << p.logdom) - 1;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i > m) return;
+#define C(j, sh) p.cp[j][(i + (uint64_t)(sh)) & m]
+)";
+
+void appendf(std::string &s, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    int n = vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (n >= (int)sizeof(buf)) {
+        std::vector<char> big(n + 1);
+        va_start(ap, fmt);
+        vsnprintf(big.data(), big.size(), fmt, ap);
+        va_end(ap);
+        s += big.data();
+    } else {
+        s += buf;
+    }
+}
+
+struct Expr {
+    std::string e;
+    int dim;
+};
+
+struct Cache {
+    std::mutex mu;
+    std::unordered_map<std::string, hipFunction_t> fn;
+};
+Cache &cache()
+{
+    static Cache c;
+    return c;
+}
+
+// grow-only device buffer for the per-launch tables
+char *jit_buf(size_t bytes)
+{
+    static char *buf = nullptr;
+    static size_t cap = 0;
+    if (bytes > cap) {
+        if (buf) (void)hipFree(buf);
+        buf = nullptr;
+        cap = 0;
+        if (hipMalloc((void **)&buf, bytes) != hipSuccess) return nullptr;
+        cap = bytes;
+    }
+    return buf;
+}
+
+// hiprtc: source -> gfx950 code object (no GPU needed)
+int rtc_compile(const std::string &src, std::vector<char> &code)
+{
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "zxp_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+        return set_error(ZKGPU_ERR_ARG, "zxp jit: hiprtcCreateProgram failed");
+    // -O1: the straight-line body needs no loop optimisation, and -O3 takes
+    // 5-10x longer to compile with the same instruction count (measured on
+    // the synthetic step42ns: 17.7 K VALU per row either way)
+    const char *opts[] = {"--offload-arch=gfx950", "-O1", "-std=c++17"};
+    const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+    if (r != HIPRTC_SUCCESS) {
+        size_t ls = 0;
+        hiprtcGetProgramLogSize(prog, &ls);
+        std::string log(ls + 1, '\0');
+        hiprtcGetProgramLog(prog, &log[0]);
+        hiprtcDestroyProgram(&prog);
+        return set_error(ZKGPU_ERR_ARG, "zxp jit: hiprtc compile failed: %.300s", log.c_str());
+    }
+    size_t cs = 0;
+    hiprtcGetCodeSize(prog, &cs);
+    code.resize(cs);
+    hiprtcGetCode(prog, code.data());
+    hiprtcDestroyProgram(&prog);
+    return cs ? 0 : set_error(ZKGPU_ERR_ARG, "zxp jit: empty code object");
+}
+
+int compile(const std::string &src, hipFunction_t *out)
+{
+    Cache &c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.fn.find(src);
+    if (it != c.fn.end()) {
+        *out = it->second;
+        return 0;
+    }
+    std::vector<char> code;
+    int rc;
+    if ((rc = rtc_compile(src, code))) return rc;
+    hipModule_t mod;
+    if ((rc = check_hip(hipModuleLoadData(&mod, code.data()), "zxp jit: hipModuleLoadData"))) return rc;
+    hipFunction_t f;
+    if ((rc = check_hip(hipModuleGetFunction(&f, mod, "zxp_jit"), "zxp jit: hipModuleGetFunction"))) return rc;
+    c.fn.emplace(src, f);
+    *out = f;
+    return 0;
+}
+
+}  // namespace
+
+int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const uint64_t *> &cp,
+                         std::vector<uint64_t> &kc, std::vector<uint32_t> &kl, std::vector<JitTerm> &zt)
+{
+    const zkgpu_sections *S = in.sections;
+    std::map<std::pair<uint32_t, uint32_t>, uint32_t> slot;  // (section, col) -> cp slot
+    auto col_slot = [&](uint32_t sec, uint32_t col) {
+        auto key = std::make_pair(sec, col);
+        auto it = slot.find(key);
+        if (it != slot.end()) return it->second;
+        cp.push_back(S->sec[sec] + (uint64_t)col * S->ld[sec]);
+        return slot[key] = (uint32_t)cp.size() - 1;
+    };
+    // columns written by the program (stores deferred; shift-0 reads forward)
+    std::vector<uint8_t> written_any;
+    auto mark = [&](uint32_t j) {
+        if (j >= written_any.size()) written_any.resize(j + 1, 0);
+        written_any[j] = 1;
+    };
+    for (uint32_t k = 0; k < in.n_instr; k++) {
+        const zxp_operand &d = in.opnd[in.ins[k].dst];
+        if (d.kind == ZXP_COL || d.kind == ZXP_COL3)
+            for (uint32_t c = 0; c < (d.kind == ZXP_COL3 ? 3u : 1u); c++) mark(col_slot(d.a, d.b + c));
+    }
+    auto is_written = [&](uint32_t j) { return j < written_any.size() && written_any[j]; };
+    std::vector<uint8_t> wlive;  // written so far (in program order)
+    auto col_read = [&](uint32_t sec, uint32_t col, int32_t sh, std::string &e) -> int {
+        const uint32_t j = col_slot(sec, col);
+        if (is_written(j)) {
+            if (sh != 0) return 1;  // cross-row read of a written column: interpreter
+            if (j < wlive.size() && wlive[j]) {
+                e = "w" + std::to_string(j);
+                return 0;
+            }
+        }
+        e = "C(" + std::to_string(j) + "," + std::to_string(sh) + ")";
+        return 0;
+    };
+    auto kconst = [&](const uint64_t *v, int dim) {
+        const size_t o = kc.size();
+        for (int t = 0; t < dim; t++) kc.push_back(v[t] % 0xFFFFFFFF00000001ULL);
+        return o;
+    };
+    bool uses_x = false;
+    auto operand = [&](uint32_t idx, Expr &x) -> int {
+        const zxp_operand &o = in.opnd[idx];
+        char b[160];
+        switch (o.kind) {
+        case ZXP_TMP1: x = {"a" + std::to_string(o.a), 1}; return 0;
+        case ZXP_TMP3: x = {"b" + std::to_string(o.a), 3}; return 0;
+        case ZXP_COL: x.dim = 1; return col_read(o.a, o.b, (int32_t)o.c, x.e);
+        case ZXP_COL3: {
+            std::string c0, c1, c2;
+            if (col_read(o.a, o.b, (int32_t)o.c, c0) || col_read(o.a, o.b + 1, (int32_t)o.c, c1) ||
+                col_read(o.a, o.b + 2, (int32_t)o.c, c2))
+                return 1;
+            x = {"gl3{{" + c0 + "," + c1 + "," + c2 + "}}", 3};
+            return 0;
+        }
+        case ZXP_LIT: {
+            const uint64_t v = ((uint64_t)o.a | ((uint64_t)o.b << 32)) % 0xFFFFFFFF00000001ULL;
+            snprintf(b, sizeof(b), "0x%llxULL", (unsigned long long)v);
+            x = {b, 1};
+            return 0;
+        }
+        case ZXP_PUB:
+        case ZXP_CHAL:
+        case ZXP_EVAL:
+        case ZXP_IMM: {
+            const uint64_t *v = o.kind == ZXP_PUB    ? in.publics + o.a
+                                : o.kind == ZXP_CHAL ? in.challenges + 3 * o.a
+                                : o.kind == ZXP_EVAL ? in.evals + 3 * o.a
+                                                     : in.csts + 3 * o.a;
+            const int dim = o.kind == ZXP_PUB ? 1 : o.kind == ZXP_IMM ? (int)o.b : 3;
+            const size_t off = kconst(v, dim);
+            if (dim == 1)
+                snprintf(b, sizeof(b), "p.kc[%zu]", off);
+            else
+                snprintf(b, sizeof(b), "gl3{{p.kc[%zu],p.kc[%zu],p.kc[%zu]}}", off, off + 1, off + 2);
+            x = {b, dim};
+            return 0;
+        }
+        case ZXP_X: uses_x = true; x = {"xv", 1}; return 0;
+        case ZXP_XDIV: x = {"gl3{{p.xdiv[3*i],p.xdiv[3*i+1],p.xdiv[3*i+2]}}", 3}; return 0;
+        case ZXP_XDIVW: x = {"gl3{{p.xdivw[3*i],p.xdivw[3*i+1],p.xdivw[3*i+2]}}", 3}; return 0;
+        case ZXP_ZI: x = {"p.zh[i & p.zmask]", 1}; return 0;
+        default: return 1;
+        }
+    };
+    auto limbs3 = [&](uint64_t c) {  // Dot3 constant init: 22/21/21-bit limbs of c
+        kl.push_back((uint32_t)(c & ((1u << 22) - 1)));
+        kl.push_back((uint32_t)((c >> 22) & ((1u << 21) - 1)));
+        kl.push_back((uint32_t)(c >> 43));
+    };
+    std::string body;
+    // assignment of a value expression to a destination operand
+    auto assign = [&](uint32_t didx, const Expr &r) -> int {
+        const zxp_operand &d = in.opnd[didx];
+        switch (d.kind) {
+        case ZXP_TMP1:
+            appendf(body, "a%u = %s%s;\n", d.a, r.e.c_str(), r.dim == 3 ? ".v[0]" : "");
+            return 0;
+        case ZXP_TMP3:
+            if (r.dim == 3)
+                appendf(body, "b%u = %s;\n", d.a, r.e.c_str());
+            else
+                appendf(body, "b%u = gl3{{%s, 0, 0}};\n", d.a, r.e.c_str());
+            return 0;
+        case ZXP_COL: {
+            const uint32_t j = col_slot(d.a, d.b);
+            appendf(body, "w%u = %s%s;\n", j, r.e.c_str(), r.dim == 3 ? ".v[0]" : "");
+            if (j >= wlive.size()) wlive.resize(j + 1, 0);
+            wlive[j] = 1;
+            return 0;
+        }
+        case ZXP_COL3: {
+            uint32_t j[3];
+            for (int c = 0; c < 3; c++) j[c] = col_slot(d.a, d.b + c);
+            if (r.dim == 3)
+                appendf(body, "{ const gl3 t_ = %s; w%u = t_.v[0]; w%u = t_.v[1]; w%u = t_.v[2]; }\n", r.e.c_str(),
+                        j[0], j[1], j[2]);
+            else
+                appendf(body, "w%u = %s; w%u = 0; w%u = 0;\n", j[0], r.e.c_str(), j[1], j[2]);
+            for (int c = 0; c < 3; c++) {
+                if (j[c] >= wlive.size()) wlive.resize(j[c] + 1, 0);
+                wlive[j[c]] = 1;
+            }
+            return 0;
+        }
+        default: return 1;
+        }
+    };
+    // DOT plan.  A term whose source is a temporary is accumulated right where
+    // that temporary is defined (exact integer sums commute), so temporaries
+    // feeding a linear combination die at once instead of staying live until
+    // the DOT: register pressure stays that of one constraint at a time.
+    struct Stream {
+        uint32_t dot;
+        bool three;
+        std::string val;
+        size_t kt;
+    };
+    std::vector<std::vector<Stream>> stream(in.n_instr);
+    std::vector<size_t> dot_k0(in.n_instr, 0);
+    std::vector<uint32_t> first_use(in.n_instr, UINT32_MAX);  // declaration point of DOT k's accumulators
+    {
+        std::vector<int64_t> last1(in.n_tmp1 + 1, -1), last3(in.n_tmp3 + 1, -1);
+        for (uint32_t k = 0; k < in.n_instr; k++) {
+            const zxp_instr &I = in.ins[k];
+            if (I.op == ZXP_DOT1 || I.op == ZXP_DOT3) {
+                const bool three = I.op == ZXP_DOT3;
+                uint64_t c0[3] = {0, 0, 0};
+                for (uint32_t t = I.a; t < I.a + I.b; t++)
+                    if (in.terms[t].src == ZXP_TERM_ONE)
+                        for (int j = 0; j < 3; j++) {
+                            const uint64_t P = 0xFFFFFFFF00000001ULL, v = in.terms[t].coef[j] % P;
+                            const uint64_t sum = c0[j] + v;
+                            c0[j] = (sum < v || sum >= P) ? sum - P : sum;
+                        }
+                dot_k0[k] = kl.size();
+                for (int j = 0; j < 3; j++) limbs3(c0[j]);
+                first_use[k] = k;
+                for (uint32_t t = I.a; t < I.a + I.b; t++) {
+                    const zxp_term &tm = in.terms[t];
+                    if (tm.src == ZXP_TERM_ONE) continue;
+                    const zxp_operand &o = in.opnd[tm.src];
+                    if (o.kind != ZXP_TMP1 && o.kind != ZXP_TMP3) continue;
+                    const int64_t d = o.kind == ZXP_TMP1 ? last1[o.a] : last3[o.a];
+                    if (d < 0) continue;  // never written: the value is 0
+                    Stream st;
+                    st.dot = k;
+                    st.three = three;
+                    st.val = o.kind == ZXP_TMP1 ? "a" + std::to_string(o.a)
+                                                : "b" + std::to_string(o.a) + ".v[" + std::to_string(tm.comp) + "]";
+                    st.kt = kl.size();
+                    for (int j = 0; j < 3; j++) {
+                        uint32_t l6[6];
+                        zxp_limbs6(tm.coef[j] % 0xFFFFFFFF00000001ULL, l6);
+                        kl.insert(kl.end(), l6, l6 + 6);
+                    }
+                    stream[d].push_back(st);
+                    first_use[k] = std::min<uint32_t>(first_use[k], (uint32_t)d);
+                }
+            }
+            const zxp_operand &D = in.opnd[I.dst];
+            if (D.kind == ZXP_TMP1) last1[D.a] = k;
+            if (D.kind == ZXP_TMP3) last3[D.a] = k;
+        }
+    }
+    std::vector<std::vector<uint32_t>> declare_at(in.n_instr);
+    for (uint32_t k = 0; k < in.n_instr; k++)
+        if (first_use[k] != UINT32_MAX) declare_at[first_use[k]].push_back(k);
+    auto emit_declarations = [&](uint32_t at) {
+        for (uint32_t k : declare_at[at]) {
+            const size_t k0 = dot_k0[k];
+            if (in.ins[k].op == ZXP_DOT3)
+                appendf(body, "Dot3 D%u_0(p.kl + %zu), D%u_1(p.kl + %zu), D%u_2(p.kl + %zu);\n", k, k0, k, k0 + 3, k,
+                        k0 + 6);
+            else
+                appendf(body, "Dot3 D%u_0(p.kl + %zu);\n", k, k0);
+        }
+    };
+    auto emit_streams = [&](uint32_t at) {
+        for (const Stream &st : stream[at]) {
+            if (st.three)
+                appendf(body,
+                        "{ const uint64_t v_ = %s; D%u_0.term(v_, p.kl + %zu); D%u_1.term(v_, p.kl + %zu); "
+                        "D%u_2.term(v_, p.kl + %zu); }\n",
+                        st.val.c_str(), st.dot, st.kt, st.dot, st.kt + 6, st.dot, st.kt + 12);
+            else
+                appendf(body, "D%u_0.term(%s, p.kl + %zu);\n", st.dot, st.val.c_str(), st.kt);
+        }
+    };
+    for (uint32_t k = 0; k < in.n_instr; k++) {
+        const zxp_instr &I = in.ins[k];
+        emit_declarations(k);
+        if (I.op == ZXP_DOT1 || I.op == ZXP_DOT3) {
+            const bool three = I.op == ZXP_DOT3;
+            // column terms read from memory: looped from the term table when
+            // there are many (code size, compile time), unrolled otherwise
+            auto memcol = [&](const zxp_term &tm) {
+                if (tm.src == ZXP_TERM_ONE) return false;
+                const zxp_operand &o = in.opnd[tm.src];
+                if (o.kind != ZXP_COL) return false;
+                const uint32_t j = col_slot(o.a, o.b);
+                return !(is_written(j) && j < wlive.size() && wlive[j]);
+            };
+            uint32_t n_mem = 0;
+            for (uint32_t t = I.a; t < I.a + I.b; t++) n_mem += memcol(in.terms[t]);
+            const bool loop = n_mem >= in.dot_loop_min;
+            if (loop) {
+                const size_t t0 = zt.size();
+                for (uint32_t t = I.a; t < I.a + I.b; t++) {
+                    const zxp_term &tm = in.terms[t];
+                    if (!memcol(tm)) continue;
+                    const zxp_operand &o = in.opnd[tm.src];
+                    if (is_written(col_slot(o.a, o.b)) && o.c != 0) return 1;
+                    JitTerm jt;
+                    memset(&jt, 0, sizeof(jt));
+                    jt.ptr = S->sec[o.a] + (uint64_t)o.b * S->ld[o.a];
+                    jt.sh = (int64_t)(int32_t)o.c;
+                    for (int j = 0; j < 3; j++) zxp_limbs6(tm.coef[j] % 0xFFFFFFFF00000001ULL, jt.c[j]);
+                    zt.push_back(jt);
+                }
+                if (three)
+                    appendf(body, "dot_cols<3>(D%u_0, D%u_1, D%u_2, p.zt + %zu, %u, i, m);\n", k, k, k, t0, n_mem);
+                else
+                    appendf(body, "dot_cols<1>(D%u_0, D%u_0, D%u_0, p.zt + %zu, %u, i, m);\n", k, k, k, t0, n_mem);
+            }
+            for (uint32_t t = I.a; t < I.a + I.b; t++) {
+                const zxp_term &tm = in.terms[t];
+                if (tm.src == ZXP_TERM_ONE) continue;
+                const zxp_operand &o = in.opnd[tm.src];
+                if (o.kind != ZXP_COL) {
+                    if (o.kind != ZXP_TMP1 && o.kind != ZXP_TMP3) return 1;
+                    continue;  // streamed at the temporary's definition
+                }
+                if (loop && memcol(tm)) continue;
+                std::string e;
+                if (col_read(o.a, o.b, (int32_t)o.c, e)) return 1;
+                const size_t kt = kl.size();
+                for (int j = 0; j < 3; j++) {
+                    uint32_t l6[6];
+                    zxp_limbs6(tm.coef[j] % 0xFFFFFFFF00000001ULL, l6);
+                    kl.insert(kl.end(), l6, l6 + 6);
+                }
+                if (three)
+                    appendf(body,
+                            "{ const uint64_t v_ = %s; D%u_0.term(v_, p.kl + %zu); D%u_1.term(v_, p.kl + %zu); "
+                            "D%u_2.term(v_, p.kl + %zu); }\n",
+                            e.c_str(), k, kt, k, kt + 6, k, kt + 12);
+                else
+                    appendf(body, "D%u_0.term(%s, p.kl + %zu);\n", k, e.c_str(), kt);
+            }
+            char fin[128];
+            if (three)
+                snprintf(fin, sizeof(fin), "gl3{{D%u_0.fin(), D%u_1.fin(), D%u_2.fin()}}", k, k, k);
+            else
+                snprintf(fin, sizeof(fin), "D%u_0.fin()", k);
+            if (assign(I.dst, Expr{fin, three ? 3 : 1})) return 1;
+            emit_streams(k);
+            continue;
+        }
+        Expr A, B;
+        if (operand(I.a, A)) return 1;
+        if (I.op != ZXP_COPY && operand(I.b, B)) return 1;
+        Expr R;
+        const char *ea = A.e.c_str(), *eb = B.e.c_str();
+        std::string s;
+        if (I.op == ZXP_COPY) {
+            R = A;
+        } else if (I.op == ZXP_MUL) {
+            if (A.dim == 3 && B.dim == 3)
+                appendf(s, "gl3_mul(%s, %s)", ea, eb);
+            else if (A.dim == 3)
+                appendf(s, "gl3_mul1(%s, %s)", ea, eb);
+            else if (B.dim == 3)
+                appendf(s, "gl3_mul1(%s, %s)", eb, ea);
+            else
+                appendf(s, "gl_mul(%s, %s)", ea, eb);
+            R = {s, std::max(A.dim, B.dim)};
+        } else if (I.op == ZXP_ADD) {
+            if (A.dim == 3 && B.dim == 3)
+                appendf(s, "gl3_add(%s, %s)", ea, eb);
+            else if (A.dim == 3)
+                appendf(s, "gl3_add1(%s, %s)", ea, eb);
+            else if (B.dim == 3)
+                appendf(s, "gl3_add1(%s, %s)", eb, ea);
+            else
+                appendf(s, "gl_add(%s, %s)", ea, eb);
+            R = {s, std::max(A.dim, B.dim)};
+        } else if (I.op == ZXP_SUB) {
+            if (A.dim == 3 && B.dim == 3)
+                appendf(s, "gl3_sub(%s, %s)", ea, eb);
+            else if (A.dim == 3)
+                appendf(s, "gl3_sub1(%s, %s)", ea, eb);
+            else if (B.dim == 3)
+                appendf(s, "gl3_rsub1(%s, %s)", ea, eb);
+            else
+                appendf(s, "gl_sub(%s, %s)", ea, eb);
+            R = {s, std::max(A.dim, B.dim)};
+        } else {
+            return 1;
+        }
+        if (assign(I.dst, R)) return 1;
+        emit_streams(k);
+    }
+    // assemble: prelude, params, declarations, body, deferred stores
+    src = k_gl_device_src;
+    if (in.waves_per_eu)
+        appendf(src, "#define ZKJIT_WAVES __attribute__((amdgpu_waves_per_eu(%u)))\n", in.waves_per_eu);
+    else
+        src += "#define ZKJIT_WAVES\n";
+    src += k_kernel_head;
+    for (uint32_t s = 0; s < in.n_tmp1; s++) appendf(src, "uint64_t a%u = 0;\n", s);
+    for (uint32_t s = 0; s < in.n_tmp3; s++) appendf(src, "gl3 b%u = gl3{{0, 0, 0}};\n", s);
+    for (uint32_t j = 0; j < written_any.size(); j++)
+        if (written_any[j]) appendf(src, "uint64_t w%u = 0;\n", j);
+    if (uses_x)
+        appendf(src, "const uint64_t ex_ = i << (%u - p.logdom);\n"
+                     "const uint64_t xv = gl_mul(p.x_start, gl_mul(p.tw_lo[ex_ & %lluULL], p.tw_hi[ex_ >> %u]));\n",
+                TW_MAX_LOG, (unsigned long long)(TW_LEVEL_SIZE - 1), TW_LEVEL_BITS);
+    src += body;
+    for (uint32_t j = 0; j < written_any.size(); j++)
+        if (written_any[j]) appendf(src, "const_cast<uint64_t *>(p.cp[%u])[i] = gl_canon(w%u);\n", j, j);
+    src += "#undef C\n}\n";
+    return 0;
+}
+
+int zxp_jit_run(const ZxpJitIn &in, hipStream_t s)
+{
+    std::string src;
+    std::vector<const uint64_t *> cp;
+    std::vector<uint64_t> kc;
+    std::vector<uint32_t> kl;
+    std::vector<JitTerm> zt;
+    int rc = zxp_jit_build_source(in, src, cp, kc, kl, zt);
+    if (rc) return rc;
+    hipFunction_t fn;
+    if ((rc = compile(src, &fn))) return rc;
+    // tables: zt | cp | kc | kl
+    const size_t off_cp = zt.size() * sizeof(JitTerm), off_kc = off_cp + cp.size() * 8;
+    const size_t off_kl = off_kc + (kc.size() + 1) * 8;
+    const size_t total = off_kl + (kl.size() + 1) * 4;
+    char *buf = jit_buf(total);
+    if (!buf) return set_error(ZKGPU_ERR_OOM, "zxp jit: table buffer");
+    std::vector<char> h(total, 0);
+    memcpy(h.data(), zt.data(), zt.size() * sizeof(JitTerm));
+    memcpy(h.data() + off_cp, cp.data(), cp.size() * 8);
+    memcpy(h.data() + off_kc, kc.data(), kc.size() * 8);
+    memcpy(h.data() + off_kl, kl.data(), kl.size() * 4);
+    if ((rc = check_hip(hipMemcpyAsync(buf, h.data(), total, hipMemcpyHostToDevice, s), "zxp jit: H2D"))) return rc;
+    if ((rc = check_hip(hipStreamSynchronize(s), "zxp jit: table upload"))) return rc;  // pageable source
+    Ctx &c = ctx();
+    JitParams p;
+    p.zt = (const JitTerm *)buf;
+    p.cp = (const uint64_t *const *)(buf + off_cp);
+    p.kc = (const uint64_t *)(buf + off_kc);
+    p.kl = (const uint32_t *)(buf + off_kl);
+    p.xdiv = in.xdiv;
+    p.xdivw = in.xdivw;
+    p.zh = in.zh_dev;
+    p.tw_lo = c.tw_lo[0];
+    p.tw_hi = c.tw_hi[0];
+    p.x_start = in.x_start;
+    p.logdom = in.log_dom;
+    p.zmask = in.zmask;
+    void *args[] = {&p};
+    const uint64_t dom = 1ULL << in.log_dom;
+    prof_begin(s);
+    rc = check_hip(hipModuleLaunchKernel(fn, (uint32_t)((dom + JIT_THREADS - 1) / JIT_THREADS), 1, 1, JIT_THREADS, 1,
+                                         1, 0, s, args, nullptr),
+                   "zxp jit: launch");
+    prof_end("k_zxp_jit", in.bytes, s);
+    return rc;
+}
+
+}  // namespace zk
+
+// Diagnostics (C-ABI, include/zkgpu.h): compile a program as
+// zkgpu_zxp_eval_dev would and print its straight-line kernel source;
+// optionally run hiprtc on it.  No GPU needed.
+extern "C" int zkgpu_zxp_jit_source(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd,
+                                    uint32_t n_tmp1, uint32_t n_tmp3, const uint64_t *challenges,
+                                    const uint64_t *publics, uint32_t n_publics, const uint64_t *evals,
+                                    uint32_t n_evals, char *buf, uint64_t buflen, int rtc_check)
+{
+    using namespace zk;
+    zxp_compiled cp;
+    int rc = zkgpu_zxp_compile(instr, n_instr, opnd, n_opnd, n_tmp1, n_tmp3, challenges, publics, n_publics, evals,
+                               n_evals, 0, &cp);
+    if (rc) return rc;
+    // placeholder sections: pointers are kernel inputs, not part of the source
+    static uint64_t dummy;
+    zkgpu_sections S;
+    for (int k = 0; k < 12; k++) {
+        S.sec[k] = &dummy;
+        S.ld[k] = 1;
+        S.ncols[k] = 0;
+    }
+    ZxpJitIn J;
+    memset(&J, 0, sizeof(J));
+    J.ins = cp.instr;
+    J.n_instr = cp.n_instr;
+    J.opnd = cp.opnd;
+    J.terms = cp.term;
+    J.csts = cp.cst;
+    J.n_tmp1 = cp.n_tmp1;
+    J.n_tmp3 = cp.n_tmp3;
+    J.sections = &S;
+    J.challenges = challenges;
+    J.publics = publics;
+    J.evals = evals;
+    std::string src;
+    std::vector<const uint64_t *> colp;
+    std::vector<uint64_t> kc;
+    std::vector<uint32_t> kl;
+    std::vector<JitTerm> zt;
+    J.dot_loop_min = 8;
+    if ((rc = zxp_jit_build_source(J, src, colp, kc, kl, zt))) return rc < 0 ? rc : set_error(ZKGPU_ERR_ARG, "zxp jit: unsupported program shape");
+    if (buf && buflen) {
+        const size_t n = std::min<size_t>(src.size(), buflen - 1);
+        memcpy(buf, src.data(), n);
+        buf[n] = 0;
+    }
+    if (rtc_check) {
+        std::vector<char> code;
+        if ((rc = rtc_compile(src, code))) return rc;
+    }
+    return (int)std::min<size_t>(src.size(), 0x7FFFFFFF);
+}

@@ -71,6 +71,8 @@ _SIGS = {
     "zkgpu_zxp_eval_dev": (ctypes.c_int, [vp, u32, vp, u32, u32, u32, vp, u32, vp, vp, u32, vp, u32, vp, vp, u32,
                                           u64]),
     "zkgpu_zxp_compile": (ctypes.c_int, [vp, u32, vp, u32, u32, u32, vp, vp, u32, vp, u32, u32, vp]),
+    "zkgpu_zxp_jit_source": (ctypes.c_int, [vp, u32, vp, u32, u32, u32, vp, vp, u32, vp, u32, vp, u64,
+                                            ctypes.c_int]),
     "zkgpu_calculate_z_dev": (ctypes.c_int, [vp, u64, vp, u64, vp, u64, u64, ctypes.POINTER(ctypes.c_int)]),
     "zkgpu_evmap_dev": (ctypes.c_int, [vp, vp, vp, vp, vp, u32, vp, vp, u64, u64, u32]),
     "zkgpu_xdivxsub_dev": (ctypes.c_int, [vp, vp, vp, u32, u32]),
@@ -383,6 +385,27 @@ def zxp_compile(prog, challenges, publics, evals=None, max_terms=0):
     return {"instr": grab(out.instr, out.n_instr, np.uint32, 4), "opnd": grab(out.opnd, out.n_opnd, np.uint32, 4),
             "term": grab(out.term, out.n_term, ZXP_TERM_DTYPE, 0), "cst": grab(out.cst, out.n_cst, np.uint64, 3),
             "n_tmp1": out.n_tmp1, "n_tmp3": out.n_tmp3}
+
+
+def zxp_jit_source(prog, challenges, publics, evals=None, rtc_check=False):
+    """Generated straight-line kernel source of a program (zkgpu_zxp_jit_source,
+    no GPU needed); with rtc_check, also compiled for gfx950 by hiprtc."""
+    ins, opn = prog.arrays()
+    ins = np.ascontiguousarray(ins, np.uint32)
+    opn = np.ascontiguousarray(opn, np.uint32)
+    ch = np.zeros(24, np.uint64)
+    c = _np(challenges).reshape(-1)
+    ch[:c.size] = c
+    pub = _np(publics if publics is not None else np.zeros(1, np.uint64))
+    ev = _np(evals if evals is not None else np.zeros(3, np.uint64)).reshape(-1)
+    buf = ctypes.create_string_buffer(1 << 22)
+    rc = lib().zkgpu_zxp_jit_source(ins.ctypes.data, ins.shape[0], opn.ctypes.data, opn.shape[0],
+                                    max(prog.n_tmp1, 1), max(prog.n_tmp3, 1), ch.ctypes.data, pub.ctypes.data,
+                                    pub.size if publics is not None else 0, ev.ctypes.data, ev.size // 3,
+                                    buf, len(buf), 1 if rtc_check else 0)
+    if rc < 0:
+        _check(rc, "zkgpu_zxp_jit_source")
+    return buf.value.decode()
 
 
 def h1h2_dev(h1, h1_ld, h2, h2_ld, f, f_ld, t, t_ld, n, dim):
