@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--blowup-bits", type=int, default=1)
     ap.add_argument("--cpu-sample-cols", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_COLS", "4")))
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--workload", choices=["lde", "merkle", "stark", "commit"], default="lde",
+    ap.add_argument("--workload", choices=["lde", "merkle", "stark", "commit", "stark-sharded"], default="lde",
                     help="lde = configs[1] (headline); merkle = configs[2] (2^23 x 100 Poseidon tree); "
                          "stark = configs[3] (full synthetic STARK proof, 2^23 trace); "
                          "commit = configs[4] (one trace column-sharded over the ranks: LDE + all-to-all + "
@@ -228,6 +228,15 @@ def main():
 
         def step():
             gs.prove_raw()
+    elif args.workload == "stark-sharded":
+        # ONE proof of one trace for the whole job, extended domain row-sharded over the ranks
+        from zkgpu.sharded_stark import ShardedStark
+        inst = stark_instance(args.log_n, args.blowup_bits, C, args.queries)
+        ss = ShardedStark(inst, device=dev)  # setup: constants + sharded constant tree (untimed)
+        ss.witness()                         # executor stand-in (untimed)
+
+        def step():
+            ss.prove()
     elif args.workload == "lde":
         trace = torch.randint(0, 2**63 - 1, (C, n), dtype=torch.int64, device=dev, generator=g)
         out = torch.empty((C, ne), dtype=torch.int64, device=dev)
@@ -285,6 +294,10 @@ def main():
             total_elems = world * args.steps
             unit, metric_unit = "s/proof", "proofs"
             alg_step = 8 * (n + ne) * (C + 48 + 6)
+        elif args.workload == "stark-sharded":
+            total_elems = args.steps  # one proof per step for the whole job
+            unit, metric_unit = "s/proof", "proofs"
+            alg_step = 8 * (n + ne) * (C + 48 + 6) // world
         elif args.workload == "lde":
             total_elems = ne * C * world * args.steps
             unit, metric_unit = "Gelem/s", "LDE output elements"
@@ -294,7 +307,7 @@ def main():
             unit, metric_unit = "Gelem/s", "Merkle leaf elements hashed"
             alg_step = 8 * n * C + 32 * n + 96 * (n - 1)
         value = total_elems / elapsed / 1e9
-        if args.workload == "stark":
+        if args.workload in ("stark", "stark-sharded"):
             value = elapsed / total_elems  # seconds per proof, whole job
         cpu = None
         if world == 1 and not args.no_cpu and args.workload == "commit":
@@ -321,24 +334,30 @@ def main():
                         "2 plookups (dim 3 + dim 1), FRI steps %s, %d queries; one independent proof per GPU"
                         % (args.log_n, args.blowup_bits, inst.n_cm1, inst.n_cm2, inst.n_cm3, inst.n_cm4,
                            inst.n_const, inst.fri_steps, args.queries))
+            if args.workload == "stark-sharded":
+                workload = workload.replace("one independent proof per GPU",
+                                            "ONE proof for the whole job, row-sharded over %d rank(s)" % world)
         res = {
             "metric": METRIC,
             "value": round(value, 4),
             "unit": unit,
-            "value_meaning": (metric_unit + " per second, all GPUs") if args.workload != "stark" else "wall seconds per proof, whole job",
+            "value_meaning": ((metric_unit + " per second, all GPUs") if not args.workload.startswith("stark")
+                              else "wall seconds per proof, whole job"),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": args.workload != "stark",
-            "scaling": "strong" if args.workload == "commit" else "weak",
+            "higher_is_better": not args.workload.startswith("stark"),
+            "scaling": "strong" if args.workload in ("commit", "stark-sharded") else "weak",
             "vs_baseline": None,
-            "dtype": "u64 (Goldilocks)" if args.workload != "stark" else "u64 (Goldilocks) + F_p^3",
+            "dtype": "u64 (Goldilocks)" if not args.workload.startswith("stark") else "u64 (Goldilocks) + F_p^3",
             "data": "synthetic (uniform canonical Goldilocks, torch generator seed 0x5EED+rank)",
             "config": {
                 "workload": workload,
                 "log_n": args.log_n, "blowup_bits": args.blowup_bits, "ncols_per_gpu": C,
                 "parallelism": {"stark": "replicas x%d (one independent proof per GPU)" % world,
+                                "stark-sharded": ("one proof, extended domain row-sharded x%d: RCCL all-to-all "
+                                                  "column->row blocks per commit, halo + q/f all-gathers" % world),
                                 "commit": "column-sharded x%d, RCCL all-to-all column->row blocks" % world}.get(
                     args.workload, "column-sharded x%d (no data-path collective)" % world),
             },
@@ -361,6 +380,8 @@ def main():
         }
         if gs is not None:
             res["stages_ms"] = {k: round(v, 3) for k, v in gs.timers().items()}
+        if args.workload == "stark-sharded":
+            res["stages_ms"] = {k: round(v, 3) for k, v in ss.timers.items()}
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -77,6 +77,11 @@ int zkgpu_cols_to_rows_dev(uint64_t *rows, const uint64_t *cols, uint64_t ld, ui
  * PoseidonGoldilocks::hash_full_result(Element out[12], const Element in[12])
  * -- transcript.cpp:23,46.  Computed on the GPU. */
 int zkgpu_gl_poseidon_full(uint64_t out[12], const uint64_t in[12]);
+/* The same permutation on the host CPU (no GPU, no zkgpu_init): the
+ * transcript's (Transcript::put/getFields, transcript.cpp:18-24 ->
+ * PoseidonGoldilocks::hash_full_result), where one serial permutation sits on
+ * the critical path and a GPU launch would only add latency. */
+int zkgpu_gl_poseidon_full_host(uint64_t out[12], const uint64_t in[12]);
 /* PoseidonGoldilocks::hash(Element out[4], const Element in[12]) */
 int zkgpu_gl_poseidon_hash(uint64_t out[4], const uint64_t in[12]);
 /* PoseidonGoldilocks::linear_hash(Element *out, Element *in, uint64_t size)
@@ -168,6 +173,20 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
                        uint32_t n_tmp3, const zkgpu_sections *sections, uint32_t log_dom, const uint64_t *challenges,
                        const uint64_t *publics, uint32_t n_publics, const uint64_t *evals, uint32_t n_evals,
                        const uint64_t *xdiv, const uint64_t *xdivw, uint32_t extend_bits, uint64_t x_start);
+
+/* The same over ONE ROW BLOCK of a row-sharded domain (the
+ * quotient and FRI programs run on the rows a GPU owns after the column ->
+ * row exchange).  Rows 0 .. 2^log_rows - 1 of every section are evaluated;
+ * x_i = x_start * w_{2^log_domain}^i (x_start = 7 * w^row0 for a block
+ * starting at global row row0), zhInv uses N = 2^(log_domain - extend_bits)
+ * (row0 must be a multiple of 2^extend_bits), and a read at row shift s >= 0
+ * does not wrap: the caller stores the next block's first s rows (the halo)
+ * after the block, so every section's ld >= 2^log_rows + s. */
+int zkgpu_zxp_eval_block_dev(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd, uint32_t n_tmp1,
+                             uint32_t n_tmp3, const zkgpu_sections *sections, uint32_t log_rows, uint32_t log_domain,
+                             const uint64_t *challenges, const uint64_t *publics, uint32_t n_publics,
+                             const uint64_t *evals, uint32_t n_evals, const uint64_t *xdiv, const uint64_t *xdivw,
+                             uint32_t extend_bits, uint64_t x_start);
 
 /* Host-only compiler behind zkgpu_zxp_eval_dev (include/zkgpu_zxp.h,
  * "compiled programs"): folds the row-constant operands (challenges 8 x 3,

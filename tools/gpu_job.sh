@@ -117,6 +117,16 @@ for step in "$@"; do
             echo "rows=$r $(python -c "import json;d=json.load(open('gpurun_out/zxp_r$r.json'));print(d['ms_per_step'],'ms', d['kernels']['k_zxp_eval'])")"
         done
         ;;
+    sharded)
+        timeout -k 10 600 python -m pytest tests/test_sharded_stark.py -x -q -p no:cacheprovider -m gpu \
+            > gpurun_out/pytest_sharded.log 2>&1
+        ok_or_stop $? "pytest sharded stark gpu"
+        tail -3 gpurun_out/pytest_sharded.log
+        timeout -k 10 600 python bench.py --workload stark-sharded --steps 3 --warmup 1 --no-cpu \
+            > gpurun_out/bench_stark_sharded.json 2> gpurun_out/bench_stark_sharded.err
+        ok_or_stop $? "bench stark-sharded"
+        cat gpurun_out/bench_stark_sharded.json
+        ;;
     jitsweep)
         for cfg in "8 0" "1000 0" "8 4" "4 0"; do
             set -- $cfg

@@ -11,6 +11,7 @@
 
 #include "gl_device.hpp"
 #include "zkgpu_internal.hpp"
+#include "poseidon_gl_constants.h"
 
 namespace zk {
 
@@ -380,6 +381,57 @@ static int poseidon_one(uint64_t *out, const uint64_t *in, int full)
 }
 
 int zkgpu_gl_poseidon_full(uint64_t out[12], const uint64_t in[12]) { return poseidon_one(out, in, 1); }
+
+// Host permutation for the transcript (PoseidonGoldilocks::hash_full_result
+// on the CPU, transcript.cpp:18-24): textbook rounds
+// (poseidon_g_executor.cpp:201-231): add constants, x^7 on all lanes
+// (rounds 0-3, 26-29) or lane 0, then M[i][j] = MCIRC[(j - i) mod 12] +
+// (i == j == 0) * 8.  Needs no GPU and no zkgpu_init.
+static uint64_t hp_mul(uint64_t a, uint64_t b)
+{
+    const unsigned __int128 x = (unsigned __int128)a * b;
+    const uint64_t lo = (uint64_t)x, hi = (uint64_t)(x >> 64);
+    const uint64_t hh = hi >> 32, hl = hi & 0xFFFFFFFFULL;
+    uint64_t t0 = lo - hh;
+    if (lo < hh) t0 -= 0xFFFFFFFFULL;  // borrow: 2^64 == 2^32 - 1
+    const uint64_t t1 = (hl << 32) - hl;
+    uint64_t r = t0 + t1;
+    if (r < t1) r += 0xFFFFFFFFULL;
+    return r >= HP ? r - HP : r;
+}
+
+int zkgpu_gl_poseidon_full_host(uint64_t out[12], const uint64_t in[12])
+{
+    static const uint32_t MC[12] = {17, 15, 41, 16, 2, 28, 13, 13, 39, 18, 34, 20};
+    uint64_t st[12];
+    for (int i = 0; i < 12; i++) st[i] = in[i] % HP;
+    for (int r = 0; r < 30; r++) {
+        const bool full = r < 4 || r >= 26;
+        for (int i = 0; i < 12; i++) {
+            uint64_t x = st[i] + ZKGPU_POSEIDON_RC[r * 12 + i];
+            if (x < st[i] || x >= HP) x -= HP;
+            if (full || i == 0) {
+                const uint64_t x2 = hp_mul(x, x), x3 = hp_mul(x2, x), x4 = hp_mul(x2, x2);
+                x = hp_mul(x3, x4);
+            }
+            st[i] = x;
+        }
+        uint64_t t[12];
+        for (int i = 0; i < 12; i++) {
+            // an MDS row: 13 products of a canonical lane and a constant < 2^6 -> < 2^74
+            unsigned __int128 acc = (i == 0) ? (unsigned __int128)st[0] * 8 : 0;
+            for (int j = 0; j < 12; j++) acc += (unsigned __int128)st[j] * MC[(j - i + 12) % 12];
+            const uint64_t lo = (uint64_t)acc, hi = (uint64_t)(acc >> 64);  // hi < 2^10
+            const uint64_t hv = (hi << 32) - hi;                            // hi * 2^64 mod p
+            uint64_t v = lo + hv;
+            if (v < hv) v += 0xFFFFFFFFULL;
+            t[i] = v >= HP ? v - HP : v;
+        }
+        memcpy(st, t, sizeof t);
+    }
+    memcpy(out, st, sizeof st);
+    return 0;
+}
 int zkgpu_gl_poseidon_hash(uint64_t out[4], const uint64_t in[12]) { return poseidon_one(out, in, 0); }
 
 int zkgpu_gl_poseidon_batch_dev(uint64_t *out, const uint64_t *in, uint64_t n, int full)
@@ -694,14 +746,18 @@ static void zxp_alloc_slots(const zxp_instr *in, uint32_t n_instr, std::vector<z
     }
 }
 
-int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd, uint32_t n_tmp1,
-                       uint32_t n_tmp3, const zkgpu_sections *sections, uint32_t log_dom, const uint64_t *challenges,
-                       const uint64_t *publics, uint32_t n_publics, const uint64_t *evals, uint32_t n_evals,
-                       const uint64_t *xdiv, const uint64_t *xdivw, uint32_t extend_bits, uint64_t x_start)
+// log_dom: rows evaluated (2^log_dom); log_omega: x_i = x_start * w_{2^log_omega}^i and zhInv's N =
+// 2^(log_omega - extend_bits); wrap: shifted reads wrap mod 2^log_dom, else halo rows follow the block
+static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd, uint32_t n_tmp1,
+                         uint32_t n_tmp3, const zkgpu_sections *sections, uint32_t log_dom, uint32_t log_omega,
+                         int wrap, const uint64_t *challenges, const uint64_t *publics, uint32_t n_publics,
+                         const uint64_t *evals, uint32_t n_evals, const uint64_t *xdiv, const uint64_t *xdivw,
+                         uint32_t extend_bits, uint64_t x_start)
 {
     int rc;
     if ((rc = require_init())) return rc;
-    if (log_dom > TW_MAX_LOG) return set_error(ZKGPU_ERR_ARG, "zxp: domain too large");
+    if (log_omega > TW_MAX_LOG || log_dom > log_omega) return set_error(ZKGPU_ERR_ARG, "zxp: domain too large");
+    if (extend_bits > log_omega) return set_error(ZKGPU_ERR_ARG, "zxp: extend bits exceed the domain");
     // validate operands on the host (no out-of-range reads in the kernel)
     const zxp_instr *in = (const zxp_instr *)instr;
     const zxp_operand *op = (const zxp_operand *)opnd;
@@ -717,8 +773,11 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
         case ZXP_COL:
         case ZXP_COL3: {
             const uint32_t w = o.kind == ZXP_COL3 ? 3 : 1;
+            const int32_t sh = (int32_t)o.c;
+            // without wrap-around a shifted read touches halo rows [2^log_dom, 2^log_dom + sh)
+            const uint64_t need = (1ULL << log_dom) + (wrap ? 0 : (uint64_t)(sh > 0 ? sh : 0));
             bad = o.a >= SEC_COUNT || !sections->sec[o.a] || (uint64_t)o.b + w > sections->ncols[o.a] ||
-                  sections->ld[o.a] < (1ULL << log_dom);
+                  sections->ld[o.a] < need || (!wrap && sh < 0);
             break;
         }
         case ZXP_CHAL: bad = o.a >= 8; break;
@@ -778,7 +837,7 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
     // zhInv[j] = 1/(7^N * W[eb]^j - 1)  (zhInv.cpp:7-31), N = 2^(log_dom - eb)
     uint64_t zhv[64];
     {
-        uint64_t sn = h_pow(7, 1ULL << (log_dom - extend_bits));
+        uint64_t sn = h_pow(7, 1ULL << (log_omega - extend_bits));
         uint64_t we = h_w(extend_bits), w = 1;
         for (size_t j = 0; j < zh; j++) {
             const uint64_t x = h_mul(sn, w);  // < HP
@@ -911,6 +970,8 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
     L.n_tmp1 = n_tmp1;
     L.n_tmp3 = n_tmp3;
     L.logdom = log_dom;
+    L.logomega = log_omega;
+    L.wrap = wrap ? 1u : 0u;
     L.challenges = nullptr;
     L.publics = nullptr;
     L.evals = nullptr;
@@ -943,6 +1004,8 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
         J.n_tmp3 = n_tmp3;
         J.sections = sections;
         J.log_dom = log_dom;
+        J.log_omega = log_omega;
+        J.wrap = wrap ? 1u : 0u;
         J.challenges = challenges;
         J.publics = publics;
         J.evals = evals;
@@ -960,6 +1023,25 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
         if (rc <= 0) return rc;  // launched, or an error; 1 = shape unsupported
     }
     return zxp_eval(L, s);
+}
+
+int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd, uint32_t n_tmp1,
+                       uint32_t n_tmp3, const zkgpu_sections *sections, uint32_t log_dom, const uint64_t *challenges,
+                       const uint64_t *publics, uint32_t n_publics, const uint64_t *evals, uint32_t n_evals,
+                       const uint64_t *xdiv, const uint64_t *xdivw, uint32_t extend_bits, uint64_t x_start)
+{
+    return zxp_eval_impl(instr, n_instr, opnd, n_opnd, n_tmp1, n_tmp3, sections, log_dom, log_dom, 1, challenges,
+                         publics, n_publics, evals, n_evals, xdiv, xdivw, extend_bits, x_start);
+}
+
+int zkgpu_zxp_eval_block_dev(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd, uint32_t n_tmp1,
+                             uint32_t n_tmp3, const zkgpu_sections *sections, uint32_t log_rows, uint32_t log_domain,
+                             const uint64_t *challenges, const uint64_t *publics, uint32_t n_publics,
+                             const uint64_t *evals, uint32_t n_evals, const uint64_t *xdiv, const uint64_t *xdivw,
+                             uint32_t extend_bits, uint64_t x_start)
+{
+    return zxp_eval_impl(instr, n_instr, opnd, n_opnd, n_tmp1, n_tmp3, sections, log_rows, log_domain, 0, challenges,
+                         publics, n_publics, evals, n_evals, xdiv, xdivw, extend_bits, x_start);
 }
 
 int zkgpu_calculate_z_dev(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,

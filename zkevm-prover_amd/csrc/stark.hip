@@ -98,8 +98,10 @@ struct ZxpEnv {
     const ZOp *prog;
     const ZTerm *terms;
     uint32_t n_instr;
-    uint32_t logdom;
-    uint64_t x_start;       // x_i = x_start * omega_dom^i
+    uint32_t logdom;        // rows evaluated: 2^logdom
+    uint32_t logomega;      // x_i = x_start * omega_{2^logomega}^i
+    uint64_t rmask;         // shifted reads: (i + shift) & rmask (all ones = no wrap, halo rows provided)
+    uint64_t x_start;
     const uint64_t *tw_lo;  // forward big twiddles (omega_2^28)
     const uint64_t *tw_hi;
 };
@@ -127,9 +129,9 @@ __device__ __forceinline__ Val zxp_load(const ZxpEnv &e, uint32_t kind, const ui
         r.dim = 3;
         break;
     }
-    case DK_C1: r.v.v[0] = ptr[(i + (uint64_t)(int64_t)ii) & ((1ULL << e.logdom) - 1)]; break;
+    case DK_C1: r.v.v[0] = ptr[(i + (uint64_t)(int64_t)ii) & e.rmask]; break;
     case DK_C3: {
-        const uint64_t *p = ptr + ((i + (uint64_t)(int64_t)ii) & ((1ULL << e.logdom) - 1));
+        const uint64_t *p = ptr + ((i + (uint64_t)(int64_t)ii) & e.rmask);
         r.v = gl3{{p[0], p[ld], p[2 * (uint64_t)ld]}};
         r.dim = 3;
         break;
@@ -137,7 +139,7 @@ __device__ __forceinline__ Val zxp_load(const ZxpEnv &e, uint32_t kind, const ui
     case DK_IMM1: r.v.v[0] = imm[0]; break;
     case DK_IMM3: r.v = gl3{{imm[0], imm[1], imm[2]}}; r.dim = 3; break;
     case DK_X: {
-        uint64_t ex = i << (TW_MAX_LOG - e.logdom);
+        uint64_t ex = i << (TW_MAX_LOG - e.logomega);
         r.v.v[0] = gl_mul(e.x_start, gl_mul(e.tw_lo[ex & (TW_LEVEL_SIZE - 1)], e.tw_hi[ex >> TW_LEVEL_BITS]));
         break;
     }
@@ -159,7 +161,7 @@ __global__ void __launch_bounds__(ZXP_THREADS) k_zxp_eval(ZxpEnv e)
     const uint64_t dom = 1ULL << e.logdom;
     const bool active = i < dom;
     const uint64_t ir = active ? i : 0;
-    const uint64_t dmask = dom - 1;
+    const uint64_t dmask = e.rmask;
     for (uint32_t k = 0; k < e.n_instr; k++) {
         const ZOp &z = e.prog[k];
         const uint32_t op = z.op;
@@ -549,6 +551,8 @@ int zxp_eval(const ZxpLaunch &L, hipStream_t s)
     e.terms = L.terms;
     e.n_instr = L.n_instr;
     e.logdom = L.logdom;
+    e.logomega = L.logomega;
+    e.rmask = L.wrap ? (1ULL << L.logdom) - 1 : ~0ULL;
     e.x_start = L.x_start;
     e.tw_lo = c.tw_lo[0];
     e.tw_hi = c.tw_hi[0];

@@ -114,7 +114,9 @@ struct ZxpLaunch {
     const ZOp *prog;  // device, n_instr records
     const ZTerm *terms;  // device, DOT terms
     uint32_t n_instr, n_tmp1, n_tmp3;
-    uint32_t logdom;
+    uint32_t logdom;    // rows evaluated
+    uint32_t logomega;  // x_i = x_start * omega_{2^logomega}^i
+    uint32_t wrap;      // shifted reads wrap mod 2^logdom (else halo rows follow)
     const uint64_t *challenges, *publics, *evals;  // device
     const uint64_t *xdiv, *xdivw;                  // device (2n domain) or null
     const uint64_t *zhinv;                         // device, 2^eb entries
@@ -131,7 +133,9 @@ struct ZxpJitIn {
     const uint64_t *csts;
     uint32_t n_tmp1, n_tmp3;
     const zkgpu_sections *sections;
-    uint32_t log_dom;
+    uint32_t log_dom;   // rows evaluated
+    uint32_t log_omega; // x_i = x_start * omega_{2^log_omega}^i
+    uint32_t wrap;      // shifted reads wrap mod 2^log_dom (else halo rows follow)
     const uint64_t *challenges, *publics, *evals;  // host
     const uint64_t *xdiv, *xdivw, *zh_dev;         // device
     uint32_t zmask;

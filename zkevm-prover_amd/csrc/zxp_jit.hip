@@ -55,8 +55,8 @@ struct JitParams {
     const uint32_t *kl;         // DOT limbs (unrolled terms)
     const JitTerm *zt;          // DOT column terms (looped)
     const uint64_t *xdiv, *xdivw, *zh, *tw_lo, *tw_hi;
-    uint64_t x_start;
-    uint32_t logdom, zmask;
+    uint64_t x_start, rmask;
+    uint32_t logdom, logomega, zmask;
 };
 
 const char *k_kernel_head = R"(
@@ -73,8 +73,8 @@ struct JitParams {
     const uint32_t *kl;
     const JitTerm *zt;
     const uint64_t *xdiv, *xdivw, *zh, *tw_lo, *tw_hi;
-    uint64_t x_start;
-    uint32_t logdom, zmask;
+    uint64_t x_start, rmask;
+    uint32_t logdom, logomega, zmask;
 };
 // long column runs of a DOT: a loop over table terms, 4 loads in flight
 template <int D>
@@ -106,9 +106,9 @@ __device__ __forceinline__ void dot_cols(Dot3 &d0, Dot3 &d1, Dot3 &d2, const Jit
 }
 extern "C" __global__ void __launch_bounds__(256) ZKJIT_WAVES zxp_jit(const JitParams p)
 {
-    const uint64_t m = (1ULL << p.logdom) - 1;
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i > m) return;
+    if (i >= (1ULL << p.logdom)) return;
+    const uint64_t m = p.rmask;
 #define C(j, sh) p.cp[j][(i + (uint64_t)(sh)) & m]
 )";
 
@@ -548,7 +548,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     for (uint32_t j = 0; j < written_any.size(); j++)
         if (written_any[j]) appendf(src, "uint64_t w%u = 0;\n", j);
     if (uses_x)
-        appendf(src, "const uint64_t ex_ = i << (%u - p.logdom);\n"
+        appendf(src, "const uint64_t ex_ = i << (%u - p.logomega);\n"
                      "const uint64_t xv = gl_mul(p.x_start, gl_mul(p.tw_lo[ex_ & %lluULL], p.tw_hi[ex_ >> %u]));\n",
                 TW_MAX_LOG, (unsigned long long)(TW_LEVEL_SIZE - 1), TW_LEVEL_BITS);
     src += body;
@@ -595,6 +595,8 @@ int zxp_jit_run(const ZxpJitIn &in, hipStream_t s)
     p.tw_hi = c.tw_hi[0];
     p.x_start = in.x_start;
     p.logdom = in.log_dom;
+    p.logomega = in.log_omega;
+    p.rmask = in.wrap ? (1ULL << in.log_dom) - 1 : ~0ULL;
     p.zmask = in.zmask;
     void *args[] = {&p};
     const uint64_t dom = 1ULL << in.log_dom;

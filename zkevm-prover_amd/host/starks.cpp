@@ -21,7 +21,6 @@
 
 #include "../../include/zkgpu.h"
 #include "../../include/zkgpu_stark.h"
-#include "../csrc/poseidon_gl_constants.h"
 
 namespace zkgpu_host {
 
@@ -71,64 +70,10 @@ static uint64_t rand_u64(uint64_t seed, uint64_t stream, uint64_t col, uint64_t 
 }
 
 // ---------------------------------------------------------------- transcript
-// Poseidon-GL permutation on the host for the transcript, which the reference
-// also runs on the CPU (transcript.cpp:18-24 -> PoseidonGoldilocks::
-// hash_full_result).  One permutation is a serial chain of ~600 dependent
-// products: ~5 us here, against ~70 us for a single-thread GPU launch plus its
-// synchronisation, and the transcript sits on the critical path between
-// stages.  Textbook rounds (poseidon_g_executor.cpp:201-231): add constants,
-// x^7 on all lanes (rounds 0-3, 26-29) or lane 0, then the MDS
-// M[i][j] = MCIRC[(j - i) mod 12] + (i == j == 0) * 8.  Bulk hashing (Merkle
-// trees) stays on the GPU; tests pin this against the GPU prover's oracle
-// (identical proofs) and the golden transcript replay.
-static uint64_t fmul(uint64_t a, uint64_t b)
-{
-    const unsigned __int128 x = (unsigned __int128)a * b;
-    const uint64_t lo = (uint64_t)x, hi = (uint64_t)(x >> 64);
-    const uint64_t hh = hi >> 32, hl = hi & 0xFFFFFFFFULL;
-    uint64_t t0 = lo - hh;
-    if (lo < hh) t0 -= 0xFFFFFFFFULL;  // borrow: 2^64 == 2^32 - 1
-    const uint64_t t1 = (hl << 32) - hl;
-    uint64_t r = t0 + t1;
-    if (r < t1) r += 0xFFFFFFFFULL;
-    return r >= P ? r - P : r;
-}
-// x < 2^96 (an MDS row: 13 products of a canonical lane and a constant < 2^6)
-static uint64_t red96(unsigned __int128 x)
-{
-    const uint64_t lo = (uint64_t)x, hi = (uint64_t)(x >> 64);  // hi < 2^32
-    const uint64_t t = (hi << 32) - hi;                          // hi * 2^64 mod p
-    uint64_t r = lo + t;
-    if (r < t) r += 0xFFFFFFFFULL;
-    return r >= P ? r - P : r;
-}
-static void poseidon_host(uint64_t out[12], const uint64_t in[12])
-{
-    static const uint32_t MC[12] = {17, 15, 41, 16, 2, 28, 13, 13, 39, 18, 34, 20};
-    uint64_t st[12];
-    for (int i = 0; i < 12; i++) st[i] = in[i] % P;
-    for (int r = 0; r < 30; r++) {
-        const bool full = r < 4 || r >= 26;
-        for (int i = 0; i < 12; i++) {
-            uint64_t x = st[i] + ZKGPU_POSEIDON_RC[r * 12 + i];
-            if (x < st[i] || x >= P) x -= P;
-            if (full || i == 0) {
-                const uint64_t x2 = fmul(x, x), x3 = fmul(x2, x), x4 = fmul(x2, x2);
-                x = fmul(x3, x4);
-            }
-            st[i] = x;
-        }
-        uint64_t t[12];
-        for (int i = 0; i < 12; i++) {
-            unsigned __int128 acc = (i == 0) ? (unsigned __int128)st[0] * 8 : 0;
-            for (int j = 0; j < 12; j++) acc += (unsigned __int128)st[j] * MC[(j - i + 12) % 12];
-            t[i] = red96(acc);
-        }
-        memcpy(st, t, sizeof t);
-    }
-    memcpy(out, st, sizeof st);
-}
-
+// The transcript runs on the host, as the reference's (transcript.cpp:4-87):
+// its permutations are a serial chain on the critical path between stages, so
+// they use the host permutation zkgpu_gl_poseidon_full_host (~5 us) rather
+// than a single-thread GPU launch plus a synchronisation (~70 us, 90 per proof).
 // Transcript (transcript.cpp:4-87)
 class Transcript
 {
@@ -144,7 +89,7 @@ public:
         uint64_t in[12];
         memcpy(in, pending, 64);
         memcpy(in + 8, state, 32);
-        poseidon_host(out, in);
+        if (zkgpu_gl_poseidon_full_host(out, in)) err = -1;
         out_cursor = 12;
         memset(pending, 0, sizeof pending);
         pending_cursor = 0;

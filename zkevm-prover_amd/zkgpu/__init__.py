@@ -47,6 +47,9 @@ _SIGS = {
     "zkgpu_rows_to_cols_dev": (ctypes.c_int, [vp, u64, vp, u64, u64]),
     "zkgpu_cols_to_rows_dev": (ctypes.c_int, [vp, vp, u64, u64, u64]),
     "zkgpu_gl_poseidon_full": (ctypes.c_int, [vp, vp]),
+    "zkgpu_gl_poseidon_full_host": (ctypes.c_int, [vp, vp]),
+    "zkgpu_zxp_eval_block_dev": (ctypes.c_int, [vp, u32, vp, u32, u32, u32, vp, u32, u32, vp, vp, u32, vp, u32, vp,
+                                                vp, u32, u64]),
     "zkgpu_gl_poseidon_hash": (ctypes.c_int, [vp, vp]),
     "zkgpu_gl_linear_hash": (ctypes.c_int, [vp, vp, u64]),
     "zkgpu_gl_poseidon_batch_dev": (ctypes.c_int, [vp, vp, u64, ctypes.c_int]),
@@ -189,6 +192,14 @@ def poseidon_full(x):
     x = _np(x)
     out = np.zeros(12, np.uint64)
     _check(lib().zkgpu_gl_poseidon_full(out.ctypes.data, x.ctypes.data), "zkgpu_gl_poseidon_full")
+    return out
+
+
+def poseidon_full_host(x):
+    """PoseidonGoldilocks::hash_full_result on the host (the transcript's)."""
+    x = _np(x)
+    out = np.zeros(12, np.uint64)
+    _check(lib().zkgpu_gl_poseidon_full_host(out.ctypes.data, x.ctypes.data), "zkgpu_gl_poseidon_full_host")
     return out
 
 
@@ -406,6 +417,43 @@ def zxp_jit_source(prog, challenges, publics, evals=None, rtc_check=False):
     if rc < 0:
         _check(rc, "zkgpu_zxp_jit_source")
     return buf.value.decode()
+
+
+def zxp_eval_block_dev(prog, sections, log_rows, log_domain, challenges, publics, evals=None, xdiv=None, xdivw=None,
+                       extend_bits=0, x_start=7):
+    """One row block of a row-sharded domain (zkgpu_zxp_eval_block_dev):
+    sections carry the block plus halo rows; x_start = 7 * w^row0."""
+    ins, opn = prog.arrays()
+    ins = np.ascontiguousarray(ins, np.uint32)
+    opn = np.ascontiguousarray(opn, np.uint32)
+    s = Sections()
+    for k, (t, ld, nc) in sections.items():
+        s.sec[k] = _addr(t)
+        s.ld[k] = ld
+        s.ncols[k] = nc
+    ch = np.zeros(24, np.uint64)
+    c = _np(challenges).reshape(-1)
+    ch[:c.size] = c
+    pub = _np(publics if publics is not None else np.zeros(1, np.uint64))
+    ev = _np(evals if evals is not None else np.zeros(3, np.uint64)).reshape(-1)
+    _check(lib().zkgpu_zxp_eval_block_dev(ins.ctypes.data, ins.shape[0], opn.ctypes.data, opn.shape[0],
+                                          max(prog.n_tmp1, 1), max(prog.n_tmp3, 1), ctypes.byref(s), log_rows,
+                                          log_domain, ch.ctypes.data, pub.ctypes.data,
+                                          pub.size if publics is not None else 0, ev.ctypes.data, ev.size // 3,
+                                          _addr(xdiv), _addr(xdivw), extend_bits, x_start),
+           "zkgpu_zxp_eval_block_dev")
+
+
+def merkle_open_rows_dev(nodes, src, ncols, nrows, idx):
+    """MerkleTreeGL::getGroupProof for a row-major device source."""
+    idx = _np(idx).reshape(-1)
+    nq = idx.size
+    nlev = max(0, int(nrows).bit_length() - 1)
+    vals = np.zeros((nq, ncols), np.uint64)
+    sibs = np.zeros((nq, nlev, 4), np.uint64)
+    _check(lib().zkgpu_gl_merkle_open_rows_dev(vals.ctypes.data, sibs.ctypes.data, _addr(nodes), _addr(src), ncols,
+                                               nrows, idx.ctypes.data, nq), "zkgpu_gl_merkle_open_rows_dev")
+    return vals, sibs
 
 
 def h1h2_dev(h1, h1_ld, h2, h2_ld, f, f_ld, t, t_ld, n, dim):

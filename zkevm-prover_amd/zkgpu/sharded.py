@@ -27,6 +27,41 @@ is no CPU fallback in the product.
 import numpy as np
 
 
+def _staged(group, t):
+    """gloo cannot run collectives on device tensors: stage through the host
+    (tests of the multi-process path on one GPU); RCCL ("nccl") runs on device."""
+    import torch.distributed as dist
+    try:
+        backend = dist.get_backend(group)
+    except Exception:
+        backend = "gloo"
+    return backend != "nccl" and t.is_cuda
+
+
+def all_gather(t, group=None):
+    """List of every rank's tensor (same shape), on t's device."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return [t]
+    stage = _staged(group, t)
+    src = t.cpu() if stage else t.contiguous()
+    out = [torch.empty_like(src) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(out, src, group=group)
+    return [o.to(t.device) for o in out] if stage else out
+
+
+def all_to_all(out, inp, out_splits, in_splits, group=None):
+    """all_to_all_single over flat tensors (RCCL on device; gloo via the host)."""
+    import torch.distributed as dist
+    if _staged(group, inp):
+        o = out.cpu()
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+
+
 def col_range(ncols, world, rank):
     """Balanced contiguous column split."""
     base, extra = divmod(ncols, world)
@@ -106,21 +141,28 @@ class ShardedCommit:
             # pack [dest rank][owned column][row in block] (contiguous per destination)
             send = ext[:c_r].reshape(c_r, W, rows).permute(1, 0, 2).contiguous().reshape(-1)
             self.block = k.empty((self.ncols, rows))
-            self.dist.all_to_all_single(self.block.reshape(-1), send, [c * rows for c in self.counts],
-                                        [c_r * rows] * W, group=self.group)
+            all_to_all(self.block.reshape(-1), send, [c * rows for c in self.counts], [c_r * rows] * W,
+                       group=self.group)
+        return self._merkelize()
+
+    def commit_rows(self, block):
+        """Commit when every rank already holds its row block of the extended
+        evaluations (ncols x rows, column-major): subtree + sub-root gather."""
+        self.block = block
+        return self._merkelize()
+
+    def _merkelize(self):
+        k, W, rows = self.k, self.world, self.rows
         self.nodes = k.merkle(self.block, rows, self.ncols, rows)
         sub = k.root(self.nodes)
         if W == 1:
             self.top = [[sub]]
             return sub
         import torch
-        gathered = [torch.zeros(4, dtype=torch.int64) for _ in range(W)]
         mine = torch.from_numpy(sub.view(np.int64).copy())
         if self._backend_is_nccl():
-            dev = self.block.device
-            gathered = [g.to(dev) for g in gathered]
-            mine = mine.to(dev)
-        self.dist.all_gather(gathered, mine, group=self.group)
+            mine = mine.to(self.block.device)
+        gathered = all_gather(mine, self.group)
         level = [g.cpu().numpy().view(np.uint64).copy() for g in gathered]
         self.top = [level]
         while len(level) > 1:
@@ -133,6 +175,25 @@ class ShardedCommit:
             return self.dist.get_backend(self.group) == "nccl"
         except Exception:
             return False
+
+    def open_local_many(self, idxs):
+        """{global row: (values, siblings)} for the rows of idxs this rank owns
+        (one batched opening launch)."""
+        own = sorted({int(i) for i in idxs if int(i) // self.rows == self.rank})
+        if not own:
+            return {}
+        vals, sibs = self.k.open(self.nodes, self.block, self.rows, self.ncols, self.rows,
+                                 [i % self.rows for i in own])
+        out = {}
+        for n, idx in enumerate(own):
+            top_sibs = []
+            j = self.rank
+            for level in self.top[:-1]:
+                top_sibs.append(level[j ^ 1])
+                j >>= 1
+            out[idx] = (vals[n], np.concatenate([sibs[n].reshape(-1, 4),
+                                                 np.array(top_sibs, np.uint64).reshape(-1, 4)]))
+        return out
 
     def open_local(self, idx):
         """Opening of global row idx if this rank owns it: (values, siblings)
