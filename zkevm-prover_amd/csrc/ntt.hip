@@ -17,7 +17,11 @@
 //   Zero padding (LDE) is a predicated load in the first NTT pass; the
 //   1/n * shift^k factor of the LDE is fused into the last INTT pass.
 //   n <= 4096 uses a single-workgroup-per-column LDS kernel.
+#include <stdlib.h>
+
+#include <algorithm>
 #include <utility>
+#include <vector>
 
 #include "gl_device.hpp"
 #include "zkgpu_internal.hpp"
@@ -64,6 +68,8 @@ struct PassArgs {
     uint32_t last;  // 1 = last pass (digit-reversed scatter)
     uint32_t npass;
     uint32_t rbits[NTT_MAX_PASSES];
+    const uint64_t *otw;  // outer twiddles omega_m^(j' k) at [k << logmp | j'] (null: recurrence)
+    uint32_t ncols;       // columns in this launch (grid x = unit * ncols + column)
 };
 
 constexpr int GROUPS = 16;
@@ -126,11 +132,13 @@ __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
     constexpr int T = GROUPS * R2;
     __shared__ uint64_t lds[R * 17];
     __shared__ uint64_t twR[R];  // omega_R^i
-    const uint32_t col = blockIdx.y;
+    // columns vary fastest across workgroups: the workgroups sharing a unit's
+    // outer-twiddle slice run together and find it in L2
+    const uint32_t col = blockIdx.x % a.ncols;
+    const uint64_t u = blockIdx.x / a.ncols;
     const uint64_t *src = a.src + (uint64_t)col * a.src_ld;
     uint64_t *dst = a.dst + (uint64_t)col * a.dst_ld;
     const int tid = threadIdx.x;
-    const uint64_t u = blockIdx.x;
 
     // omega_R^i = omega_{2^28}^(i << (28 - LOGR))
     for (int i = tid; i < R; i += T) twR[i] = tw_big(a.tw_lo, a.tw_hi, (uint64_t)i << (TW_MAX_LOG - LOGR));
@@ -183,7 +191,19 @@ __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
 #pragma unroll
     for (int jj = 0; jj < R2; jj++) v[jj] = lds[(k1 * R2 + jj) * 17 + g];
     dft_regs<L2, INV>(v);
-    if (!a.last) {
+    if (!a.last && a.otw) {
+        // X[k] * omega_m^(j' k) from the table (one coalesced load per element
+        // instead of a recurrence product), k = k1 + R1*k2, j' = j0 + g
+        const uint64_t jp = (base & ((1ULL << logmp) - 1)) + g;
+#pragma unroll
+        for (int k2 = 0; k2 < R2; k2++) {
+            const int r = brev_c(k2, L2);
+            const uint64_t k = (uint64_t)(k1 + R1 * k2);
+            uint64_t x = v[r];
+            if (k1 | k2) x = gl_mul(x, a.otw[(k << logmp) + jp]);
+            dst[base + (k << logmp) + g] = x;  // intermediate: lazy
+        }
+    } else if (!a.last) {
         // X[k] * omega_m^(j' k), k = k1 + R1*k2, j' = j0 + g
         const uint32_t tshift = TW_MAX_LOG - a.logm;
         const uint64_t jp = (base & ((1ULL << logmp) - 1)) + g;
@@ -317,7 +337,50 @@ __global__ void k_cols_to_rows(const uint64_t *__restrict__ in, uint64_t *__rest
     }
 }
 
+// outer twiddle table of a pass over blocks of m = 2^logm with sub-DFT size
+// R = 2^logr: out[k << (logm - logr) | j'] = omega_m^(j' k), k < R, j' < m / R
+__global__ void k_otw_table(uint64_t *out, const uint64_t *tw_lo, const uint64_t *tw_hi, uint32_t logm,
+                            uint32_t logr)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >> logm) return;
+    const uint32_t logmp = logm - logr;
+    const uint64_t k = i >> logmp, jp = i & ((1ULL << logmp) - 1);
+    out[i] = gl_canon(tw_big(tw_lo, tw_hi, (jp * k) << (TW_MAX_LOG - logm)));
+}
+
 // ---------------------------------------------------------------- host side
+// Outer-twiddle tables, built on first use per (direction, log m, log R) and
+// kept for the process (<= 2^OTW_MAX_LOG entries each; 128 MB at 2^24).
+constexpr uint32_t OTW_MAX_LOG = 24;
+struct OtwTable {
+    int d;
+    uint32_t logm, logr;
+    uint64_t *ptr;
+};
+static std::vector<OtwTable> g_otw;
+
+static const uint64_t *otw_table(Ctx &ctx, int d, uint32_t logm, uint32_t logr, hipStream_t s)
+{
+    static const int enabled = [] {
+        const char *v = getenv("ZKGPU_NTT_OTW");
+        return v ? atoi(v) : 1;
+    }();
+    if (!enabled || logm > OTW_MAX_LOG) return nullptr;
+    for (const OtwTable &t : g_otw)
+        if (t.d == d && t.logm == logm && t.logr == logr) return t.ptr;
+    uint64_t *p = nullptr;
+    const uint64_t m = 1ULL << logm;
+    if (hipMalloc((void **)&p, m * sizeof(uint64_t)) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;  // no memory for the table: the recurrence path is exact too
+    }
+    hipLaunchKernelGGL(k_otw_table, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, s, p, ctx.tw_lo[d], ctx.tw_hi[d],
+                       logm, logr);
+    g_otw.push_back(OtwTable{d, logm, logr, p});
+    return p;
+}
+
 static const char *PASS_NAMES[9] = {"", "", "", "", "k_ntt_pass<4>", "k_ntt_pass<5>",
                                      "k_ntt_pass<6>", "k_ntt_pass<7>", "k_ntt_pass<8>"};
 
@@ -335,7 +398,7 @@ static void launch_pass(const PassArgs &a, uint64_t ncols, int inverse, hipStrea
 {
     constexpr int LOGR = L1 + L2;
     uint64_t units = (1ULL << (a.logn - LOGR)) / 16;
-    dim3 grid((uint32_t)units, (uint32_t)ncols);
+    dim3 grid((uint32_t)(units * ncols));
     if (inverse)
         hipLaunchKernelGGL((k_ntt_pass<L1, L2, true>), grid, dim3(16 << L2), 0, s, a);
     else
@@ -408,6 +471,7 @@ int ntt_columns(Ctx &ctx, uint64_t *dst, uint64_t dst_ld, const uint64_t *src, u
         // factor ratio between outputs k1 + R1*k2 and k1 + R1*(k2+1): base^(R1 * n/R)
         const uint32_t rb = a.rbits[p];
         a.post_step = h_pow(post_base, (uint64_t)(1u << (rb / 2)) << (logn - rb));
+        a.otw = a.last ? nullptr : otw_table(ctx, d, logm, rb, s);
         if (p == 0) {
             a.src = src;
             a.src_ld = src_ld;
@@ -426,11 +490,15 @@ int ntt_columns(Ctx &ctx, uint64_t *dst, uint64_t dst_ld, const uint64_t *src, u
         }
         const uint64_t n = 1ULL << logn;
         const uint64_t nread = (a.src_valid < n ? a.src_valid : n);
-        for (uint64_t c0 = 0; c0 < ncols; c0 += 65535) {
-            uint64_t nc = ncols - c0 < 65535 ? ncols - c0 : 65535;
+        // columns per launch: grid x = units * columns, at most 2^32 threads
+        const uint64_t units = (1ULL << (logn - rb)) / 16;
+        const uint64_t cmax = std::max<uint64_t>(1, std::min<uint64_t>(65535, (1ULL << 32) / (units * 256)));
+        for (uint64_t c0 = 0; c0 < ncols; c0 += cmax) {
+            uint64_t nc = ncols - c0 < cmax ? ncols - c0 : cmax;
             PassArgs b = a;
             b.src = a.src + c0 * a.src_ld;
             b.dst = a.dst + c0 * a.dst_ld;
+            b.ncols = (uint32_t)nc;
             prof_begin(s);
             dispatch_pass(rb, b, nc, inverse, s);
             prof_end(PASS_NAMES[rb], 8.0 * (double)(nread + n) * (double)nc, s);
