@@ -752,10 +752,12 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
                          uint32_t n_tmp3, const zkgpu_sections *sections, uint32_t log_dom, uint32_t log_omega,
                          int wrap, const uint64_t *challenges, const uint64_t *publics, uint32_t n_publics,
                          const uint64_t *evals, uint32_t n_evals, const uint64_t *xdiv, const uint64_t *xdivw,
-                         uint32_t extend_bits, uint64_t x_start)
+                         uint32_t extend_bits, uint64_t x_start, int force_interp = 0)
 {
     int rc;
     if ((rc = require_init())) return rc;
+    const uint32_t n_instr0 = n_instr, n_tmp1_0 = n_tmp1, n_tmp3_0 = n_tmp3;
+    const void *opnd0 = opnd;
     if (log_omega > TW_MAX_LOG || log_dom > log_omega) return set_error(ZKGPU_ERR_ARG, "zxp: domain too large");
     if (extend_bits > log_omega) return set_error(ZKGPU_ERR_ARG, "zxp: extend bits exceed the domain");
     // validate operands on the host (no out-of-range reads in the kernel)
@@ -798,6 +800,13 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
     const char *env_terms = getenv("ZKGPU_ZXP_MAX_TERMS");
     const int fuse = env_fuse ? atoi(env_fuse) : 1;
     const uint32_t max_terms = env_terms ? (uint32_t)atoi(env_terms) : 0u;
+    // The compiled program runs as a run-time compiled straight-line kernel
+    // (csrc/zxp_jit.hip, compiled once per program per process) on domains of
+    // 2^16 rows and more, where it pays for its ~1-2 s compile; smaller
+    // domains use the interpreter.  ZKGPU_ZXP_JIT=0 never, =2 always.
+    const char *env_jit = getenv("ZKGPU_ZXP_JIT");
+    const int jit_mode = env_jit ? atoi(env_jit) : 1;
+    const bool use_jit = !force_interp && fuse && (jit_mode == 2 || (jit_mode == 1 && log_dom >= 16));
     std::vector<zxp_operand> opv;
     const zxp_instr *pin = in;
     const zxp_term *terms = nullptr;
@@ -805,6 +814,8 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
     uint32_t n_terms = 0;
     if (fuse) {
         zxp_compiled cp;
+        // (one compile serves both paths: measured, longer DOTs / fused DOT
+        // column passes / no live-temporary cap made the compiled kernels slower)
         if ((rc = zkgpu_zxp_compile(instr, n_instr, opnd, n_opnd, n_tmp1, n_tmp3, challenges, publics, n_publics,
                                     evals, n_evals, max_terms, &cp)))
             return rc;
@@ -939,7 +950,7 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
         if ((z.kd == DK_C1 || z.kd == DK_C3) && z.id != 0)
             return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u writes a shifted column", k);
     }
-    {
+    if (!use_jit) {  // interpreter temporaries live in LDS
         const uint64_t slots = (uint64_t)n_tmp1 + 3ULL * n_tmp3;
         if (slots * 64 * 8 > 160 * 1024)
             return set_error(ZKGPU_ERR_ARG, "zxp: %llu temp slots exceed LDS", (unsigned long long)slots);
@@ -987,13 +998,7 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
         else if (op[k].kind == ZXP_COL3) cols += 3;
         else if (op[k].kind == ZXP_XDIV || op[k].kind == ZXP_XDIVW) cols += 3;
     L.bytes = 8.0 * cols * (double)(1ULL << log_dom);
-    // The compiled program runs as a run-time compiled straight-line kernel
-    // (csrc/zxp_jit.hip, compiled once per program per process) on domains of
-    // 2^16 rows and more, where it pays for its ~1-2 s compile; smaller
-    // domains use the interpreter.  ZKGPU_ZXP_JIT=0 never, =2 always.
-    const char *env_jit = getenv("ZKGPU_ZXP_JIT");
-    const int jit_mode = env_jit ? atoi(env_jit) : 1;
-    if (fuse && (jit_mode == 2 || (jit_mode == 1 && log_dom >= 16))) {
+    if (use_jit) {
         ZxpJitIn J;
         J.ins = pin;
         J.n_instr = n_instr;
@@ -1020,7 +1025,10 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
         J.dot_loop_min = env_loop ? (uint32_t)atoi(env_loop) : 8u;
         J.waves_per_eu = env_waves ? (uint32_t)atoi(env_waves) : 0u;
         rc = zxp_jit_run(J, s);
-        if (rc <= 0) return rc;  // launched, or an error; 1 = shape unsupported
+        if (rc <= 0) return rc;  // launched, or an error
+        // 1 = shape unsupported: compile for the interpreter instead
+        return zxp_eval_impl(instr, n_instr0, opnd0, n_opnd, n_tmp1_0, n_tmp3_0, sections, log_dom, log_omega, wrap,
+                             challenges, publics, n_publics, evals, n_evals, xdiv, xdivw, extend_bits, x_start, 1);
     }
     return zxp_eval(L, s);
 }
