@@ -12,6 +12,51 @@
 
 using namespace zk;
 
+// previous MDS form (round 1 v3): plain C, the compiler strength-reduces the
+// entries 2, 8, 16 into shift-adds and recombines with a 64-bit compare
+__device__ __forceinline__ void mds_fold_v1(uint64_t st[12], const uint64_t *K)
+{
+    uint32_t lo[12], hi[12];
+#pragma unroll
+    for (int y = 0; y < 12; y++) {
+        lo[y] = (uint32_t)st[y];
+        hi[y] = (uint32_t)(st[y] >> 32);
+    }
+#pragma unroll
+    for (int x = 0; x < 12; x++) {
+        uint64_t sl = (uint32_t)K[x], sh = K[x] >> 32;
+#pragma unroll
+        for (int y = 0; y < 12; y++) {
+            sl += (uint64_t)lo[y] * mds_entry(x, y);
+            sh += (uint64_t)hi[y] * mds_entry(x, y);
+        }
+        uint64_t l;
+        const bool c = __builtin_add_overflow(sl, sh << 32, &l);
+        const uint32_t h = (uint32_t)(sh >> 32) + (c ? 1u : 0u);
+        st[x] = gl_reduce96(l, h);
+    }
+}
+
+__device__ __forceinline__ void full_rounds_fold_v1(uint64_t st[12], int r0)
+{
+#pragma unroll 1
+    for (int r = r0; r < r0 + 4; r++) {
+#pragma unroll
+        for (int s = 0; s < 12; s++) st[s] = pow7(st[s]);
+        const uint64_t *K = r == 3 ? ZKGPU_PSP_PRE : (r == 29 ? ZKGPU_PS_ZERO12 : &ZKGPU_POSEIDON_RC[(r + 1) * 12]);
+        mds_fold_v1(st, K);
+    }
+}
+
+__device__ __forceinline__ void perm_fast_v1(uint64_t st[12])
+{
+#pragma unroll
+    for (int s = 0; s < 12; s++) st[s] = gl_add(st[s], ZKGPU_POSEIDON_RC[s]);
+    full_rounds_fold_v1(st, 0);
+    partial_rounds_blocks(st);
+    full_rounds_fold_v1(st, 26);
+}
+
 template <int V>
 __global__ void __launch_bounds__(256) k_perm(uint64_t *st_all, uint64_t n, int reps)
 {
@@ -26,6 +71,7 @@ __global__ void __launch_bounds__(256) k_perm(uint64_t *st_all, uint64_t n, int 
         if constexpr (V == 2) perm_sparse<false>(st);
         if constexpr (V == 3) perm_sparse<true>(st);
         if constexpr (V == 4) perm_fast(st);
+        if constexpr (V == 5) perm_fast_v1(st);
     }
 #pragma unroll
     for (int k = 0; k < 12; k++) st_all[k * n + i] = gl_canon(st[k]);
@@ -53,9 +99,10 @@ int main()
         {"sparse/halves", k_perm<2>},
         {"sparse/limbs24", k_perm<3>},
         {"fast (folded MDS + block dots)", k_perm<4>},
+        {"fast, previous MDS form", k_perm<5>},
     };
     int bad = 0;
-    for (int v = 0; v < 5; v++) {
+    for (int v = 0; v < 6; v++) {
         float best = 1e30f;
         for (int rep = 0; rep < 3; rep++) {
             (void)hipMemcpy(d, h, 12 * n * 8, hipMemcpyHostToDevice);
