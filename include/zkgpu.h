@@ -229,6 +229,12 @@ int zkgpu_xdivxsub_dev(uint64_t *xdiv, uint64_t *xdivw, const uint64_t xi[3], ui
 /* base^k for k < n into 3 columns of ld (LEv / LpEv, starks.cpp:308-324) */
 int zkgpu_ext_powers_dev(uint64_t *out, uint64_t ld, const uint64_t base[3], uint64_t n);
 
+/* cols[c][k] *= base^k for k < n, c < ncols (canonical outputs): the coset
+ * shift of coefficient vectors (the shift^i multiply of
+ * NTT_Goldilocks::extendPol, starks.cpp:53), used to move the quotient
+ * pieces between coset-scaled and plain coefficients. */
+int zkgpu_scale_by_powers_dev(uint64_t *cols, uint64_t ld, uint32_t ncols, uint64_t n, uint64_t base);
+
 /* quotient split (starks.cpp:266-281): qq2 col 3p+d row k = qq1 col d row pN+k * shift_in^p, k < n */
 int zkgpu_qsplit_dev(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t q_deg,
                      uint64_t shift_in);

@@ -116,18 +116,19 @@ def test_xdivxsub_dev(oracle, zkgpu):
     assert np.array_equal(zkgpu.from_device(db).reshape(-1, 3), b)
 
 
-def test_evmap_dev(oracle, zkgpu):
+@pytest.mark.parametrize("n,eb", [(1 << 12, 1), (3 * 61440 + 777, 0)])
+def test_evmap_dev(oracle, zkgpu, n, eb):
+    """Several row blocks (61440 rows each) and a ragged tail; sub-entry
+    groups of mixed size (dim-3 entries split into three)."""
     import ctypes
-    import torch
-    rng = np.random.default_rng(6)
-    n, eb = 1 << 12, 1
+    rng = np.random.default_rng(6 + n)
     ne = n << eb
-    cols = rand_gl(rng, (ne, 7))  # row-major for the oracle
+    cols = rand_gl(rng, (ne, 9))  # row-major for the oracle
     lev = rand_gl(rng, (n, 3))
     lpev = rand_gl(rng, (n, 3))
-    entries = [(0, 1, 0), (1, 1, 1), (2, 3, 0), (2, 3, 1), (6, 1, 0)]
+    entries = [(0, 1, 0), (1, 1, 1), (2, 3, 0), (2, 3, 1), (6, 1, 0), (5, 3, 1), (8, 1, 1), (7, 1, 0), (3, 3, 0)]
     ptrs = (ctypes.c_void_p * len(entries))(*[cols.ctypes.data + 8 * c for c, _, _ in entries])
-    strides = np.full(len(entries), 7, np.uint64)
+    strides = np.full(len(entries), 9, np.uint64)
     dims = np.array([d for _, d, _ in entries], np.uint32)
     primes = np.array([p for _, _, p in entries], np.uint32)
     ref = np.zeros((len(entries), 3), np.uint64)

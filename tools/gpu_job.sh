@@ -136,6 +136,15 @@ for step in "$@"; do
             echo "loop=$1 waves=$2 $(python -c "import json;d=json.load(open('gpurun_out/jit_$1_$2.json'));s=d['stages_ms'];print(d['ms_per_step'],'ms q',s['STARK_STEP_4_CALCULATE_EXPS_2NS'],'f',s['STARK_STEP_5_CALCULATE_EXPS'],'s2',s['STARK_STEP_2_CALCULATE_EXPS'],'s3',s['STARK_STEP_3_CALCULATE_EXPS'])")"
         done
         ;;
+    evsweep)
+        for cfg in "1 1" "2 1" "4 1" "1 4" "2 2" "2 4" "4 2" "4 4"; do
+            set -- $cfg
+            ZKGPU_EVMAP_G=$1 ZKGPU_EVMAP_U=$2 timeout -k 10 300 python bench.py --workload stark --steps 2 --warmup 1 --no-cpu \
+                > gpurun_out/ev_$1_$2.json 2>> gpurun_out/ev_sweep.err
+            ok_or_stop $? "stark evmap G=$1 U=$2"
+            echo "G=$1 U=$2 $(python -c "import json;d=json.load(open('gpurun_out/ev_$1_$2.json'));print(d['ms_per_step'],'ms evmap',d['kernels']['k_evmap'])")"
+        done
+        ;;
     sqpmc)
         # VALU/SALU/SMEM issue and wave-state counters for every kernel of a 2^20 STARK proof
         cd /tmp

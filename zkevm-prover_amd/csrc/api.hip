@@ -1078,30 +1078,65 @@ int zkgpu_evmap_dev(uint64_t *evals_out, const uint64_t *const *cols, const uint
     int rc;
     if ((rc = require_init())) return rc;
     if (!n_ev) return 0;
-    const size_t es = evmap_entry_size();
-    struct E {
-        const uint64_t *col;
-        uint64_t ld;
-        uint32_t dim, prime;
+    // sub-entries: a dim-1 entry is one, a dim-3 entry three (component j,
+    // weighted by X^j when the sums are combined); grouped by L (prime or not)
+    // into EV_G-wide groups
+    struct G {
+        const uint64_t *col[8];
+        uint32_t prime, sub0;
     };
-    if (es != sizeof(E)) return set_error(ZKGPU_ERR_ARG, "evmap entry layout");
-    E *h = (E *)malloc(n_ev * sizeof(E));
-    for (uint32_t e = 0; e < n_ev; e++) h[e] = E{cols[e], lds[e], dims[e], primes[e]};
-    uint32_t nchunks = 256;
-    while (nchunks > 1 && (n / nchunks) < 4096) nchunks >>= 1;
-    size_t off_part = ((n_ev * sizeof(E) + 15) & ~15ULL);
-    size_t off_ev = off_part + (size_t)n_ev * nchunks * 24;
-    char *p = param_buf(off_ev + n_ev * 24);
-    if (!p) {
-        free(h);
-        return set_error(ZKGPU_ERR_OOM, "param buffer");
+    if (evmap_group_size() != sizeof(G) || evmap_group_width() != 8) return set_error(ZKGPU_ERR_ARG, "evmap group layout");
+    static const uint32_t GW = [] {  // sub-entries per group: accumulator VGPRs vs shared limb work
+        const char *e = getenv("ZKGPU_EVMAP_G");
+        const uint32_t w = e ? (uint32_t)atoi(e) : 4u;
+        return (w == 1 || w == 2 || w == 4) ? w : 4u;
+    }();
+    static const uint32_t UR = [] {  // rows per thread and iteration
+        const char *e = getenv("ZKGPU_EVMAP_U");
+        const uint32_t u = e ? (uint32_t)atoi(e) : 2u;
+        return (u == 1 || u == 2 || u == 4) ? u : 2u;
+    }();
+    struct Sub {
+        const uint64_t *col;
+        uint32_t prime, which, entry;
+    };
+    std::vector<Sub> subs;
+    for (uint32_t e = 0; e < n_ev; e++) {
+        if (dims[e] != 1 && dims[e] != 3) return set_error(ZKGPU_ERR_ARG, "evmap: entry %u dim %u", e, dims[e]);
+        for (uint32_t j = 0; j < dims[e]; j++) subs.push_back(Sub{cols[e] + (uint64_t)j * lds[e], primes[e] ? 1u : 0u, j, e});
     }
-    rc = check_hip(hipMemcpyAsync(p, h, n_ev * sizeof(E), hipMemcpyHostToDevice, g_ctx.stream), "H2D");
-    if (!rc) rc = check_hip(hipStreamSynchronize(g_ctx.stream), "evmap param upload");
-    free(h);
-    if (rc) return rc;
-    if ((rc = evmap((uint64_t *)(p + off_ev), p, n_ev, lev, lpev, l_ld, n, extend_bits, (uint64_t *)(p + off_part),
-                    nchunks, g_ctx.stream)))
+    std::stable_sort(subs.begin(), subs.end(), [](const Sub &a, const Sub &b) { return a.prime < b.prime; });
+    std::vector<G> groups;
+    std::vector<int32_t> sub_of(3 * (size_t)n_ev, -1);
+    for (size_t i = 0; i < subs.size();) {
+        G g;
+        memset(&g, 0, sizeof(g));
+        g.prime = subs[i].prime;
+        g.sub0 = (uint32_t)i;
+        uint32_t c = 0;
+        while (c < GW && i < subs.size() && subs[i].prime == g.prime) {
+            g.col[c++] = subs[i].col;
+            sub_of[3 * (size_t)subs[i].entry + subs[i].which] = (int32_t)i;
+            i++;
+        }
+        groups.push_back(g);
+    }
+    const uint64_t rpb = evmap_rows_per_block();
+    const uint64_t nblk_ = (n + rpb - 1) / rpb;
+    const size_t off_sub = (groups.size() * sizeof(G) + 15) & ~15ULL;
+    const size_t off_part = (off_sub + sub_of.size() * 4 + 15) & ~15ULL;
+    const size_t off_ev = off_part + subs.size() * nblk_ * 24;
+    char *p = param_buf(off_ev + n_ev * 24);
+    if (!p) return set_error(ZKGPU_ERR_OOM, "param buffer");
+    if ((rc = check_hip(hipMemcpyAsync(p, groups.data(), groups.size() * sizeof(G), hipMemcpyHostToDevice,
+                                       g_ctx.stream), "H2D")) ||
+        (rc = check_hip(hipMemcpyAsync(p + off_sub, sub_of.data(), sub_of.size() * 4, hipMemcpyHostToDevice,
+                                       g_ctx.stream), "H2D")) ||
+        (rc = check_hip(hipStreamSynchronize(g_ctx.stream), "evmap param upload")))
+        return rc;
+    if ((rc = evmap_groups((uint64_t *)(p + off_ev), p, (uint32_t)groups.size(), GW, UR, (const int32_t *)(p + off_sub), n_ev,
+                           (uint32_t)subs.size(), lev, lpev, l_ld, n, extend_bits, (uint64_t *)(p + off_part),
+                           g_ctx.stream)))
         return rc;
     if ((rc = check_hip(hipMemcpyAsync(evals_out, p + off_ev, n_ev * 24, hipMemcpyDeviceToHost, g_ctx.stream), "D2H")))
         return rc;
@@ -1122,6 +1157,15 @@ int zkgpu_ext_powers_dev(uint64_t *out, uint64_t ld, const uint64_t base[3], uin
     if ((rc = require_init())) return rc;
     if (!n) return 0;
     return ext_powers(out, ld, base, n, g_ctx.stream);
+}
+
+int zkgpu_scale_by_powers_dev(uint64_t *cols, uint64_t ld, uint32_t ncols, uint64_t n, uint64_t base)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!n || !ncols) return 0;
+    if (ld < n) return set_error(ZKGPU_ERR_ARG, "scale_by_powers: ld < n");
+    return scale_powers(cols, ld, ncols, n, base, g_ctx.stream);
 }
 
 int zkgpu_qsplit_dev(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t q_deg,

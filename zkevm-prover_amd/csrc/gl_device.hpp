@@ -180,6 +180,18 @@ __device__ __forceinline__ gl3 gl3_rsub1(uint64_t a, const gl3 &b)
 struct Dot3 {
     uint64_t A0, A1, A2;
     __device__ __forceinline__ explicit Dot3(const uint32_t *k) : A0(k[0]), A1(k[1]), A2(k[2]) {}
+    __device__ __forceinline__ Dot3() : A0(0), A1(0), A2(0) {}
+    // limbs of a ROW-VARYING coefficient c (any u64): c and c * 2^32 mod p
+    __device__ __forceinline__ static void limbs(uint64_t c, uint32_t out[6])
+    {
+        const uint64_t cs = mul2e<32>(c);
+        out[0] = (uint32_t)c & 0x3FFFFFu;
+        out[1] = (uint32_t)(c >> 22) & 0x1FFFFFu;
+        out[2] = (uint32_t)(c >> 43);
+        out[3] = (uint32_t)cs & 0x3FFFFFu;
+        out[4] = (uint32_t)(cs >> 22) & 0x1FFFFFu;
+        out[5] = (uint32_t)(cs >> 43);
+    }
     __device__ __forceinline__ void term(uint64_t a, const uint32_t *c)
     {
         const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);

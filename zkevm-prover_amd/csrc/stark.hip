@@ -386,59 +386,93 @@ __global__ void k_z_check(uint32_t *ok, const uint64_t *z, uint64_t z_ld, const 
 }
 
 // ---------------------------------------------------------------- evmap
-struct EvEntry {
-    const uint64_t *col;  // first column of the polynomial (2ns section, column-major)
-    uint64_t ld;
-    uint32_t dim;
-    uint32_t prime;
-};
-
 constexpr int EV_THREADS = 256;
 
-// partial[e][blk] = sum over the block's rows k of L(k) * pol_e[k << eb]
-__global__ void __launch_bounds__(EV_THREADS) k_evmap(uint64_t *partial, const EvEntry *ents, uint32_t n_ev,
-                                                     const uint64_t *lev, const uint64_t *lpev, uint64_t l_ld,
-                                                     uint64_t n, uint32_t eb, uint64_t rows_per_block)
+// Sub-entry form: an F_p^3 entry pol = p0 + p1 X + p2 X^2 is three base
+// sub-entries, S_j = sum_k L(k) p_j[k] and pol(xi) = S_0 + S_1 X + S_2 X^2
+// (k_evmap_sum_subs).  EV_G sub-entries with the same L (prime or not) form
+// a group: each thread turns L(k) into Dot3 limbs once per row, and every
+// sub-entry's term costs 6 carry-free multiply-adds per component, instead of
+// a reduced F_p^3 product per entry and row.
+constexpr int EV_G = 8;  // group slots; a launch uses the first G (template)
+constexpr uint64_t EV_ROWS_PER_THREAD = 240;  // Dot3 accumulators: < 2^63 for <= 250 terms
+struct EvGroup {
+    const uint64_t *col[EV_G];  // null: unused slot
+    uint32_t prime, sub0;
+};
+
+// U rows per thread and iteration: all their loads are issued before the
+// multiply-adds (memory-level parallelism at the kernel's modest occupancy).
+template <int G, int U>
+__global__ void __launch_bounds__(EV_THREADS) k_evmap_groups(uint64_t *partial, const EvGroup *groups,
+                                                            const uint64_t *lev, const uint64_t *lpev, uint64_t l_ld,
+                                                            uint64_t n, uint32_t eb, uint64_t rows_per_block)
 {
     __shared__ gl3 sh[EV_THREADS];
-    const uint32_t e = blockIdx.x;  // entry fastest: a chunk's L rows are reused from L2 by all entries
+    const EvGroup g = groups[blockIdx.x];
     const uint64_t blk = blockIdx.y;
-    const EvEntry en = ents[e];
-    const uint64_t *L = en.prime ? lpev : lev;
-    gl3 acc{{0, 0, 0}};
+    const uint64_t *L = g.prime ? lpev : lev;
+    Dot3 acc[G][3];
     const uint64_t r0 = blk * rows_per_block;
     uint64_t r1 = r0 + rows_per_block;
     if (r1 > n) r1 = n;
-    for (uint64_t k = r0 + threadIdx.x; k < r1; k += EV_THREADS) {
-        gl3 l = ld3(L + k, l_ld);
-        const uint64_t row = k << eb;
-        if (en.dim == 1)
-            acc = gl3_add(acc, gl3_mul1(l, en.col[row]));
-        else
-            acc = gl3_add(acc, gl3_mul(l, ld3(en.col + row, en.ld)));
+    for (uint64_t k0 = r0 + threadIdx.x; k0 < r1; k0 += (uint64_t)EV_THREADS * U) {
+        gl3 c[U];
+        uint64_t a[U][G];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t k = k0 + (uint64_t)u * EV_THREADS;
+            const bool in = k < r1;  // out of range: zero terms (still within the 240-term bound)
+            c[u] = in ? ld3(L + k, l_ld) : gl3{{0, 0, 0}};
+#pragma unroll
+            for (int e = 0; e < G; e++) a[u][e] = (in && g.col[e]) ? g.col[e][k << eb] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            uint32_t cl[3][6];
+#pragma unroll
+            for (int j = 0; j < 3; j++) Dot3::limbs(c[u].v[j], cl[j]);
+#pragma unroll
+            for (int e = 0; e < G; e++) {
+#pragma unroll
+                for (int j = 0; j < 3; j++) acc[e][j].term(a[u][e], cl[j]);
+            }
+        }
     }
-    sh[threadIdx.x] = acc;
-    __syncthreads();
-    for (int off = EV_THREADS / 2; off > 0; off >>= 1) {
-        if (threadIdx.x < off) sh[threadIdx.x] = gl3_add(sh[threadIdx.x], sh[threadIdx.x + off]);
+#pragma unroll
+    for (int e = 0; e < G; e++) {
+        if (!g.col[e]) break;
+        sh[threadIdx.x] = gl3{{acc[e][0].fin(), acc[e][1].fin(), acc[e][2].fin()}};
         __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        uint64_t *o = partial + 3 * ((uint64_t)e * gridDim.y + blk);
-        o[0] = sh[0].v[0];
-        o[1] = sh[0].v[1];
-        o[2] = sh[0].v[2];
+        for (int off = EV_THREADS / 2; off > 0; off >>= 1) {
+            if (threadIdx.x < off) sh[threadIdx.x] = gl3_add(sh[threadIdx.x], sh[threadIdx.x + off]);
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            uint64_t *o = partial + 3 * ((uint64_t)(g.sub0 + e) * gridDim.y + blk);
+            o[0] = sh[0].v[0];
+            o[1] = sh[0].v[1];
+            o[2] = sh[0].v[2];
+        }
+        __syncthreads();
     }
 }
 
-__global__ void k_evmap_sum(uint64_t *evals, const uint64_t *partial, uint32_t n_ev, uint32_t nblk)
+// evals[e] = sum_j X^j * (sum over blocks of sub-entry j's partials); subs: 3 per entry, -1 = none
+__global__ void k_evmap_sum_subs(uint64_t *evals, const uint64_t *partial, const int32_t *subs, uint32_t n_ev,
+                                 uint32_t nblk)
 {
     uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n_ev) return;
     gl3 acc{{0, 0, 0}};
-    for (uint32_t b = 0; b < nblk; b++) {
-        const uint64_t *p = partial + 3 * ((uint64_t)e * nblk + b);
-        acc = gl3_add(acc, gl3{{p[0], p[1], p[2]}});
+    for (int j = 2; j >= 0; j--) {  // Horner in X; x^3 = x + 1: (a0 + a1 x + a2 x^2) x = a2 + (a0 + a2) x + a1 x^2
+        acc = gl3{{acc.v[2], gl_add(acc.v[0], acc.v[2]), acc.v[1]}};
+        const int32_t sub = subs[3 * e + j];
+        if (sub < 0) continue;
+        for (uint32_t b = 0; b < nblk; b++) {
+            const uint64_t *p = partial + 3 * ((uint64_t)sub * nblk + b);
+            acc = gl3_add(acc, gl3{{p[0], p[1], p[2]}});
+        }
     }
     acc = gl3_canon(acc);
     evals[3 * e] = acc.v[0];
@@ -504,6 +538,22 @@ __global__ void k_ext_powers(uint64_t *out, uint64_t ld, gl3 base, uint64_t n, u
     for (uint32_t j = 0; j < per_thread && k0 + j < n; j++) {
         st3(out + k0 + j, ld, r);
         r = gl3_mul(r, base);
+    }
+}
+
+// cols[c][k] *= base^k, k < n: thread t owns rows t + j*T (coalesced), its
+// factor starts at base^t and steps by base^T
+__global__ void k_scale_powers(uint64_t *cols, uint64_t ld, uint32_t ncols, uint64_t n, uint64_t base, uint64_t base_t,
+                               uint32_t per)
+{
+    const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t f = gl_pow(base, t);
+    for (uint32_t j = 0; j < per; j++) {
+        const uint64_t k = t + (uint64_t)j * T;
+        if (k >= n) break;
+        for (uint32_t c = 0; c < ncols; c++) cols[(uint64_t)c * ld + k] = gl_canon(gl_mul(cols[(uint64_t)c * ld + k], f));
+        f = gl_mul(f, base_t);
     }
 }
 
@@ -588,20 +638,35 @@ int calculate_z(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld
     return check_launch("calculateZ");
 }
 
-int evmap(uint64_t *evals, const void *ents_dev, uint32_t n_ev, const uint64_t *lev, const uint64_t *lpev,
-          uint64_t l_ld, uint64_t n, uint32_t eb, uint64_t *partial, uint32_t nchunks, hipStream_t s)
+size_t evmap_group_size() { return sizeof(EvGroup); }
+uint32_t evmap_group_width() { return EV_G; }
+uint64_t evmap_rows_per_block() { return EV_ROWS_PER_THREAD * EV_THREADS; }
+
+int evmap_groups(uint64_t *evals, const void *groups_dev, uint32_t n_groups, uint32_t width, uint32_t unroll,
+                 const int32_t *subs_dev,
+                 uint32_t n_ev, uint32_t n_sub, const uint64_t *lev, const uint64_t *lpev, uint64_t l_ld, uint64_t n,
+                 uint32_t eb, uint64_t *partial, hipStream_t s)
 {
     if (!n_ev) return 0;
-    uint64_t rows_per_block = (n + nchunks - 1) / nchunks;
+    const uint64_t rpb = evmap_rows_per_block();
+    const uint32_t nblk_ = (uint32_t)((n + rpb - 1) / rpb);
+    const EvGroup *g = (const EvGroup *)groups_dev;
+    const dim3 grid(n_groups, nblk_);
     prof_begin(s);
-    hipLaunchKernelGGL(k_evmap, dim3(n_ev, nchunks), dim3(EV_THREADS), 0, s, partial, (const EvEntry *)ents_dev, n_ev,
-                       lev, lpev, l_ld, n, eb, rows_per_block);
-    prof_end("k_evmap", 8.0 * n * n_ev * 2.0 + 24.0 * n * 2, s);
-    hipLaunchKernelGGL(k_evmap_sum, dim3(nblk(n_ev, 64)), dim3(64), 0, s, evals, partial, n_ev, nchunks);
-    return check_launch("k_evmap");
+#define EVG(G_, U_)                                                                                                  \
+    case G_ * 16 + U_:                                                                                                 \
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_evmap_groups<G_, U_>), grid, dim3(EV_THREADS), 0, s, partial, g, lev,      \
+                           lpev, l_ld, n, eb, rpb);                                                                    \
+        break;
+    switch (width * 16 + unroll) {
+        EVG(1, 1) EVG(1, 2) EVG(1, 4) EVG(2, 1) EVG(2, 2) EVG(2, 4) EVG(4, 1) EVG(4, 2) EVG(4, 4)
+    default: return set_error(ZKGPU_ERR_ARG, "evmap group width %u unroll %u", width, unroll);
+    }
+#undef EVG
+    prof_end("k_evmap", 8.0 * n * n_sub + 24.0 * n * 2, s);
+    hipLaunchKernelGGL(k_evmap_sum_subs, dim3(nblk(n_ev, 64)), dim3(64), 0, s, evals, partial, subs_dev, n_ev, nblk_);
+    return check_launch("k_evmap_groups");
 }
-
-size_t evmap_entry_size() { return sizeof(EvEntry); }
 
 int xdivxsub(uint64_t *xdiv, uint64_t *xdivw, const uint64_t xi[3], uint64_t w, uint32_t logn, hipStream_t s)
 {
@@ -624,6 +689,17 @@ int ext_powers(uint64_t *out, uint64_t ld, const uint64_t base[3], uint64_t n, h
     uint64_t threads = (n + per - 1) / per;
     hipLaunchKernelGGL(k_ext_powers, dim3(nblk(threads, 256)), dim3(256), 0, s, out, ld, b, n, per);
     return check_launch("k_ext_powers");
+}
+
+int scale_powers(uint64_t *cols, uint64_t ld, uint32_t ncols, uint64_t n, uint64_t base, hipStream_t s)
+{
+    const uint32_t per = 64;
+    const uint64_t threads = (n + per - 1) / per;
+    const uint32_t blocks = nblk(threads, 256);
+    const uint64_t T = (uint64_t)blocks * 256;
+    hipLaunchKernelGGL(k_scale_powers, dim3(blocks), dim3(256), 0, s, cols, ld, ncols, n, base % ZK_P,
+                       h_pow(base, T), per);
+    return check_launch("k_scale_powers");
 }
 
 int qsplit(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t qdeg,

@@ -163,11 +163,16 @@ int rand_cols(uint64_t *base, uint64_t ld, const uint32_t *cols_dev, uint32_t nc
 int zxp_eval(const ZxpLaunch &L, hipStream_t s);
 int calculate_z(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,
                 uint64_t den_ld, uint64_t n, uint64_t *scratch, uint32_t *ok_dev, hipStream_t s);
-int evmap(uint64_t *evals, const void *ents_dev, uint32_t n_ev, const uint64_t *lev, const uint64_t *lpev,
-          uint64_t l_ld, uint64_t n, uint32_t eb, uint64_t *partial, uint32_t nchunks, hipStream_t s);
-size_t evmap_entry_size();
+size_t evmap_group_size();
+uint32_t evmap_group_width();
+uint64_t evmap_rows_per_block();
+int evmap_groups(uint64_t *evals, const void *groups_dev, uint32_t n_groups, uint32_t width, uint32_t unroll,
+                 const int32_t *subs_dev,
+                 uint32_t n_ev, uint32_t n_sub, const uint64_t *lev, const uint64_t *lpev, uint64_t l_ld, uint64_t n, uint32_t eb,
+                 uint64_t *partial, hipStream_t s);
 int xdivxsub(uint64_t *xdiv, uint64_t *xdivw, const uint64_t xi[3], uint64_t w, uint32_t logn, hipStream_t s);
 int ext_powers(uint64_t *out, uint64_t ld, const uint64_t base[3], uint64_t n, hipStream_t s);
+int scale_powers(uint64_t *cols, uint64_t ld, uint32_t ncols, uint64_t n, uint64_t base, hipStream_t s);
 int qsplit(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t qdeg,
            uint64_t shift_in, hipStream_t s);
 int cols3_to_interleaved(uint64_t *out, const uint64_t *cols, uint64_t ld, uint64_t n, hipStream_t s);

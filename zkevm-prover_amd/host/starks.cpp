@@ -161,7 +161,7 @@ public:
     std::vector<void *> allocs;
     uint64_t *nodes[4] = {nullptr, nullptr, nullptr, nullptr};
     uint64_t *const_nodes = nullptr;
-    uint64_t *qq1 = nullptr, *qq2 = nullptr, *lev = nullptr, *lpev = nullptr, *xdiv = nullptr, *xdivw = nullptr;
+    uint64_t *qq1 = nullptr, *qq2 = nullptr, *cm4_n = nullptr, *lev = nullptr, *lpev = nullptr, *xdiv = nullptr, *xdivw = nullptr;
     uint64_t *fri_pol[2] = {nullptr, nullptr};
     std::vector<uint64_t *> fri_aux, fri_nodes;
     uint64_t verkey[4];
@@ -236,7 +236,8 @@ public:
         uint64_t tn = zkgpu_gl_merkle_num_elements(NE);
         for (int t = 0; t < 4; t++)
             if (dalloc(&nodes[t], tn)) return -1;
-        if (dalloc(&const_nodes, tn) || dalloc(&qq1, 3 * NE) || dalloc(&qq2, 6 * NE) || dalloc(&lev, 3 * N) ||
+        if (dalloc(&const_nodes, tn) || dalloc(&qq1, 3 * NE) || dalloc(&qq2, 6 * NE) ||
+            dalloc(&cm4_n, (uint64_t)(info.n_cm4 ? info.n_cm4 : 1) * N) || dalloc(&lev, 3 * N) ||
             dalloc(&lpev, 3 * N) || dalloc(&xdiv, 3 * NE) || dalloc(&xdivw, 3 * NE) || dalloc(&fri_pol[0], 3 * NE) ||
             dalloc(&fri_pol[1], 3 * NE))
             return -1;
@@ -402,6 +403,13 @@ public:
         uint64_t shift_in = pw(inv(7), N);
         CK(zkgpu_qsplit_dev(qq2, NE, qq1, NE, N, info.q_deg, shift_in));
         CK(zkgpu_gl_ntt_dev(S.sec[SEC_CM4_2NS], NE, qq2, NE, NE, info.n_cm4, 0));
+        // the quotient pieces on the n-domain too (for evmap below): qq2 holds
+        // coset-scaled coefficients c_k 7^k (k < N, the rest zero); plain
+        // coefficients c_k = qq2_k 7^-k, then NTT_N -> q_p(w_N^j)
+        for (uint32_t c = 0; c < info.n_cm4; c++)
+            CK(zkgpu_memcpy_d2d(cm4_n + (uint64_t)c * N, qq2 + (uint64_t)c * NE, N * 8));
+        CK(zkgpu_scale_by_powers_dev(cm4_n, N, info.n_cm4, N, inv(7)));
+        CK(zkgpu_gl_ntt_dev(cm4_n, N, cm4_n, N, N, info.n_cm4, 0));
         if (tstop("STARK_STEP_4_CALCULATE_EXPS_2NS_INTT_NTT")) return -1;
         tstart();
         CK(zkgpu_gl_merkletree_dev(nodes[3], S.sec[SEC_CM4_2NS], NE, info.n_cm4, NE));
@@ -412,11 +420,18 @@ public:
         tstart();
         uint64_t *xi = ch + 21;
         tr.get_field(xi);
-        uint64_t i7 = inv(7), wN = w_of(info.n_bits);
+        // Starks::evmap (starks.cpp:308-333,556-669) interpolates every
+        // polynomial from its extension rows k << eb, the coset points
+        // 7 w_N^k, with L = INTT((xi/7)^i).  The same values pol(xi) come
+        // from the n-domain rows (points w_N^k) with L = INTT(xi^i): the
+        // polynomial of degree < N is the same, the field sums are exact, and
+        // contiguous n-domain columns read half the lines of the strided
+        // extension rows.
+        uint64_t wN = w_of(info.n_bits);
         uint64_t xis[3], wxis[3];
         for (int k = 0; k < 3; k++) {
-            xis[k] = mul(xi[k], i7);
-            wxis[k] = mul(mul(xi[k], wN), i7);
+            xis[k] = xi[k] % P;
+            wxis[k] = mul(xi[k], wN);
         }
         CK(zkgpu_ext_powers_dev(lev, N, xis, N));
         CK(zkgpu_ext_powers_dev(lpev, N, wxis, N));
@@ -429,13 +444,18 @@ public:
             std::vector<uint64_t> lds(info.n_ev);
             std::vector<uint32_t> dims(info.n_ev), primes(info.n_ev);
             for (uint32_t e = 0; e < info.n_ev; e++) {
-                cols[e] = S.sec[ev[4 * e]] + (uint64_t)ev[4 * e + 1] * S.ld[ev[4 * e]];
-                lds[e] = S.ld[ev[4 * e]];
+                const uint32_t sec = ev[4 * e];
+                const uint64_t *base = sec == SEC_CM4_2NS ? cm4_n
+                                       : sec == SEC_CONST_2NS ? S.sec[SEC_CONST_N]
+                                                              : S.sec[sec - SEC_CM1_2NS + SEC_CM1_N];
+                if (sec < SEC_CM1_2NS || sec > SEC_CONST_2NS) return fail("evMap entry %u: section %u", e, sec);
+                cols[e] = base + (uint64_t)ev[4 * e + 1] * N;
+                lds[e] = N;
                 dims[e] = ev[4 * e + 2];
                 primes[e] = ev[4 * e + 3];
             }
             CK(zkgpu_evmap_dev(evals.data(), cols.data(), lds.data(), dims.data(), primes.data(), info.n_ev, lev, lpev,
-                               N, N, eb));
+                               N, N, 0));
         }
         if (tstop("STARK_STEP_5_EVMAP")) return -1;
         tr.put(evals.data(), evals.size());

@@ -81,6 +81,7 @@ _SIGS = {
     "zkgpu_xdivxsub_dev": (ctypes.c_int, [vp, vp, vp, u32, u32]),
     "zkgpu_ext_powers_dev": (ctypes.c_int, [vp, u64, vp, u64]),
     "zkgpu_qsplit_dev": (ctypes.c_int, [vp, u64, vp, u64, u64, u32, u64]),
+    "zkgpu_scale_by_powers_dev": (ctypes.c_int, [vp, u64, u32, u64, u64]),
     "zkgpu_cols3_to_interleaved_dev": (ctypes.c_int, [vp, vp, u64, u64]),
     "zkgpu_h1h2_dev": (ctypes.c_int, [vp, u64, vp, u64, vp, u64, vp, u64, u64, u32, pu64]),
     "zkgpu_gl_merkle_open_rows_dev": (ctypes.c_int, [vp, vp, vp, vp, u64, u64, vp, u64]),
