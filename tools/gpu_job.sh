@@ -109,6 +109,21 @@ for step in "$@"; do
         cd "$GRAFT_REPO_ROOT"
         ok_or_stop $rc "rocprofv3 pmc SQ_INSTS_VALU"
         ;;
+    starkpmc)
+        # 2^23 STARK proof: HBM traffic (separate FETCH / WRITE passes) and VALU issue per kernel
+        for pass in "FETCH_SIZE:pmc_sfetch" "WRITE_SIZE:pmc_swrite" \
+                    "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE:pmc_ssq"; do
+            ctr=${pass%%:*}
+            out=${pass##*:}
+            cd /tmp
+            timeout -k 10 400 rocprofv3 --pmc $ctr --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/$out" -o run \
+                --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --workload stark --no-cpu --steps 1 --warmup 0 \
+                > /dev/null 2> "$GRAFT_REPO_ROOT/gpurun_out/$out.err"
+            rc=$?
+            cd "$GRAFT_REPO_ROOT"
+            ok_or_stop $rc "rocprofv3 stark pmc $out"
+        done
+        ;;
     zxpsweep)
         for r in 1 2 4; do
             ZKGPU_ZXP_ROWS=$r timeout -k 10 300 python bench.py --workload stark --steps 2 --warmup 1 --no-cpu \
@@ -128,12 +143,13 @@ for step in "$@"; do
         cat gpurun_out/bench_stark_sharded.json
         ;;
     jitsweep)
-        for cfg in "8 0" "1000 0" "8 4" "4 0"; do
+        # KLDS OPT WAVES
+        for cfg in "0 1 0" "1 1 0" "1 2 0" "1 2 4" "1 2 3" "0 2 0"; do
             set -- $cfg
-            ZKGPU_ZXP_JIT_DOTLOOP=$1 ZKGPU_ZXP_JIT_WAVES=$2 timeout -k 10 300 python bench.py --workload stark --steps 2 --warmup 1 --no-cpu \
-                > gpurun_out/jit_$1_$2.json 2>> gpurun_out/jit_sweep.err
-            ok_or_stop $? "stark jit loop=$1 waves=$2"
-            echo "loop=$1 waves=$2 $(python -c "import json;d=json.load(open('gpurun_out/jit_$1_$2.json'));s=d['stages_ms'];print(d['ms_per_step'],'ms q',s['STARK_STEP_4_CALCULATE_EXPS_2NS'],'f',s['STARK_STEP_5_CALCULATE_EXPS'],'s2',s['STARK_STEP_2_CALCULATE_EXPS'],'s3',s['STARK_STEP_3_CALCULATE_EXPS'])")"
+            ZKGPU_ZXP_JIT_KLDS=$1 ZKGPU_ZXP_JIT_OPT=$2 ZKGPU_ZXP_JIT_WAVES=$3 timeout -k 10 300 python bench.py --workload stark --steps 2 --warmup 1 --no-cpu \
+                > gpurun_out/jit_$1_$2_$3.json 2>> gpurun_out/jit_sweep.err
+            ok_or_stop $? "stark jit klds=$1 opt=$2 waves=$3"
+            echo "klds=$1 opt=$2 waves=$3 $(python -c "import json;d=json.load(open('gpurun_out/jit_$1_$2_$3.json'));s=d['stages_ms'];print(d['ms_per_step'],'ms q',s['STARK_STEP_4_CALCULATE_EXPS_2NS'],'f',s['STARK_STEP_5_CALCULATE_EXPS'],'s2',s['STARK_STEP_2_CALCULATE_EXPS'],'s3',s['STARK_STEP_3_CALCULATE_EXPS'])")"
         done
         ;;
     evsweep)

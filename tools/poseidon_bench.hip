@@ -48,6 +48,24 @@ __device__ __forceinline__ void full_rounds_fold_v1(uint64_t st[12], int r0)
     }
 }
 
+// integer multiply-add MDS (mds_fold, 438 VALU) instead of the frequency-domain form
+__device__ __forceinline__ void perm_fast_fold(uint64_t st[12])
+{
+#pragma unroll
+    for (int s = 0; s < 12; s++) st[s] = gl_add(st[s], ZKGPU_POSEIDON_RC[s]);
+    for (int h = 0; h < 2; h++) {
+        if (h) partial_rounds_blocks(st);
+        const int r0 = h ? 26 : 0;
+#pragma unroll 1
+        for (int r = r0; r < r0 + 4; r++) {
+#pragma unroll
+            for (int s = 0; s < 12; s++) st[s] = pow7(st[s]);
+            const uint64_t *K = r == 3 ? ZKGPU_PSP_PRE : (r == 29 ? ZKGPU_PS_ZERO12 : &ZKGPU_POSEIDON_RC[(r + 1) * 12]);
+            mds_fold(st, K);
+        }
+    }
+}
+
 __device__ __forceinline__ void perm_fast_v1(uint64_t st[12])
 {
 #pragma unroll
@@ -71,7 +89,8 @@ __global__ void __launch_bounds__(256) k_perm(uint64_t *st_all, uint64_t n, int 
         if constexpr (V == 2) perm_sparse<false>(st);
         if constexpr (V == 3) perm_sparse<true>(st);
         if constexpr (V == 4) perm_fast(st);
-        if constexpr (V == 5) perm_fast_v1(st);
+        if constexpr (V == 5) perm_fast_fold(st);
+        if constexpr (V == 6) perm_fast_v1(st);
     }
 #pragma unroll
     for (int k = 0; k < 12; k++) st_all[k * n + i] = gl_canon(st[k]);
@@ -98,11 +117,12 @@ int main()
         {"textbook/limbs24", k_perm<1>},
         {"sparse/halves", k_perm<2>},
         {"sparse/limbs24", k_perm<3>},
-        {"fast (folded MDS + block dots)", k_perm<4>},
-        {"fast, previous MDS form", k_perm<5>},
+        {"fast (FFT MDS + block dots)", k_perm<4>},
+        {"fast, multiply-add MDS (mds_fold)", k_perm<5>},
+        {"fast, older MDS form", k_perm<6>},
     };
     int bad = 0;
-    for (int v = 0; v < 6; v++) {
+    for (int v = 0; v < 7; v++) {
         float best = 1e30f;
         for (int rep = 0; rep < 3; rep++) {
             (void)hipMemcpy(d, h, 12 * n * 8, hipMemcpyHostToDevice);

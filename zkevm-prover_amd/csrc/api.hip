@@ -1058,11 +1058,10 @@ int zkgpu_calculate_z_dev(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint6
     int rc;
     if ((rc = require_init())) return rc;
     if (!n) return 0;
-    const uint64_t chunk = 256 * 16;
-    uint64_t nb = (n + chunk - 1) / chunk;
-    uint64_t *scr = workspace(2, (3 * n + 6 * nb + 8) * sizeof(uint64_t));
+    const size_t words = calculate_z_scratch_words(n);
+    uint64_t *scr = workspace(2, (words + 8) * sizeof(uint64_t));
     if (!scr) return ZKGPU_ERR_OOM;
-    uint32_t *ok = (uint32_t *)(scr + 3 * n + 6 * nb);
+    uint32_t *ok = (uint32_t *)(scr + words);
     if ((rc = calculate_z(z, z_ld, num, num_ld, den, den_ld, n, scr, ok, g_ctx.stream))) return rc;
     uint32_t okh = 0;
     if ((rc = check_hip(hipMemcpyAsync(&okh, ok, 4, hipMemcpyDeviceToHost, g_ctx.stream), "D2H"))) return rc;

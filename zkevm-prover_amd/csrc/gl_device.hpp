@@ -32,6 +32,14 @@ using __hip_internal::int32_t;
 
 namespace zk {
 
+// Accesses through a pointer that was itself read from memory (column tables,
+// term records): the compiler cannot infer the global address space there and
+// emits FLAT instructions, which also count against LGKM_CNT -- every
+// s_waitcnt for a scalar constant load would then wait for them as well.
+typedef __attribute__((address_space(1))) uint64_t gu64_t;
+__device__ __forceinline__ uint64_t gload(const uint64_t *p) { return *(const gu64_t *)p; }
+__device__ __forceinline__ void gstore(uint64_t *p, uint64_t v) { *(gu64_t *)p = v; }
+
 // any u64 -> [0, p)   (x < 2^64 < 2p, so one conditional subtraction)
 __device__ __forceinline__ uint64_t gl_canon(uint64_t a) { return a >= ZK_P ? a - ZK_P : a; }
 
@@ -177,6 +185,13 @@ __device__ __forceinline__ gl3 gl3_rsub1(uint64_t a, const gl3 &b)
 // a = a0 + a1*2^32 contributes a0*c_k + a1*c'_k to accumulator k (weights
 // 2^0, 2^22, 2^43): six carry-free 32x32->64 multiply-adds per term, each
 // term adding < 2^55 (< 2^61 for <= 34 terms, < 2^63 for <= 250).
+struct alignas(16) LimbQ {
+    uint32_t x, y, z, w;
+};
+struct alignas(8) LimbP {
+    uint32_t x, y;
+};
+
 struct Dot3 {
     uint64_t A0, A1, A2;
     __device__ __forceinline__ explicit Dot3(const uint32_t *k) : A0(k[0]), A1(k[1]), A2(k[2]) {}
@@ -201,6 +216,19 @@ struct Dot3 {
         A0 += (uint64_t)a1 * c[3];
         A1 += (uint64_t)a1 * c[4];
         A2 += (uint64_t)a1 * c[5];
+    }
+    // the same from a 16-byte aligned limb slot (one 16-byte + one 8-byte load)
+    __device__ __forceinline__ void term_al(uint64_t a, const uint32_t *c)
+    {
+        const LimbQ q = *(const LimbQ *)c;
+        const LimbP r = *(const LimbP *)(c + 4);
+        const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);
+        A0 += (uint64_t)a0 * q.x;
+        A1 += (uint64_t)a0 * q.y;
+        A2 += (uint64_t)a0 * q.z;
+        A0 += (uint64_t)a1 * q.w;
+        A1 += (uint64_t)a1 * r.x;
+        A2 += (uint64_t)a1 * r.y;
     }
     // coefficient 1: a0 -> A0, a1 * 2^32 = a1 * 2^10 * 2^22 -> A1
     __device__ __forceinline__ void lane(uint64_t a)

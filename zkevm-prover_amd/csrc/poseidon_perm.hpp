@@ -277,6 +277,73 @@ __device__ __forceinline__ void mds_fold(uint64_t st[12], const uint64_t *K)
     }
 }
 
+// Circulant part of the MDS on 32-bit halves, in the frequency domain
+// (tools/mds_fft.py checks the algebra): Good-Thomas maps the length-12 cyclic
+// convolution y = r * v (r_k = MCIRC[-k]) onto 4 x 3, n = (9a + 4b) mod 12.
+// Along a, X^4 - 1 = (X - 1)(X + 1)(X^2 + 1); along b, 3-point cyclic
+// convolutions with the transformed kernel, which for this matrix is all
+// signed powers of two once the inverse's 1/4 and 1/2 are folded in:
+//   (X - 1): [16, 32, 16]   (X + 1): [-1, 8, 2]   (X^2 + 1): [2 - i, -1 - 4i, -16 - i]
+// so every product is a shift.  Wrapping u64 arithmetic is exact: the
+// outputs are the (non-negative, < 2^41) integer row sums.
+__device__ __forceinline__ void mds_circ_fft(const uint64_t v[12], uint64_t w[12])
+{
+    uint64_t u0[3], u1[3], p[3], q[3];
+#pragma unroll
+    for (int b = 0; b < 3; b++) {
+        const uint64_t S0 = v[(4 * b) % 12], S1 = v[(9 + 4 * b) % 12], S2 = v[(18 + 4 * b) % 12],
+                       S3 = v[(27 + 4 * b) % 12];
+        const uint64_t t0 = S0 + S2, t1 = S1 + S3;
+        u0[b] = t0 + t1;
+        u1[b] = t0 - t1;
+        p[b] = S0 - S2;
+        q[b] = S1 - S3;
+    }
+    const uint64_t s0 = u0[0] + u0[1] + u0[2];
+#pragma unroll
+    for (int b = 0; b < 3; b++) {
+        const int b1 = (b + 2) % 3, b2 = (b + 1) % 3;  // b - 1, b - 2
+        const uint64_t V0 = (s0 + u0[b1]) << 4;
+        const uint64_t V1 = (u1[b1] << 3) + (u1[b2] << 1) - u1[b];
+        const uint64_t re = (p[b] << 1) + q[b] + (q[b1] << 2) + q[b2] - p[b1] - (p[b2] << 4);
+        const uint64_t im = (q[b] << 1) - p[b] - q[b1] - (p[b1] << 2) - (q[b2] << 4) - p[b2];
+        const uint64_t A = V0 + V1, B = V0 - V1;
+        w[(4 * b) % 12] = A + re;
+        w[(18 + 4 * b) % 12] = A - re;
+        w[(9 + 4 * b) % 12] = B + im;
+        w[(27 + 4 * b) % 12] = B - im;
+    }
+}
+
+// st = M * st + K with the circulant part from mds_circ_fft (same result as
+// mds_fold, bit for bit)
+__device__ __forceinline__ void mds_fft_fold(uint64_t st[12], const uint64_t *K)
+{
+    uint64_t lo[12], hi[12], wl[12], wh[12];
+#pragma unroll
+    for (int y = 0; y < 12; y++) {
+        lo[y] = (uint32_t)st[y];
+        hi[y] = st[y] >> 32;
+    }
+    mds_circ_fft(lo, wl);
+    mds_circ_fft(hi, wh);
+    wl[0] += lo[0] << 3;  // MDIAG[0] = 8
+    wh[0] += hi[0] << 3;
+#pragma unroll
+    for (int x = 0; x < 12; x++) {
+        const uint64_t sl = wl[x] + (uint32_t)K[x], sh = wh[x] + (K[x] >> 32);
+        // value = sl + sh * 2^32 < 2^75: (h : mid : sl0)
+        uint32_t c1, c2;
+        const uint32_t mid = __builtin_addc((uint32_t)(sl >> 32), (uint32_t)sh, 0u, &c1);
+        const uint32_t h = __builtin_addc((uint32_t)(sh >> 32), 0u, c1, &c2);
+        st[x] = gl_reduce96(((uint64_t)mid << 32) | (uint32_t)sl, h);
+    }
+}
+
+#ifndef ZKGPU_MDS_FFT
+#define ZKGPU_MDS_FFT 1
+#endif
+
 // Dot3 (table-coefficient dot products): csrc/gl_device.hpp
 
 static constexpr uint64_t ZKGPU_PS_ZERO12[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -288,7 +355,10 @@ __device__ __forceinline__ void full_rounds_fold(uint64_t st[12], int r0)
 #pragma unroll
         for (int s = 0; s < 12; s++) st[s] = pow7(st[s]);
         const uint64_t *K = r == 3 ? ZKGPU_PSP_PRE : (r == 29 ? ZKGPU_PS_ZERO12 : &ZKGPU_POSEIDON_RC[(r + 1) * 12]);
-        mds_fold(st, K);
+        if constexpr (ZKGPU_MDS_FFT)
+            mds_fft_fold(st, K);
+        else
+            mds_fold(st, K);
     }
 }
 

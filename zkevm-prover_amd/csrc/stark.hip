@@ -129,10 +129,10 @@ __device__ __forceinline__ Val zxp_load(const ZxpEnv &e, uint32_t kind, const ui
         r.dim = 3;
         break;
     }
-    case DK_C1: r.v.v[0] = ptr[(i + (uint64_t)(int64_t)ii) & e.rmask]; break;
+    case DK_C1: r.v.v[0] = gload(ptr + ((i + (uint64_t)(int64_t)ii) & e.rmask)); break;
     case DK_C3: {
         const uint64_t *p = ptr + ((i + (uint64_t)(int64_t)ii) & e.rmask);
-        r.v = gl3{{p[0], p[ld], p[2 * (uint64_t)ld]}};
+        r.v = gl3{{gload(p), gload(p + ld), gload(p + 2 * (uint64_t)ld)}};
         r.dim = 3;
         break;
     }
@@ -143,8 +143,8 @@ __device__ __forceinline__ Val zxp_load(const ZxpEnv &e, uint32_t kind, const ui
         r.v.v[0] = gl_mul(e.x_start, gl_mul(e.tw_lo[ex & (TW_LEVEL_SIZE - 1)], e.tw_hi[ex >> TW_LEVEL_BITS]));
         break;
     }
-    case DK_I3: r.v = gl3{{ptr[3 * i], ptr[3 * i + 1], ptr[3 * i + 2]}}; r.dim = 3; break;
-    case DK_ZI: r.v.v[0] = ptr[i & (uint32_t)ii]; break;
+    case DK_I3: r.v = gl3{{gload(ptr + 3 * i), gload(ptr + 3 * i + 1), gload(ptr + 3 * i + 2)}}; r.dim = 3; break;
+    case DK_ZI: r.v.v[0] = gload(ptr + (i & (uint32_t)ii)); break;
     default: break;
     }
     return r;
@@ -250,45 +250,22 @@ __global__ void __launch_bounds__(ZXP_THREADS) k_zxp_eval(ZxpEnv e)
 }
 
 // ---------------------------------------------------------------- calculateZ
-// ratio[i] = num[i] / den[i]; each thread inverts CH strided elements with one
-// F_p^3 inversion (Montgomery's trick).
-constexpr int BI_CHUNK = 16;
-
-__global__ void __launch_bounds__(256) k_ratio(uint64_t *ratio, const uint64_t *num, uint64_t num_ld,
-                                               const uint64_t *den, uint64_t den_ld, uint64_t n)
-{
-    const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    gl3 pre[BI_CHUNK];
-    gl3 acc{{1, 0, 0}};
-#pragma unroll
-    for (int j = 0; j < BI_CHUNK; j++) {
-        uint64_t k = t + j * T;
-        gl3 d = k < n ? ld3(den + k, den_ld) : gl3{{1, 0, 0}};
-        acc = j ? gl3_mul(acc, d) : d;
-        pre[j] = acc;
-    }
-    gl3 inv = gl3_inv(acc);
-#pragma unroll
-    for (int j = BI_CHUNK - 1; j >= 0; j--) {
-        uint64_t k = t + j * T;
-        gl3 dinv = j ? gl3_mul(inv, pre[j - 1]) : inv;
-        if (k < n) {
-            gl3 d = ld3(den + k, den_ld);
-            gl3 r = gl3_mul(ld3(num + k, num_ld), dinv);
-            uint64_t *o = ratio + 3 * k;
-            o[0] = r.v[0];
-            o[1] = r.v[1];
-            o[2] = r.v[2];
-            inv = gl3_mul(inv, d);
-        }
-    }
-}
-
-// scan phase 1: each block reduces its contiguous chunk of the ratio array
+// Z[k] = prod_{i<k} num[i] / den[i]  (starks.cpp:146-224, polinomial.hpp:560-607).
+// Tiles of Z_TILE = 256 x 8 rows.  Global traffic is always row-coalesced (lane
+// = consecutive row); the per-thread CONTIGUOUS runs a prefix product needs are
+// read from an LDS image of the tile.
+//   k_z_ratio:  ratio = num / den (Montgomery batch inversion over each
+//               thread's 8 strided rows), LDS image, per-thread run products,
+//               block scan -> per-thread exclusive prefixes + tile total
+//   k_z_totals: exclusive prefix of the tile totals (one workgroup)
+//   k_z_apply:  z = tile prefix * thread prefix * running product, through LDS
+constexpr int BI_CHUNK = 16;  // k_xdivxsub / k_ext: rows per thread sharing one inversion
 constexpr int SCAN_THREADS = 256;
-constexpr int SCAN_PER_THREAD = 16;
-constexpr uint64_t SCAN_CHUNK = SCAN_THREADS * SCAN_PER_THREAD;
+constexpr int Z_PER = 8;
+constexpr uint64_t Z_TILE = SCAN_THREADS * Z_PER;
+// LDS slot of tile row e: one pad slot per Z_PER rows (run reads: 2-way bank conflicts)
+__device__ __forceinline__ int z_slot(int e) { return e + e / Z_PER; }
+constexpr int Z_SLOTS = Z_TILE + Z_TILE / Z_PER;
 
 __device__ gl3 block_exclusive_scan3(gl3 v, gl3 *sh, gl3 *total)
 {
@@ -303,76 +280,125 @@ __device__ gl3 block_exclusive_scan3(gl3 v, gl3 *sh, gl3 *total)
         sh[t] = t >= off ? gl3_mul(x, y) : x;
         __syncthreads();
     }
-    gl3 incl = sh[t];
     gl3 excl = t ? sh[t - 1] : gl3{{1, 0, 0}};
     *total = sh[SCAN_THREADS - 1];
     __syncthreads();
-    (void)incl;
     return excl;
 }
 
-__global__ void __launch_bounds__(SCAN_THREADS) k_scan_reduce(uint64_t *block_tot, const uint64_t *ratio, uint64_t n)
+__device__ __forceinline__ void lds_st3(uint64_t *img, int slot, const gl3 &v)
 {
-    __shared__ gl3 sh[SCAN_THREADS];
-    const uint64_t base = (uint64_t)blockIdx.x * SCAN_CHUNK + (uint64_t)threadIdx.x * SCAN_PER_THREAD;
-    gl3 acc{{1, 0, 0}};
-    for (int j = 0; j < SCAN_PER_THREAD; j++) {
-        uint64_t k = base + j;
-        if (k < n) acc = gl3_mul(acc, gl3{{ratio[3 * k], ratio[3 * k + 1], ratio[3 * k + 2]}});
-    }
-    gl3 tot;
-    block_exclusive_scan3(acc, sh, &tot);
-    if (threadIdx.x == 0) {
-        block_tot[3 * blockIdx.x] = tot.v[0];
-        block_tot[3 * blockIdx.x + 1] = tot.v[1];
-        block_tot[3 * blockIdx.x + 2] = tot.v[2];
-    }
+    img[slot] = v.v[0];
+    img[Z_SLOTS + slot] = v.v[1];
+    img[2 * Z_SLOTS + slot] = v.v[2];
+}
+__device__ __forceinline__ gl3 lds_ld3(const uint64_t *img, int slot)
+{
+    return gl3{{img[slot], img[Z_SLOTS + slot], img[2 * Z_SLOTS + slot]}};
 }
 
-// scan phase 2: exclusive scan of the block totals (single block, sequential chunks)
-__global__ void __launch_bounds__(SCAN_THREADS) k_scan_totals(uint64_t *block_pre, const uint64_t *block_tot,
-                                                              uint64_t nblocks)
+__global__ void __launch_bounds__(SCAN_THREADS) k_z_ratio(uint64_t *ratio, uint64_t *thr_pre, uint64_t *tile_tot,
+                                                          const uint64_t *num, uint64_t num_ld, const uint64_t *den,
+                                                          uint64_t den_ld, uint64_t n)
 {
+    __shared__ uint64_t img[3 * Z_SLOTS];
     __shared__ gl3 sh[SCAN_THREADS];
-    gl3 carry{{1, 0, 0}};
-    for (uint64_t b0 = 0; b0 < nblocks; b0 += SCAN_THREADS) {
-        uint64_t b = b0 + threadIdx.x;
-        gl3 v = b < nblocks ? gl3{{block_tot[3 * b], block_tot[3 * b + 1], block_tot[3 * b + 2]}} : gl3{{1, 0, 0}};
-        gl3 tot;
-        gl3 ex = block_exclusive_scan3(v, sh, &tot);
-        if (b < nblocks) {
-            gl3 r = gl3_mul(carry, ex);
-            block_pre[3 * b] = r.v[0];
-            block_pre[3 * b + 1] = r.v[1];
-            block_pre[3 * b + 2] = r.v[2];
+    const int t = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * Z_TILE;
+    gl3 pre[Z_PER];
+    gl3 acc{{1, 0, 0}};
+#pragma unroll
+    for (int j = 0; j < Z_PER; j++) {
+        const uint64_t k = base + j * SCAN_THREADS + t;
+        const gl3 d = k < n ? ld3(den + k, den_ld) : gl3{{1, 0, 0}};
+        acc = j ? gl3_mul(acc, d) : d;
+        pre[j] = acc;
+    }
+    gl3 inv = gl3_inv(acc);
+#pragma unroll
+    for (int jj = 0; jj < Z_PER; jj++) {
+        const int j = Z_PER - 1 - jj;
+        const int e = j * SCAN_THREADS + t;
+        const uint64_t k = base + e;
+        const gl3 dinv = j ? gl3_mul(inv, pre[j - 1]) : inv;
+        gl3 r{{1, 0, 0}};
+        if (k < n) {
+            r = gl3_mul(ld3(num + k, num_ld), dinv);
+            uint64_t *o = ratio + 3 * k;
+            o[0] = r.v[0];
+            o[1] = r.v[1];
+            o[2] = r.v[2];
+            if (j) inv = gl3_mul(inv, ld3(den + k, den_ld));
         }
-        carry = gl3_mul(carry, tot);
+        lds_st3(img, z_slot(e), r);
+    }
+    __syncthreads();
+    gl3 run = lds_ld3(img, z_slot(t * Z_PER));
+#pragma unroll
+    for (int i = 1; i < Z_PER; i++) run = gl3_mul(run, lds_ld3(img, z_slot(t * Z_PER + i)));
+    gl3 tot;
+    const gl3 ex = block_exclusive_scan3(run, sh, &tot);
+    uint64_t *tp = thr_pre + 3 * ((uint64_t)blockIdx.x * SCAN_THREADS + t);
+    tp[0] = ex.v[0];
+    tp[1] = ex.v[1];
+    tp[2] = ex.v[2];
+    if (t == 0) {
+        tile_tot[3 * blockIdx.x] = tot.v[0];
+        tile_tot[3 * blockIdx.x + 1] = tot.v[1];
+        tile_tot[3 * blockIdx.x + 2] = tot.v[2];
     }
 }
 
-// scan phase 3: z[k] = block_pre * exclusive product within the block
-__global__ void __launch_bounds__(SCAN_THREADS) k_scan_apply(uint64_t *z, uint64_t z_ld, const uint64_t *ratio,
-                                                             const uint64_t *block_pre, uint64_t n)
+// exclusive prefix of the tile totals: each thread multiplies a contiguous run
+// of ceil(ntiles / 256) totals, one block scan, then the run is re-walked
+__global__ void __launch_bounds__(SCAN_THREADS) k_z_totals(uint64_t *tile_pre, const uint64_t *tile_tot,
+                                                           uint64_t ntiles)
 {
     __shared__ gl3 sh[SCAN_THREADS];
-    const uint64_t base = (uint64_t)blockIdx.x * SCAN_CHUNK + (uint64_t)threadIdx.x * SCAN_PER_THREAD;
+    const uint64_t per = (ntiles + SCAN_THREADS - 1) / SCAN_THREADS;
+    const uint64_t b0 = threadIdx.x * per;
+    uint64_t b1 = b0 + per;
+    if (b1 > ntiles) b1 = ntiles;
     gl3 acc{{1, 0, 0}};
-    gl3 loc[SCAN_PER_THREAD];
-#pragma unroll
-    for (int j = 0; j < SCAN_PER_THREAD; j++) {
-        uint64_t k = base + j;
-        loc[j] = k < n ? gl3{{ratio[3 * k], ratio[3 * k + 1], ratio[3 * k + 2]}} : gl3{{1, 0, 0}};
-        acc = gl3_mul(acc, loc[j]);
-    }
+    for (uint64_t b = b0; b < b1; b++) acc = gl3_mul(acc, ld3(tile_tot + 3 * b, 1));
     gl3 tot;
-    gl3 ex = block_exclusive_scan3(acc, sh, &tot);
-    gl3 run = gl3_mul(gl3{{block_pre[3 * blockIdx.x], block_pre[3 * blockIdx.x + 1], block_pre[3 * blockIdx.x + 2]}},
-                      ex);
+    gl3 run = block_exclusive_scan3(acc, sh, &tot);
+    for (uint64_t b = b0; b < b1; b++) {
+        tile_pre[3 * b] = run.v[0];
+        tile_pre[3 * b + 1] = run.v[1];
+        tile_pre[3 * b + 2] = run.v[2];
+        run = gl3_mul(run, ld3(tile_tot + 3 * b, 1));
+    }
+}
+
+__global__ void __launch_bounds__(SCAN_THREADS) k_z_apply(uint64_t *z, uint64_t z_ld, const uint64_t *ratio,
+                                                          const uint64_t *thr_pre, const uint64_t *tile_pre,
+                                                          uint64_t n)
+{
+    __shared__ uint64_t img[3 * Z_SLOTS];
+    const int t = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * Z_TILE;
 #pragma unroll
-    for (int j = 0; j < SCAN_PER_THREAD; j++) {
-        uint64_t k = base + j;
-        if (k < n) st3(z + k, z_ld, run);  // exclusive: z[k] = prod_{i<k} ratio[i]
-        run = gl3_mul(run, loc[j]);
+    for (int j = 0; j < Z_PER; j++) {
+        const int e = j * SCAN_THREADS + t;
+        const uint64_t k = base + e;
+        lds_st3(img, z_slot(e), k < n ? ld3(ratio + 3 * k, 1) : gl3{{1, 0, 0}});
+    }
+    gl3 run = gl3_mul(ld3(tile_pre + 3 * blockIdx.x, 1), ld3(thr_pre + 3 * ((uint64_t)blockIdx.x * SCAN_THREADS + t), 1));
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < Z_PER; i++) {  // exclusive: z[k] = prod_{i<k} ratio[i]
+        const int sl = z_slot(t * Z_PER + i);
+        const gl3 r = lds_ld3(img, sl);
+        lds_st3(img, sl, run);
+        run = gl3_mul(run, r);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < Z_PER; j++) {
+        const int e = j * SCAN_THREADS + t;
+        const uint64_t k = base + e;
+        if (k < n) st3(z + k, z_ld, lds_ld3(img, z_slot(e)));
     }
 }
 
@@ -425,7 +451,7 @@ __global__ void __launch_bounds__(EV_THREADS) k_evmap_groups(uint64_t *partial, 
             const bool in = k < r1;  // out of range: zero terms (still within the 240-term bound)
             c[u] = in ? ld3(L + k, l_ld) : gl3{{0, 0, 0}};
 #pragma unroll
-            for (int e = 0; e < G; e++) a[u][e] = (in && g.col[e]) ? g.col[e][k << eb] : 0;
+            for (int e = 0; e < G; e++) a[u][e] = (in && g.col[e]) ? gload(g.col[e] + (k << eb)) : 0;
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -505,7 +531,8 @@ __global__ void __launch_bounds__(256) k_xdivxsub(uint64_t *xdiv, uint64_t *xdiv
         }
         gl3 inv = gl3_inv(acc);
 #pragma unroll
-        for (int j = BI_CHUNK - 1; j >= 0; j--) {
+        for (int jj = 0; jj < BI_CHUNK; jj++) {  // (descending j; this form unrolls, keeping pre[] in registers)
+            const int j = BI_CHUNK - 1 - jj;
             uint64_t k = t + j * T;
             gl3 dinv = j ? gl3_mul(inv, pre[j - 1]) : inv;
             if (k < n) {
@@ -616,24 +643,29 @@ int zxp_eval(const ZxpLaunch &L, hipStream_t s)
     return check_launch("k_zxp_eval");
 }
 
+size_t calculate_z_scratch_words(uint64_t n)
+{
+    const uint64_t nt = (n + Z_TILE - 1) / Z_TILE;
+    return 3 * n + 3 * nt * SCAN_THREADS + 6 * nt;
+}
+
 int calculate_z(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,
                 uint64_t den_ld, uint64_t n, uint64_t *scratch, uint32_t *ok_dev, hipStream_t s)
 {
-    // scratch: ratio (3n) + block totals + block prefixes
+    // scratch: ratio (3n) + per-thread prefixes (3 * 256 per tile) + tile totals + tile prefixes
+    const uint64_t nt = (n + Z_TILE - 1) / Z_TILE;
     uint64_t *ratio = scratch;
-    uint64_t nb = (n + SCAN_CHUNK - 1) / SCAN_CHUNK;
-    uint64_t *tot = ratio + 3 * n;
-    uint64_t *pre = tot + 3 * nb;
-    uint64_t threads = (n + BI_CHUNK - 1) / BI_CHUNK;
-    uint32_t blocks = nblk(threads, 256);
+    uint64_t *thr = ratio + 3 * n;
+    uint64_t *tot = thr + 3 * nt * SCAN_THREADS;
+    uint64_t *pre = tot + 3 * nt;
     prof_begin(s);
-    hipLaunchKernelGGL(k_ratio, dim3(blocks), dim3(256), 0, s, ratio, num, num_ld, den, den_ld, n);
-    prof_end("k_ratio", 8.0 * 9 * n, s);
-    hipLaunchKernelGGL(k_scan_reduce, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, tot, ratio, n);
-    hipLaunchKernelGGL(k_scan_totals, dim3(1), dim3(SCAN_THREADS), 0, s, pre, tot, nb);
+    hipLaunchKernelGGL(k_z_ratio, dim3((uint32_t)nt), dim3(SCAN_THREADS), 0, s, ratio, thr, tot, num, num_ld, den,
+                       den_ld, n);
+    prof_end("k_z_ratio", 8.0 * 9 * n, s);
+    hipLaunchKernelGGL(k_z_totals, dim3(1), dim3(SCAN_THREADS), 0, s, pre, tot, nt);
     prof_begin(s);
-    hipLaunchKernelGGL(k_scan_apply, dim3((uint32_t)nb), dim3(SCAN_THREADS), 0, s, z, z_ld, ratio, pre, n);
-    prof_end("k_scan_apply", 8.0 * 6 * n, s);
+    hipLaunchKernelGGL(k_z_apply, dim3((uint32_t)nt), dim3(SCAN_THREADS), 0, s, z, z_ld, ratio, thr, pre, n);
+    prof_end("k_z_apply", 8.0 * 6 * n, s);
     hipLaunchKernelGGL(k_z_check, dim3(1), dim3(1), 0, s, ok_dev, z, z_ld, ratio, n);
     return check_launch("calculateZ");
 }

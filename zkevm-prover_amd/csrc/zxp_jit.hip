@@ -57,7 +57,14 @@ struct JitParams {
     const uint64_t *xdiv, *xdivw, *zh, *tw_lo, *tw_hi;
     uint64_t x_start, rmask;
     uint32_t logdom, logomega, zmask;
+    uint32_t nkl;  // limb words staged in LDS (0: read from p.kl)
 };
+
+// DOT limb tables up to this size are staged in LDS per workgroup: read from
+// there, the straight-line terms' constants do not compete for the 106 SGPRs
+// (scalar loads of every term's limbs hoisted by the scheduler spill SGPRs
+// into VGPR lanes -- thousands of v_readlane/v_writelane per row).
+constexpr size_t JIT_KL_LDS_MAX = 48 * 1024;
 
 const char *k_kernel_head = R"(
 using namespace zk;
@@ -75,6 +82,7 @@ struct JitParams {
     const uint64_t *xdiv, *xdivw, *zh, *tw_lo, *tw_hi;
     uint64_t x_start, rmask;
     uint32_t logdom, logomega, zmask;
+    uint32_t nkl;
 };
 // long column runs of a DOT: a loop over table terms, 4 loads in flight
 template <int D>
@@ -85,7 +93,7 @@ __device__ __forceinline__ void dot_cols(Dot3 &d0, Dot3 &d1, Dot3 &d2, const Jit
     for (; k + 4 <= n; k += 4) {
         uint64_t a[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) a[u] = t[k + u].ptr[(i + (uint64_t)t[k + u].sh) & m];
+        for (int u = 0; u < 4; u++) a[u] = gload(t[k + u].ptr + ((i + (uint64_t)t[k + u].sh) & m));
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             d0.term(a[u], t[k + u].c[0]);
@@ -96,7 +104,7 @@ __device__ __forceinline__ void dot_cols(Dot3 &d0, Dot3 &d1, Dot3 &d2, const Jit
         }
     }
     for (; k < n; k++) {
-        const uint64_t a = t[k].ptr[(i + (uint64_t)t[k].sh) & m];
+        const uint64_t a = gload(t[k].ptr + ((i + (uint64_t)t[k].sh) & m));
         d0.term(a, t[k].c[0]);
         if (D == 3) {
             d1.term(a, t[k].c[1]);
@@ -106,10 +114,18 @@ __device__ __forceinline__ void dot_cols(Dot3 &d0, Dot3 &d1, Dot3 &d2, const Jit
 }
 extern "C" __global__ void __launch_bounds__(256) ZKJIT_WAVES zxp_jit(const JitParams p)
 {
+#if ZKJIT_KL_LDS
+    extern __shared__ __attribute__((aligned(16))) uint32_t kls[];
+    for (uint32_t w = threadIdx.x; w < p.nkl; w += 256) kls[w] = p.kl[w];
+    __syncthreads();
+    const uint32_t *K = kls;
+#else
+    const uint32_t *K = p.kl;
+#endif
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (1ULL << p.logdom)) return;
     const uint64_t m = p.rmask;
-#define C(j, sh) p.cp[j][(i + (uint64_t)(sh)) & m]
+#define C(j, sh) gload(p.cp[j] + ((i + (uint64_t)(sh)) & m))
 )";
 
 void appendf(std::string &s, const char *fmt, ...)
@@ -166,10 +182,18 @@ int rtc_compile(const std::string &src, std::vector<char> &code)
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "zxp_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
         return set_error(ZKGPU_ERR_ARG, "zxp jit: hiprtcCreateProgram failed");
-    // -O1: the straight-line body needs no loop optimisation, and -O3 takes
-    // 5-10x longer to compile with the same instruction count (measured on
-    // the synthetic step42ns: 17.7 K VALU per row either way)
-    const char *opts[] = {"--offload-arch=gfx950", "-O1", "-std=c++17"};
+    // LDS-staged limb tables compile at -O2: the load/store vectorizer merges
+    // each term's limb reads into 16+8-byte loads (-O1 does not run it).
+    // Otherwise -O1 (-O2 is no faster there: the scheduler hoists more scalar
+    // loads, e.g. step42ns without LDS 14.1 -> 16.7 ms).  Compile time is about
+    // the same.  ZKGPU_ZXP_JIT_OPT overrides.
+    const bool klds = src.find("#define ZKJIT_KL_LDS 1") != std::string::npos;
+    const std::string olev = [&] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_OPT");
+        const int o = e ? atoi(e) : (klds ? 2 : 1);
+        return std::string("-O") + std::to_string(o >= 0 && o <= 3 ? o : 1);
+    }();
+    const char *opts[] = {"--offload-arch=gfx950", olev.c_str(), "-std=c++17"};
     const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
     if (r != HIPRTC_SUCCESS) {
         size_t ls = 0;
@@ -209,6 +233,22 @@ int compile(const std::string &src, hipFunction_t *out)
 }
 
 }  // namespace
+
+// ZKGPU_ZXP_JIT_KLDS: 0 never, 1 (default) for limb tables of at least
+// JIT_KL_LDS_MIN words, 2 always.  Measured on the config-4 STARK at 2^23:
+// step42ns (4.1 K words) 14.1 -> 12.4 ms; step52ns (0.4 K words) is
+// 9.2 -> 14.4 ms with LDS (its VGPRs go 74 -> 198), so small tables stay on
+// scalar loads.
+constexpr size_t JIT_KL_LDS_MIN = 1024;
+static bool jit_kl_lds(size_t nkl)
+{
+    static const int mode = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_KLDS");
+        return e ? atoi(e) : 1;
+    }();
+    if (!mode || !nkl || nkl * 4 > JIT_KL_LDS_MAX) return false;
+    return mode == 2 || nkl >= JIT_KL_LDS_MIN;
+}
 
 int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const uint64_t *> &cp,
                          std::vector<uint64_t> &kc, std::vector<uint32_t> &kl, std::vector<JitTerm> &zt)
@@ -292,16 +332,34 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             return 0;
         }
         case ZXP_X: uses_x = true; x = {"xv", 1}; return 0;
-        case ZXP_XDIV: x = {"gl3{{p.xdiv[3*i],p.xdiv[3*i+1],p.xdiv[3*i+2]}}", 3}; return 0;
-        case ZXP_XDIVW: x = {"gl3{{p.xdivw[3*i],p.xdivw[3*i+1],p.xdivw[3*i+2]}}", 3}; return 0;
-        case ZXP_ZI: x = {"p.zh[i & p.zmask]", 1}; return 0;
+        case ZXP_XDIV: x = {"gl3{{gload(p.xdiv+3*i),gload(p.xdiv+3*i+1),gload(p.xdiv+3*i+2)}}", 3}; return 0;
+        case ZXP_XDIVW: x = {"gl3{{gload(p.xdivw+3*i),gload(p.xdivw+3*i+1),gload(p.xdivw+3*i+2)}}", 3}; return 0;
+        case ZXP_ZI: x = {"gload(p.zh + (i & p.zmask))", 1}; return 0;
         default: return 1;
         }
+    };
+    // limb table layout: Dot3 inits 3 words in 4-word slots, terms 6 words in
+    // 8-word slots, so the kernel reads them with 16-byte vector loads
+    auto align_kl = [&](size_t a) {
+        while (kl.size() % a) kl.push_back(0);
     };
     auto limbs3 = [&](uint64_t c) {  // Dot3 constant init: 22/21/21-bit limbs of c
         kl.push_back((uint32_t)(c & ((1u << 22) - 1)));
         kl.push_back((uint32_t)((c >> 22) & ((1u << 21) - 1)));
         kl.push_back((uint32_t)(c >> 43));
+        kl.push_back(0);
+    };
+    auto limbs6x3 = [&](const uint64_t coef[3]) {  // term limbs of the three components; returns the slot
+        align_kl(8);
+        const size_t kt = kl.size();
+        for (int j = 0; j < 3; j++) {
+            uint32_t l6[6];
+            zxp_limbs6(coef[j] % 0xFFFFFFFF00000001ULL, l6);
+            kl.insert(kl.end(), l6, l6 + 6);
+            kl.push_back(0);
+            kl.push_back(0);
+        }
+        return kt;
     };
     std::string body;
     // assignment of a value expression to a destination operand
@@ -368,6 +426,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                             const uint64_t sum = c0[j] + v;
                             c0[j] = (sum < v || sum >= P) ? sum - P : sum;
                         }
+                align_kl(4);
                 dot_k0[k] = kl.size();
                 for (int j = 0; j < 3; j++) limbs3(c0[j]);
                 first_use[k] = k;
@@ -383,12 +442,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                     st.three = three;
                     st.val = o.kind == ZXP_TMP1 ? "a" + std::to_string(o.a)
                                                 : "b" + std::to_string(o.a) + ".v[" + std::to_string(tm.comp) + "]";
-                    st.kt = kl.size();
-                    for (int j = 0; j < 3; j++) {
-                        uint32_t l6[6];
-                        zxp_limbs6(tm.coef[j] % 0xFFFFFFFF00000001ULL, l6);
-                        kl.insert(kl.end(), l6, l6 + 6);
-                    }
+                    st.kt = limbs6x3(tm.coef);
                     stream[d].push_back(st);
                     first_use[k] = std::min<uint32_t>(first_use[k], (uint32_t)d);
                 }
@@ -405,21 +459,21 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         for (uint32_t k : declare_at[at]) {
             const size_t k0 = dot_k0[k];
             if (in.ins[k].op == ZXP_DOT3)
-                appendf(body, "Dot3 D%u_0(p.kl + %zu), D%u_1(p.kl + %zu), D%u_2(p.kl + %zu);\n", k, k0, k, k0 + 3, k,
-                        k0 + 6);
+                appendf(body, "Dot3 D%u_0(K + %zu), D%u_1(K + %zu), D%u_2(K + %zu);\n", k, k0, k, k0 + 4, k,
+                        k0 + 8);
             else
-                appendf(body, "Dot3 D%u_0(p.kl + %zu);\n", k, k0);
+                appendf(body, "Dot3 D%u_0(K + %zu);\n", k, k0);
         }
     };
     auto emit_streams = [&](uint32_t at) {
         for (const Stream &st : stream[at]) {
             if (st.three)
                 appendf(body,
-                        "{ const uint64_t v_ = %s; D%u_0.term(v_, p.kl + %zu); D%u_1.term(v_, p.kl + %zu); "
-                        "D%u_2.term(v_, p.kl + %zu); }\n",
-                        st.val.c_str(), st.dot, st.kt, st.dot, st.kt + 6, st.dot, st.kt + 12);
+                        "{ const uint64_t v_ = %s; D%u_0.term_al(v_, K + %zu); D%u_1.term_al(v_, K + %zu); "
+                        "D%u_2.term_al(v_, K + %zu); }\n",
+                        st.val.c_str(), st.dot, st.kt, st.dot, st.kt + 8, st.dot, st.kt + 16);
             else
-                appendf(body, "D%u_0.term(%s, p.kl + %zu);\n", st.dot, st.val.c_str(), st.kt);
+                appendf(body, "D%u_0.term_al(%s, K + %zu);\n", st.dot, st.val.c_str(), st.kt);
         }
     };
     for (uint32_t k = 0; k < in.n_instr; k++) {
@@ -469,19 +523,14 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                 if (loop && memcol(tm)) continue;
                 std::string e;
                 if (col_read(o.a, o.b, (int32_t)o.c, e)) return 1;
-                const size_t kt = kl.size();
-                for (int j = 0; j < 3; j++) {
-                    uint32_t l6[6];
-                    zxp_limbs6(tm.coef[j] % 0xFFFFFFFF00000001ULL, l6);
-                    kl.insert(kl.end(), l6, l6 + 6);
-                }
+                const size_t kt = limbs6x3(tm.coef);
                 if (three)
                     appendf(body,
-                            "{ const uint64_t v_ = %s; D%u_0.term(v_, p.kl + %zu); D%u_1.term(v_, p.kl + %zu); "
-                            "D%u_2.term(v_, p.kl + %zu); }\n",
-                            e.c_str(), k, kt, k, kt + 6, k, kt + 12);
+                            "{ const uint64_t v_ = %s; D%u_0.term_al(v_, K + %zu); D%u_1.term_al(v_, K + %zu); "
+                            "D%u_2.term_al(v_, K + %zu); }\n",
+                            e.c_str(), k, kt, k, kt + 8, k, kt + 16);
                 else
-                    appendf(body, "D%u_0.term(%s, p.kl + %zu);\n", k, e.c_str(), kt);
+                    appendf(body, "D%u_0.term_al(%s, K + %zu);\n", k, e.c_str(), kt);
             }
             char fin[128];
             if (three)
@@ -538,6 +587,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     }
     // assemble: prelude, params, declarations, body, deferred stores
     src = k_gl_device_src;
+    appendf(src, "#define ZKJIT_KL_LDS %d\n", jit_kl_lds(kl.size()) ? 1 : 0);
     if (in.waves_per_eu)
         appendf(src, "#define ZKJIT_WAVES __attribute__((amdgpu_waves_per_eu(%u)))\n", in.waves_per_eu);
     else
@@ -549,11 +599,11 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         if (written_any[j]) appendf(src, "uint64_t w%u = 0;\n", j);
     if (uses_x)
         appendf(src, "const uint64_t ex_ = i << (%u - p.logomega);\n"
-                     "const uint64_t xv = gl_mul(p.x_start, gl_mul(p.tw_lo[ex_ & %lluULL], p.tw_hi[ex_ >> %u]));\n",
+                     "const uint64_t xv = gl_mul(p.x_start, gl_mul(gload(p.tw_lo + (ex_ & %lluULL)), gload(p.tw_hi + (ex_ >> %u))));\n",
                 TW_MAX_LOG, (unsigned long long)(TW_LEVEL_SIZE - 1), TW_LEVEL_BITS);
     src += body;
     for (uint32_t j = 0; j < written_any.size(); j++)
-        if (written_any[j]) appendf(src, "const_cast<uint64_t *>(p.cp[%u])[i] = gl_canon(w%u);\n", j, j);
+        if (written_any[j]) appendf(src, "gstore(const_cast<uint64_t *>(p.cp[%u]) + i, gl_canon(w%u));\n", j, j);
     src += "#undef C\n}\n";
     return 0;
 }
@@ -598,11 +648,13 @@ int zxp_jit_run(const ZxpJitIn &in, hipStream_t s)
     p.logomega = in.log_omega;
     p.rmask = in.wrap ? (1ULL << in.log_dom) - 1 : ~0ULL;
     p.zmask = in.zmask;
+    const bool klds = jit_kl_lds(kl.size());
+    p.nkl = klds ? (uint32_t)kl.size() : 0;
     void *args[] = {&p};
     const uint64_t dom = 1ULL << in.log_dom;
     prof_begin(s);
     rc = check_hip(hipModuleLaunchKernel(fn, (uint32_t)((dom + JIT_THREADS - 1) / JIT_THREADS), 1, 1, JIT_THREADS, 1,
-                                         1, 0, s, args, nullptr),
+                                         1, klds ? (uint32_t)(kl.size() * 4) : 0, s, args, nullptr),
                    "zxp jit: launch");
     prof_end("k_zxp_jit", in.bytes, s);
     return rc;
