@@ -90,6 +90,129 @@ __global__ void __launch_bounds__(256) k_leaves_rows(uint64_t *digests, const ui
     for (int k = 0; k < 4; k++) d[k] = ncols <= 4 ? st[k] : gl_canon(st[k]);
 }
 
+// ---------------------------------------------------------------- lane-parallel form
+// Tree levels and leaf sets too small to fill the GPU take the LATENCY of one
+// thread's ~19 K-instruction permutation chain (~65 us per level, measured).
+// Here one permutation is spread over 16 lanes (lane x < 12 holds st[x], 4
+// states per wave): the S-boxes run side by side and each lane forms its MDS
+// row sum from the state exchanged through LDS -- ~4 K instructions on the
+// critical path.  Textbook round structure (poseidon_g_executor.cpp:201-231):
+// add constants, S-box (full rounds: all lanes; partial: lane 0), MDS.
+constexpr int LP_LANES = 16;
+// Crossover: the lane form costs ~3.1x the instructions per permutation
+// (3.8 K VALU per 4 states vs 19.4 K per 64), so it wins while a launch is
+// latency-bound: up to ~2^15 concurrent permutations on 256 CUs.
+constexpr uint64_t LP_MAX_PERMS = 1ULL << 15;
+
+struct LpCtx {
+    uint64_t rc[30];  // this lane's round constants
+    uint32_t m[12];   // this lane's MDS row
+    uint32_t x;       // state element held (>= 12: idle lane)
+    uint64_t *xch;    // the state's 16 exchange slots in LDS
+};
+
+__device__ __forceinline__ void lp_init(LpCtx &c, uint64_t *lds)
+{
+    c.x = threadIdx.x & (LP_LANES - 1);
+    const uint32_t xx = c.x < 12 ? c.x : 0;
+#pragma unroll
+    for (int r = 0; r < 30; r++) c.rc[r] = c.x < 12 ? ZKGPU_POSEIDON_RC[r * 12 + xx] : 0;
+#pragma unroll
+    for (int y = 0; y < 12; y++) c.m[y] = mds_entry((int)xx, y);
+    c.xch = lds + (threadIdx.x & ~(LP_LANES - 1));
+}
+
+// the 12 state elements as seen by every lane of the state's group
+__device__ __forceinline__ void lp_share(const LpCtx &c, uint64_t s, uint64_t v[12])
+{
+    c.xch[c.x] = s;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int y = 0; y < 12; y++) v[y] = c.xch[y];
+    __builtin_amdgcn_wave_barrier();  // reads done before the next round's write
+}
+
+template <int r>
+__device__ __forceinline__ void lp_round(const LpCtx &c, uint64_t &s)
+{
+    {
+        s = gl_add(s, c.rc[r]);
+        if constexpr (r < 4 || r >= 26)
+            s = pow7(s);
+        else if (c.x == 0)
+            s = pow7(s);
+        uint64_t v[12];
+        lp_share(c, s, v);
+        uint64_t sl = 0, sh = 0;
+#pragma unroll
+        for (int y = 0; y < 12; y++) {
+            sl += (uint64_t)(uint32_t)v[y] * c.m[y];
+            sh += (uint64_t)(uint32_t)(v[y] >> 32) * c.m[y];
+        }
+        // value = sl + sh * 2^32 < 2^75
+        uint32_t c1, c2;
+        const uint32_t mid = __builtin_addc((uint32_t)(sl >> 32), (uint32_t)sh, 0u, &c1);
+        const uint32_t h = __builtin_addc((uint32_t)(sh >> 32), 0u, c1, &c2);
+        s = gl_reduce96(((uint64_t)mid << 32) | (uint32_t)sl, h);
+    }
+}
+
+template <int... rs>
+__device__ __forceinline__ void lp_rounds(const LpCtx &c, uint64_t &s, std::integer_sequence<int, rs...>)
+{
+    (lp_round<rs>(c, s), ...);
+}
+
+__device__ __forceinline__ uint64_t lp_perm(const LpCtx &c, uint64_t s)
+{
+    lp_rounds(c, s, std::make_integer_sequence<int, 30>{});
+    return s;
+}
+
+// one tree level, 16 lanes per node
+__global__ void __launch_bounds__(256) k_merkle_level_lp(uint64_t *dst, const uint64_t *lvl, uint64_t next)
+{
+    __shared__ uint64_t lds[256];
+    LpCtx c;
+    lp_init(c, lds);
+    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / LP_LANES;
+    if (i >= next) return;  // whole 16-lane groups
+    uint64_t s = c.x < 8 ? lvl[8 * i + c.x] : 0;
+    s = lp_perm(c, s);
+    if (c.x < 4) dst[4 * i + c.x] = gl_canon(s);
+}
+
+// leaf digests (linear_hash) of a row-major source, 16 lanes per row
+__global__ void __launch_bounds__(256) k_leaves_rows_lp(uint64_t *digests, const uint64_t *__restrict__ src,
+                                                       uint64_t ncols, uint64_t nrows)
+{
+    __shared__ uint64_t lds[256];
+    LpCtx c;
+    lp_init(c, lds);
+    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / LP_LANES;
+    if (i >= nrows) return;
+    const uint64_t *row = src + i * ncols;
+    uint64_t s;
+    if (ncols <= 4) {
+        s = c.x < ncols ? row[c.x] : 0;  // copied, not hashed (and not canonicalised)
+    } else {
+        s = 0;
+        for (uint64_t c0 = 0; c0 < ncols; c0 += 8) {
+            if (c0) {  // capacity = previous output[0..3]
+                uint64_t v[12];
+                lp_share(c, s, v);
+                s = c.x >= 8 && c.x < 12 ? v[c.x - 8] : s;
+            }
+            if (c.x < 8) s = c0 + c.x < ncols ? row[c0 + c.x] : 0;
+            s = lp_perm(c, s);
+        }
+        s = gl_canon(s);
+    }
+    if (c.x < 4) digests[4 * i + c.x] = s;
+}
+
 // one tree level: dst[i] = hash(lvl[2i] || lvl[2i+1] || 0000)
 __global__ void __launch_bounds__(256) k_merkle_level(uint64_t *dst, const uint64_t *lvl, uint64_t next)
 {
@@ -157,7 +280,11 @@ int merkle_leaves_rows(uint64_t *digests, const uint64_t *src, uint64_t ncols, u
 {
     if (!nrows) return 0;
     prof_begin(s);
-    hipLaunchKernelGGL(k_leaves_rows, dim3(blocks_for(nrows, 256)), dim3(256), 0, s, digests, src, ncols, nrows);
+    if (nrows <= LP_MAX_PERMS && ncols > 4)
+        hipLaunchKernelGGL(k_leaves_rows_lp, dim3(blocks_for(nrows * LP_LANES, 256)), dim3(256), 0, s, digests, src,
+                           ncols, nrows);
+    else
+        hipLaunchKernelGGL(k_leaves_rows, dim3(blocks_for(nrows, 256)), dim3(256), 0, s, digests, src, ncols, nrows);
     prof_end("k_leaves_rows", 8.0 * (double)nrows * (double)ncols + 32.0 * (double)nrows, s);
     return check_launch("k_leaves_rows");
 }
@@ -168,8 +295,12 @@ int merkle_levels(uint64_t *nodes, uint64_t nrows, hipStream_t s)
     while (pending > 1) {
         uint64_t next = pending / 2;
         prof_begin(s);
-        hipLaunchKernelGGL(k_merkle_level, dim3(blocks_for(next, 256)), dim3(256), 0, s, nodes + off + 4 * pending,
-                           nodes + off, next);
+        if (next <= LP_MAX_PERMS)
+            hipLaunchKernelGGL(k_merkle_level_lp, dim3(blocks_for(next * LP_LANES, 256)), dim3(256), 0, s,
+                               nodes + off + 4 * pending, nodes + off, next);
+        else
+            hipLaunchKernelGGL(k_merkle_level, dim3(blocks_for(next, 256)), dim3(256), 0, s, nodes + off + 4 * pending,
+                               nodes + off, next);
         prof_end("k_merkle_level", 96.0 * (double)next, s);
         off += 4 * pending;
         pending = next;
