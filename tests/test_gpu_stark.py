@@ -46,6 +46,24 @@ def test_full_proof_bit_exact(oracle, zkgpu, n_bits, blow, t, m, q):
     g.close()
 
 
+def test_recursive1_shaped_proof_bit_exact(oracle, zkgpu):
+    """The golden recursive1 proofs' structure at a small size: blowup 2^3,
+    43 queries, FRI step reductions of 4 and 3 bits (golden: nBitsExt 20,
+    steps [20, 16, 12, 9, 6]) -- here nBitsExt 14, steps [14, 10, 7, 4]."""
+    from zkgpu.synthetic import SyntheticStark
+    from zkgpu.stark import GpuStark
+    inst = SyntheticStark(n_bits=11, blowup_bits=3, t=5, m=2, n_queries=43, fri_steps=[14, 10, 7, 4])
+    o, ref = oracle_proof(inst)
+    g = GpuStark(inst)
+    g.witness()
+    got = g.prove()
+    for k in ref:
+        assert got[k] == ref[k], k
+    bad, _, _ = verify_fri(oracle, got, g.verkey(), g.publics(), inst.fri_steps, inst.n_queries)
+    assert bad["s0"] == bad["fri_tree"] == bad["fold"] == bad["final"] == 0
+    g.close()
+
+
 def test_set_cm1_row_major_boundary(oracle, zkgpu):
     """Loading the trace through the reference's row-major layout gives the same proof."""
     from zkgpu.synthetic import SyntheticStark

@@ -28,7 +28,7 @@ def per_kernel(path, counter):
 def bench_label(name):
     """rocprof kernel name -> the label bench.py / zkgpu_prof_* use."""
     base = name.split("(")[0].replace("void ", "").replace("zk::", "").strip()
-    m = re.match(r"k_ntt_pass<(\d+), (\d+), \w+>", base)
+    m = re.match(r"k_ntt_pass<(\d+), (\d+),", base)
     if m:
         return "k_ntt_pass<%d>" % (int(m.group(1)) + int(m.group(2)))
     return base

@@ -125,12 +125,16 @@ __host__ __device__ constexpr int brev_c(int x, int bits)
 //   step 2: thread (g, k1) reads y[j2][k1] (j2 < R2), R2-point DFT in
 //           registers -> X[k1 + R1*k2], outer twiddle / post-scale, store.
 // LDS image (k1*R2 + j2)*17 + g: conflict-free for both access patterns.
-template <int L1, int L2, bool INV>
+// SPLIT: the LDS transpose moves the low and then the high 32-bit words
+// through a half-size image (two more barriers), halving the workgroup's LDS
+// so more waves fit per CU (LDS, not VGPRs, limits the radix-256 pass).
+template <int L1, int L2, bool INV, bool SPLIT>
 __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
 {
     constexpr int R1 = 1 << L1, R2 = 1 << L2, LOGR = L1 + L2, R = 1 << LOGR;
     constexpr int T = GROUPS * R2;
-    __shared__ uint64_t lds[R * 17];
+    __shared__ uint64_t lds[SPLIT ? (R * 17 + 1) / 2 : R * 17];
+    uint32_t *lds32 = reinterpret_cast<uint32_t *>(lds);
     __shared__ uint64_t twR[R];  // omega_R^i
     // columns vary fastest across workgroups: the workgroups sharing a unit's
     // outer-twiddle slice run together and find it in L2
@@ -179,17 +183,37 @@ __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
 #pragma unroll
     for (int r = 0; r < R1; r++) {
         const int k1 = brev_c(r, L1);
-        uint64_t y = v[r];
-        if (k1) y = gl_mul(y, twR[(j2 * k1) & (R - 1)]);
-        lds[(k1 * R2 + j2) * 17 + g] = y;
+        if (k1) v[r] = gl_mul(v[r], twR[(j2 * k1) & (R - 1)]);
     }
-    __syncthreads();
-    // ------------------------------------------------ step 2 (R2-DFT + store)
-    if (tid >= GROUPS * R1) return;
-    g = tid & 15;
-    const int k1 = tid >> 4;
+    const bool active = tid < GROUPS * R1;  // step-2 threads
+    const int g2 = tid & 15, k1s = tid >> 4;
+    if constexpr (SPLIT) {
+        uint32_t lo[R2 > R1 ? R2 : R1];
 #pragma unroll
-    for (int jj = 0; jj < R2; jj++) v[jj] = lds[(k1 * R2 + jj) * 17 + g];
+        for (int r = 0; r < R1; r++) lds32[(brev_c(r, L1) * R2 + j2) * 17 + g] = (uint32_t)v[r];
+        __syncthreads();
+        if (active) {
+#pragma unroll
+            for (int jj = 0; jj < R2; jj++) lo[jj] = lds32[(k1s * R2 + jj) * 17 + g2];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < R1; r++) lds32[(brev_c(r, L1) * R2 + j2) * 17 + g] = (uint32_t)(v[r] >> 32);
+        __syncthreads();
+        if (!active) return;
+#pragma unroll
+        for (int jj = 0; jj < R2; jj++) v[jj] = ((uint64_t)lds32[(k1s * R2 + jj) * 17 + g2] << 32) | lo[jj];
+    } else {
+#pragma unroll
+        for (int r = 0; r < R1; r++) lds[(brev_c(r, L1) * R2 + j2) * 17 + g] = v[r];
+        __syncthreads();
+        if (!active) return;
+#pragma unroll
+        for (int jj = 0; jj < R2; jj++) v[jj] = lds[(k1s * R2 + jj) * 17 + g2];
+    }
+    // ------------------------------------------------ step 2 (R2-DFT + store)
+    g = g2;
+    const int k1 = k1s;
     dft_regs<L2, INV>(v);
     if (!a.last && a.otw) {
         // X[k] * omega_m^(j' k) from the table (one coalesced load per element
@@ -399,10 +423,18 @@ static void launch_pass(const PassArgs &a, uint64_t ncols, int inverse, hipStrea
     constexpr int LOGR = L1 + L2;
     uint64_t units = (1ULL << (a.logn - LOGR)) / 16;
     dim3 grid((uint32_t)(units * ncols));
-    if (inverse)
-        hipLaunchKernelGGL((k_ntt_pass<L1, L2, true>), grid, dim3(16 << L2), 0, s, a);
+    static const bool split = [] {
+        const char *e = getenv("ZKGPU_NTT_SPLIT");
+        return !e || atoi(e) != 0;
+    }();
+    if (inverse && split)
+        hipLaunchKernelGGL((k_ntt_pass<L1, L2, true, true>), grid, dim3(16 << L2), 0, s, a);
+    else if (inverse)
+        hipLaunchKernelGGL((k_ntt_pass<L1, L2, true, false>), grid, dim3(16 << L2), 0, s, a);
+    else if (split)
+        hipLaunchKernelGGL((k_ntt_pass<L1, L2, false, true>), grid, dim3(16 << L2), 0, s, a);
     else
-        hipLaunchKernelGGL((k_ntt_pass<L1, L2, false>), grid, dim3(16 << L2), 0, s, a);
+        hipLaunchKernelGGL((k_ntt_pass<L1, L2, false, false>), grid, dim3(16 << L2), 0, s, a);
 }
 
 static void dispatch_pass(uint32_t logr, const PassArgs &a, uint64_t ncols, int inverse, hipStream_t s)
