@@ -152,6 +152,14 @@ for step in "$@"; do
             echo "klds=$1 opt=$2 waves=$3 $(python -c "import json;d=json.load(open('gpurun_out/jit_$1_$2_$3.json'));s=d['stages_ms'];print(d['ms_per_step'],'ms q',s['STARK_STEP_4_CALCULATE_EXPS_2NS'],'f',s['STARK_STEP_5_CALCULATE_EXPS'],'s2',s['STARK_STEP_2_CALCULATE_EXPS'],'s3',s['STARK_STEP_3_CALCULATE_EXPS'])")"
         done
         ;;
+    jitzt)
+        for u in 0 1; do
+            ZKGPU_ZXP_JIT_ZTLDS=$u timeout -k 10 300 python bench.py --workload stark --steps 2 --warmup 1 --no-cpu \
+                > gpurun_out/jitu_$u.json 2>> gpurun_out/jitu.err
+            ok_or_stop $? "stark jit ztlds=$u"
+            echo "ztlds=$u $(python -c "import json;d=json.load(open('gpurun_out/jitu_$u.json'));s=d['stages_ms'];print(d['ms_per_step'],'ms q',s['STARK_STEP_4_CALCULATE_EXPS_2NS'],'f',s['STARK_STEP_5_CALCULATE_EXPS'],'s2',s['STARK_STEP_2_CALCULATE_EXPS'],'s3',s['STARK_STEP_3_CALCULATE_EXPS'])")"
+        done
+        ;;
     nttsplit)
         for v in 0 1 0 1; do
             ZKGPU_NTT_SPLIT=$v timeout -k 10 300 python bench.py --no-cpu > gpurun_out/ntt_split_$v.json 2>> gpurun_out/ntt_split.err

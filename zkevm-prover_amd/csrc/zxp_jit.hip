@@ -84,18 +84,19 @@ struct JitParams {
     uint32_t logdom, logomega, zmask;
     uint32_t nkl;
 };
-// long column runs of a DOT: a loop over table terms, 4 loads in flight
+// long column runs of a DOT: a loop over table terms, ZKJIT_UNROLL loads in flight
 template <int D>
 __device__ __forceinline__ void dot_cols(Dot3 &d0, Dot3 &d1, Dot3 &d2, const JitTerm *t, int n, uint64_t i,
                                          uint64_t m)
 {
+    constexpr int U = ZKJIT_UNROLL;
     int k = 0;
-    for (; k + 4 <= n; k += 4) {
-        uint64_t a[4];
+    for (; k + U <= n; k += U) {
+        uint64_t a[U];
 #pragma unroll
-        for (int u = 0; u < 4; u++) a[u] = gload(t[k + u].ptr + ((i + (uint64_t)t[k + u].sh) & m));
+        for (int u = 0; u < U; u++) a[u] = gload(t[k + u].ptr + ((i + (uint64_t)t[k + u].sh) & m));
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < U; u++) {
             d0.term(a[u], t[k + u].c[0]);
             if (D == 3) {
                 d1.term(a[u], t[k + u].c[1]);
@@ -117,10 +118,13 @@ extern "C" __global__ void __launch_bounds__(256) ZKJIT_WAVES zxp_jit(const JitP
 #if ZKJIT_KL_LDS
     extern __shared__ __attribute__((aligned(16))) uint32_t kls[];
     for (uint32_t w = threadIdx.x; w < p.nkl; w += 256) kls[w] = p.kl[w];
-    __syncthreads();
     const uint32_t *K = kls;
 #else
     const uint32_t *K = p.kl;
+#endif
+    const JitTerm *ZT = p.zt;  // (in LDS: measured slower, 9.0 -> 11.4 ms for step52ns)
+#if ZKJIT_KL_LDS
+    __syncthreads();
 #endif
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (1ULL << p.logdom)) return;
@@ -508,9 +512,9 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                     zt.push_back(jt);
                 }
                 if (three)
-                    appendf(body, "dot_cols<3>(D%u_0, D%u_1, D%u_2, p.zt + %zu, %u, i, m);\n", k, k, k, t0, n_mem);
+                    appendf(body, "dot_cols<3>(D%u_0, D%u_1, D%u_2, ZT + %zu, %u, i, m);\n", k, k, k, t0, n_mem);
                 else
-                    appendf(body, "dot_cols<1>(D%u_0, D%u_0, D%u_0, p.zt + %zu, %u, i, m);\n", k, k, k, t0, n_mem);
+                    appendf(body, "dot_cols<1>(D%u_0, D%u_0, D%u_0, ZT + %zu, %u, i, m);\n", k, k, k, t0, n_mem);
             }
             for (uint32_t t = I.a; t < I.a + I.b; t++) {
                 const zxp_term &tm = in.terms[t];
@@ -588,6 +592,14 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     // assemble: prelude, params, declarations, body, deferred stores
     src = k_gl_device_src;
     appendf(src, "#define ZKJIT_KL_LDS %d\n", jit_kl_lds(kl.size()) ? 1 : 0);
+    {
+        static const int unroll = [] {  // column terms per loop iteration (loads in flight)
+            const char *e = getenv("ZKGPU_ZXP_JIT_UNROLL");
+            const int u = e ? atoi(e) : 4;
+            return (u == 2 || u == 4 || u == 8 || u == 16) ? u : 4;
+        }();
+        appendf(src, "#define ZKJIT_UNROLL %d\n", unroll);
+    }
     if (in.waves_per_eu)
         appendf(src, "#define ZKJIT_WAVES __attribute__((amdgpu_waves_per_eu(%u)))\n", in.waves_per_eu);
     else
