@@ -152,13 +152,15 @@ for step in "$@"; do
             echo "klds=$1 opt=$2 waves=$3 $(python -c "import json;d=json.load(open('gpurun_out/jit_$1_$2_$3.json'));s=d['stages_ms'];print(d['ms_per_step'],'ms q',s['STARK_STEP_4_CALCULATE_EXPS_2NS'],'f',s['STARK_STEP_5_CALCULATE_EXPS'],'s2',s['STARK_STEP_2_CALCULATE_EXPS'],'s3',s['STARK_STEP_3_CALCULATE_EXPS'])")"
         done
         ;;
-    jitzt)
-        for u in 0 1; do
-            ZKGPU_ZXP_JIT_ZTLDS=$u timeout -k 10 300 python bench.py --workload stark --steps 2 --warmup 1 --no-cpu \
-                > gpurun_out/jitu_$u.json 2>> gpurun_out/jitu.err
-            ok_or_stop $? "stark jit ztlds=$u"
-            echo "ztlds=$u $(python -c "import json;d=json.load(open('gpurun_out/jitu_$u.json'));s=d['stages_ms'];print(d['ms_per_step'],'ms q',s['STARK_STEP_4_CALCULATE_EXPS_2NS'],'f',s['STARK_STEP_5_CALCULATE_EXPS'],'s2',s['STARK_STEP_2_CALCULATE_EXPS'],'s3',s['STARK_STEP_3_CALCULATE_EXPS'])")"
+    jitopt)
+        for o in d 2 d 2; do
+            if [ "$o" = d ]; then unset ZKGPU_ZXP_JIT_OPT; else export ZKGPU_ZXP_JIT_OPT=$o; fi
+            timeout -k 10 300 python bench.py --workload stark --steps 2 --warmup 1 --no-cpu \
+                > gpurun_out/jito_$o.json 2>> gpurun_out/jito.err
+            ok_or_stop $? "stark jit opt=$o"
+            echo "opt=$o $(python -c "import json;d=json.load(open('gpurun_out/jito_$o.json'));s=d['stages_ms'];print(d['ms_per_step'],'ms q',s['STARK_STEP_4_CALCULATE_EXPS_2NS'],'f',s['STARK_STEP_5_CALCULATE_EXPS'],'s2',s['STARK_STEP_2_CALCULATE_EXPS'],'s3',s['STARK_STEP_3_CALCULATE_EXPS'])")"
         done
+        unset ZKGPU_ZXP_JIT_OPT
         ;;
     nttsplit)
         for v in 0 1 0 1; do

@@ -633,7 +633,7 @@ int zxp_jit_run(const ZxpJitIn &in, hipStream_t s)
     if ((rc = compile(src, &fn))) return rc;
     // tables: zt | cp | kc | kl
     const size_t off_cp = zt.size() * sizeof(JitTerm), off_kc = off_cp + cp.size() * 8;
-    const size_t off_kl = off_kc + (kc.size() + 1) * 8;
+    const size_t off_kl = (off_kc + (kc.size() + 1) * 8 + 15) & ~(size_t)15;  // 16-byte limb slots
     const size_t total = off_kl + (kl.size() + 1) * 4;
     char *buf = jit_buf(total);
     if (!buf) return set_error(ZKGPU_ERR_OOM, "zxp jit: table buffer");
@@ -713,7 +713,7 @@ extern "C" int zkgpu_zxp_jit_source(const void *instr, uint32_t n_instr, const v
     std::vector<uint64_t> kc;
     std::vector<uint32_t> kl;
     std::vector<JitTerm> zt;
-    J.dot_loop_min = 8;
+    J.dot_loop_min = getenv("ZKGPU_ZXP_JIT_DOTLOOP") ? (uint32_t)atoi(getenv("ZKGPU_ZXP_JIT_DOTLOOP")) : 8;
     if ((rc = zxp_jit_build_source(J, src, colp, kc, kl, zt))) return rc < 0 ? rc : set_error(ZKGPU_ERR_ARG, "zxp jit: unsupported program shape");
     if (buf && buflen) {
         const size_t n = std::min<size_t>(src.size(), buflen - 1);
