@@ -59,29 +59,67 @@ __device__ __forceinline__ int h12_cmp(const uint64_t *sk, uint64_t n, uint64_t 
     return 0;
 }
 
+// Two-level upper_bound: the first H12_S levels of the search run on a sample
+// of the sorted first components held in LDS (smp[j] = sk0[r_j], r_j =
+// min((j+1) step, n) - 1), the rest in global memory over one sample
+// interval -- 23 -> ~11 dependent random HBM reads per f row at 2^23.
+constexpr uint32_t H12_S = 4096;
+constexpr uint32_t H12_ROWS = 8;  // f rows per thread (amortises the LDS fill)
+
+__device__ __forceinline__ uint64_t h12_sample_row(uint64_t j, uint64_t step, uint64_t n)
+{
+    const uint64_t r = (j + 1) * step;
+    return (r < n ? r : n) - 1;
+}
+
+__global__ void k_h12_sample(uint64_t *smp, const uint64_t *sk0, uint64_t n, uint64_t step, uint32_t S)
+{
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < S) smp[j] = sk0[h12_sample_row(j, step, n)];
+}
+
 // sk: DIM sorted key columns (ld n); perm: sorted position -> table row
 template <int DIM>
-__global__ void k_h12_count(const uint64_t *f, uint64_t f_ld, const uint64_t *sk, const uint32_t *perm, uint64_t n,
-                            uint32_t *cnt, unsigned long long *miss)
+__global__ void __launch_bounds__(256) k_h12_count(const uint64_t *f, uint64_t f_ld, const uint64_t *sk,
+                                                   const uint32_t *perm, uint64_t n, const uint64_t *smp, uint32_t S,
+                                                   uint64_t step, uint32_t *cnt, unsigned long long *miss)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint64_t key[DIM];
+    __shared__ uint64_t ls[H12_S];
+    for (uint32_t j = threadIdx.x; j < S; j += blockDim.x) ls[j] = smp[j];
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * blockDim.x * H12_ROWS + threadIdx.x;
+    for (uint32_t q = 0; q < H12_ROWS; q++) {
+        const uint64_t i = base + (uint64_t)q * blockDim.x;
+        if (i >= n) return;
+        uint64_t key[DIM];
 #pragma unroll
-    for (int c = 0; c < DIM; c++) key[c] = gl_canon(f[c * f_ld + i]);
-    uint64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (h12_cmp<DIM>(sk, n, mid, key) <= 0)
-            lo = mid + 1;
-        else
-            hi = mid;
+        for (int c = 0; c < DIM; c++) key[c] = gl_canon(f[c * f_ld + i]);
+        // first sample j whose row's key is > key
+        uint32_t a = 0, b = S;
+        while (a < b) {
+            const uint32_t mid = (a + b) >> 1;
+            const uint64_t v = ls[mid];
+            const bool gt = v > key[0] || (v == key[0] && h12_cmp<DIM>(sk, n, h12_sample_row(mid, step, n), key) > 0);
+            if (gt)
+                b = mid;
+            else
+                a = mid + 1;
+        }
+        uint64_t lo = a ? h12_sample_row(a - 1, step, n) + 1 : 0;
+        uint64_t hi = a < S ? h12_sample_row(a, step, n) : n;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (h12_cmp<DIM>(sk, n, mid, key) <= 0)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        if (lo == 0 || h12_cmp<DIM>(sk, n, lo - 1, key) != 0) {
+            atomicMin(miss, (unsigned long long)i);
+            continue;
+        }
+        atomicAdd(&cnt[perm[lo - 1]], 1u);
     }
-    if (lo == 0 || h12_cmp<DIM>(sk, n, lo - 1, key) != 0) {
-        atomicMin(miss, (unsigned long long)i);
-        return;
-    }
-    atomicAdd(&cnt[perm[lo - 1]], 1u);
 }
 
 template <int DIM>
@@ -111,7 +149,7 @@ int h1h2(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint6
     // scratch: keys_in, keys_out (n u64 each), sk (dim n u64; sk[0] = keys_out
     // of the last pass), perm_in, perm_out, cnt (n u32 each), miss (u64)
     const size_t kb = n * sizeof(uint64_t), pb = n * sizeof(uint32_t);
-    const size_t need = 2 * kb + 2 * kb /* sk[1], sk[2] */ + 3 * pb + 16;
+    const size_t need = 2 * kb + 2 * kb /* sk[1], sk[2] */ + 3 * pb + 16 + H12_S * 8 /* search sample */;
     char *w = (char *)workspace(4, need);
     if (!w) return ZKGPU_ERR_OOM;
     uint64_t *keys_in = (uint64_t *)w;
@@ -155,10 +193,17 @@ int h1h2(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint6
     uint64_t *sk = keys_out;  // keys_out, sk12[0..n), sk12[n..2n) are contiguous (keys_out + n == sk12)
     hipLaunchKernelGGL(k_h12_fill1, dim3(nblk2(n, B)), dim3(B), 0, s, cnt, n);
     (void)hipMemsetAsync(miss, 0xFF, 8, s);
+    const uint32_t S = (uint32_t)(n < H12_S ? n : H12_S);
+    const uint64_t step = (n + S - 1) / S;
+    uint64_t *smp = (uint64_t *)(miss + 1);
+    hipLaunchKernelGGL(k_h12_sample, dim3(nblk2(S, B)), dim3(B), 0, s, smp, sk, n, step, S);
+    const uint32_t cblocks = nblk2(n, B * H12_ROWS);
     if (dim == 1)
-        hipLaunchKernelGGL(k_h12_count<1>, dim3(nblk2(n, B)), dim3(B), 0, s, f, f_ld, sk, perm_in, n, cnt, miss);
+        hipLaunchKernelGGL(k_h12_count<1>, dim3(cblocks), dim3(B), 0, s, f, f_ld, sk, perm_in, n, smp, S, step, cnt,
+                           miss);
     else
-        hipLaunchKernelGGL(k_h12_count<3>, dim3(nblk2(n, B)), dim3(B), 0, s, f, f_ld, sk, perm_in, n, cnt, miss);
+        hipLaunchKernelGGL(k_h12_count<3>, dim3(cblocks), dim3(B), 0, s, f, f_ld, sk, perm_in, n, smp, S, step, cnt,
+                           miss);
     uint32_t *start = perm_out;  // free now
     {
         size_t tb = tmp_bytes;
