@@ -133,8 +133,13 @@ __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
 {
     constexpr int R1 = 1 << L1, R2 = 1 << L2, LOGR = L1 + L2, R = 1 << LOGR;
     constexpr int T = GROUPS * R2;
-    __shared__ uint64_t lds[SPLIT ? (R * 17 + 1) / 2 : R * 17];
+    __shared__ uint64_t lds[SPLIT ? R * 8 : R * 17];
     uint32_t *lds32 = reinterpret_cast<uint32_t *>(lds);
+    // SPLIT image: row rho = k1 * R2 + j2 holds the 16 groups' words; row
+    // rho is stored at rho ^ (bit L2 of rho), so both 32-lane groups of
+    // ds_write_b32 (two consecutive j2) and of ds_read_b32 (two consecutive
+    // k1) cover the 32 banks once: conflict-free, no padding
+
     __shared__ uint64_t twR[R];  // omega_R^i
     // columns vary fastest across workgroups: the workgroups sharing a unit's
     // outer-twiddle slice run together and find it in L2
@@ -189,20 +194,31 @@ __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
     const int g2 = tid & 15, k1s = tid >> 4;
     if constexpr (SPLIT) {
         uint32_t lo[R2 > R1 ? R2 : R1];
+        // write: row brev(r) * R2 + j2 -> flip = bit 0 of brev(r) (R2 even): two bases
+        const int wb0 = (j2 << 4) + g, wb1 = ((j2 ^ 1) << 4) + g;
+        // read: row k1s * R2 + jj -> flip = k1s & 1: slot = k1s*R2*16 + ((jj ^ f) << 4) + g2
+        const int fm = (k1s & 1) << 4;
+        const int rbe = k1s * R2 * 16 + g2 + fm, rbo = k1s * R2 * 16 + g2 - fm;
 #pragma unroll
-        for (int r = 0; r < R1; r++) lds32[(brev_c(r, L1) * R2 + j2) * 17 + g] = (uint32_t)v[r];
+        for (int r = 0; r < R1; r++) {
+            const int k1 = brev_c(r, L1);
+            lds32[k1 * R2 * 16 + ((k1 & 1) ? wb1 : wb0)] = (uint32_t)v[r];
+        }
         __syncthreads();
         if (active) {
 #pragma unroll
-            for (int jj = 0; jj < R2; jj++) lo[jj] = lds32[(k1s * R2 + jj) * 17 + g2];
+            for (int jj = 0; jj < R2; jj++) lo[jj] = lds32[((jj & 1) ? rbo : rbe) + (jj << 4)];
         }
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < R1; r++) lds32[(brev_c(r, L1) * R2 + j2) * 17 + g] = (uint32_t)(v[r] >> 32);
+        for (int r = 0; r < R1; r++) {
+            const int k1 = brev_c(r, L1);
+            lds32[k1 * R2 * 16 + ((k1 & 1) ? wb1 : wb0)] = (uint32_t)(v[r] >> 32);
+        }
         __syncthreads();
         if (!active) return;
 #pragma unroll
-        for (int jj = 0; jj < R2; jj++) v[jj] = ((uint64_t)lds32[(k1s * R2 + jj) * 17 + g2] << 32) | lo[jj];
+        for (int jj = 0; jj < R2; jj++) v[jj] = ((uint64_t)lds32[((jj & 1) ? rbo : rbe) + (jj << 4)] << 32) | lo[jj];
     } else {
 #pragma unroll
         for (int r = 0; r < R1; r++) lds[(brev_c(r, L1) * R2 + j2) * 17 + g] = v[r];
