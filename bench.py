@@ -150,15 +150,44 @@ def cpu_baseline_stark(sample_bits, log_n, blow, ncols, n_queries):
 VALU_PEAK_WAVE_INSTR_S = 256 * 4 * 2.4e9 / 4  # 256 CUs x 4 SIMDs, one wave64 VALU op per 4 clk @ 2.4 GHz
 
 
+def _profile_order(path):
+    """Natural order of profiles/rNN_vM_* names (r01_v10 after r01_v9); the
+    newest summary wins.  File mtimes are not used: a fresh checkout or a
+    gpurun snapshot gives every file the same one."""
+    import re
+    return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
+
+
 def pmc_for(kernel, args, avg_ms):
     """HBM traffic and VALU issue for the dominant kernel from the committed
-    PMC summary (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py
-    from separate rocprofv3 --pmc passes of this same default command).
-    Returns (traffic bytes per launch or None, valu dict or None)."""
+    PMC summaries (separate rocprofv3 --pmc passes of this same command):
+    profiles/*_pmc_traffic.json (tools/pmc_traffic.py) for the default LDE
+    workload, profiles/*_stark_pmc.json (tools/stark_pmc.py) for the 2^23
+    STARK proof.  Returns (traffic bytes per launch or None, valu dict or None)."""
     import glob
-    if args.workload != "lde" or args.log_n != 23 or args.ncols != 100 or args.blowup_bits != 1:
+    if args.log_n != 23 or args.ncols != 100 or args.blowup_bits != 1:
         return None, None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=os.path.getmtime)
+    if args.workload == "stark":
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_stark_pmc.json")), key=_profile_order)
+        for f in reversed(files):
+            try:
+                ks = json.load(open(f)).get("kernels", {})
+            except (OSError, ValueError):
+                continue
+            lab = ks.get(kernel)
+            if not lab or not lab.get("launches"):
+                continue
+            valu = {"kernel": kernel, "achieved": round(lab["valu_frac"] * VALU_PEAK_WAVE_INSTR_S / 1e9, 1),
+                    "peak": VALU_PEAK_WAVE_INSTR_S / 1e9, "unit": "G wave-instr/s",
+                    "frac": lab["valu_frac"], "source": os.path.basename(f),
+                    "note": ("SQ_INSTS_VALU x 4 clk / (kernel time x 1024 SIMDs) over the kernel's launches "
+                             "in one 2^23 proof; > 1 means part of the stream issues faster than "
+                             "4 clk per wave64 op, i.e. VALU issue is saturated")}
+            return lab["hbm_GB"] * 1e9 / lab["launches"], valu
+        return None, None
+    if args.workload != "lde":
+        return None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=_profile_order)
     for f in reversed(files):
         try:
             lab = json.load(open(f)).get("bench_labels", {}).get(kernel)
