@@ -55,6 +55,9 @@ typedef struct {
      * h1 cm2 col, h2 cm2 col, dim) quintuples; h1/h2 are computed after step2 */
     uint32_t n_pu;
     const uint32_t *pu;
+    /* post-Z stage-3 expressions (starks.cpp:193-208, Steps::step3_parser_first):
+     * run after calculateZ, before the stage-3 LDE + commit (may be empty) */
+    zkgpu_zxp_prog step3;
 } zkgpu_stark_info;
 
 /* allocate the HBM memory map, build the constant polynomials, their LDE and

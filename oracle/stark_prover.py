@@ -126,6 +126,9 @@ class OracleStark:
             ok = oc.lib().oc_calculate_z(_p(zc), 3, _p(num), 3, _p(den), 3, N)
             assert ok, "calculateZ: product does not close"
             S[2][:, z_c:z_c + 3] = zc
+        # step3: post-Z expressions (starks.cpp:193-208)
+        if "step3" in inst.programs and inst.programs["step3"].instr:
+            self.run(inst.programs["step3"], ch, np.zeros(3, np.uint64))
         S[7] = oc.extend_pol(S[2], NE)
         trees.append((oc.merkletree(S[7]), S[7]))
         roots.append(trees[-1][0][-4:].copy())

@@ -25,12 +25,14 @@ def oracle_proof(inst):
     return o, o.prove()
 
 
-@pytest.mark.parametrize("n_bits,blow,t,m,q", [(8, 1, 4, 2, 8), (10, 1, 6, 3, 16), (9, 2, 3, 1, 12),
-                                               (12, 1, 10, 4, 32), (13, 1, 4, 2, 24)])
-def test_full_proof_bit_exact(oracle, zkgpu, n_bits, blow, t, m, q):
+@pytest.mark.parametrize("n_bits,blow,t,m,q,q_deg", [(8, 1, 4, 2, 8, 2), (10, 1, 6, 3, 16, 2), (9, 2, 3, 1, 12, 2),
+                                                     (12, 1, 10, 4, 32, 2), (13, 1, 4, 2, 24, 2),
+                                                     (10, 2, 4, 2, 16, 4), (9, 3, 3, 1, 12, 7)])
+def test_full_proof_bit_exact(oracle, zkgpu, n_bits, blow, t, m, q, q_deg):
+    """q_deg > 2 (blowup 2^2 / 2^3): qq2 holds 3*q_deg columns (starks.cpp:233)."""
     from zkgpu.synthetic import SyntheticStark
     from zkgpu.stark import GpuStark
-    inst = SyntheticStark(n_bits=n_bits, blowup_bits=blow, t=t, m=m, n_queries=q)
+    inst = SyntheticStark(n_bits=n_bits, blowup_bits=blow, t=t, m=m, n_queries=q, q_deg=q_deg)
     o, ref = oracle_proof(inst)
     g = GpuStark(inst)
     assert np.array_equal(g.verkey(), o.verkey)
@@ -43,6 +45,25 @@ def test_full_proof_bit_exact(oracle, zkgpu, n_bits, blow, t, m, q):
     assert bad["s0"] == bad["fri_tree"] == bad["fold"] == bad["final"] == 0
     timers = g.timers()
     assert "STARK_STEP_1_LDE" in timers and timers["STARK_TOTAL"] > 0
+    g.close()
+
+
+def test_config4_shape_bit_exact(oracle, zkgpu):
+    """The benchmarked config-4 instance shape (bench.stark_instance: 100 cm1
+    columns, 2 plookups, post-Z step3, 128 queries, FRI steps nBitsExt, -4, ...)
+    at 2^16 rows: GPU proof == oracle proof, and it verifies."""
+    from bench import stark_instance
+    from zkgpu.stark import GpuStark
+    inst = stark_instance(16, 1, 100, 128)
+    assert len(inst.fri_steps) >= 3 and inst.n_cm1 == 100 and inst.n_queries == 128
+    o, ref = oracle_proof(inst)
+    g = GpuStark(inst)
+    g.witness()
+    got = g.prove()
+    for k in ref:
+        assert got[k] == ref[k], k
+    bad, _, _ = verify_fri(oracle, got, g.verkey(), g.publics(), inst.fri_steps, inst.n_queries)
+    assert bad["s0"] == bad["fri_tree"] == bad["fold"] == bad["final"] == 0
     g.close()
 
 

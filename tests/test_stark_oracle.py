@@ -14,10 +14,10 @@ from golden_replay import arr, verify_fri
 P = 0xFFFFFFFF00000001
 
 
-def make(n_bits=8, blow=1, t=4, m=2, n_k=3, q=8, seed=0x5EED):
+def make(n_bits=8, blow=1, t=4, m=2, n_k=3, q=8, seed=0x5EED, q_deg=2):
     from zkgpu.synthetic import SyntheticStark
     from oracle.stark_prover import OracleStark
-    inst = SyntheticStark(n_bits=n_bits, blowup_bits=blow, t=t, m=m, n_k=n_k, n_queries=q, seed=seed)
+    inst = SyntheticStark(n_bits=n_bits, blowup_bits=blow, t=t, m=m, n_k=n_k, n_queries=q, seed=seed, q_deg=q_deg)
     o = OracleStark(inst)
     o.witness()
     return inst, o, o.prove()
@@ -79,6 +79,9 @@ def quotient_identity(inst, proof, ch):
         r = m3(m3(add3(E(S.SEC_CM2_2NS, 3 * j, 1), gamma), beta), E(S.SEC_CM3_2NS, 3 * j, 1))
         s = m3(m3(add3(E(S.SEC_CM2_2NS, 3 * j, 0), gamma), beta), E(S.SEC_CM3_2NS, 3 * j, 0))
         cons.append(sub3(r, s))
+    if inst.with_step3:  # W - (Z_0 a_0 + K_0), W written by step3 after calculateZ
+        w = add3(m3(E(S.SEC_CM3_2NS, inst.z_ctx[0][2]), E(S.SEC_CM1_2NS, 0)), E(S.SEC_CONST_2NS, 0))
+        cons.append(sub3(E(S.SEC_CM3_2NS, inst.cm3_w), w))
     # plookups (pil-stark Plookup): L_first (Z - 1); Z' den - Z num
     one = [1, 0, 0]
     ob = add3(beta, one)
@@ -113,9 +116,12 @@ def quotient_identity(inst, proof, ch):
     return C == m3(zh, acc)
 
 
-@pytest.mark.parametrize("n_bits,blow,t,m", [(8, 1, 4, 2), (9, 2, 3, 1), (10, 1, 6, 3)])
-def test_synthetic_proof_is_valid(oracle, n_bits, blow, t, m):
-    inst, o, proof = make(n_bits=n_bits, blow=blow, t=t, m=m)
+@pytest.mark.parametrize("n_bits,blow,t,m,q_deg", [(8, 1, 4, 2, 2), (9, 2, 3, 1, 2), (10, 1, 6, 3, 2),
+                                                   (8, 2, 3, 2, 4), (8, 3, 2, 1, 5)])
+def test_synthetic_proof_is_valid(oracle, n_bits, blow, t, m, q_deg):
+    """q_deg > 2 (blowup 2^2, 2^3): the quotient split writes q_deg pieces,
+    the ones above the constraint degree are zero polynomials."""
+    inst, o, proof = make(n_bits=n_bits, blow=blow, t=t, m=m, q_deg=q_deg)
     bad, ys, ch = verify_fri(oracle, proof, o.verkey, o.publics, inst.fri_steps, inst.n_queries)
     assert bad["s0"] == 0 and bad["fri_tree"] == 0 and bad["fold"] == 0 and bad["final"] == 0, bad
     # challenges re-derived by the verifier equal the prover's

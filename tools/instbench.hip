@@ -1,5 +1,6 @@
-// Integer-instruction throughput on gfx950 (wave64), for choosing the field
-// arithmetic formulation.  8 independent chains per thread, inline asm pins
+// Integer-instruction issue cost on gfx950 (wave64) at 1/2/4/8 waves per SIMD:
+// the VALU peak that bench.py prices the field kernels against, and the
+// basis for choosing the field arithmetic formulation.  8 independent chains per thread, inline asm pins
 // the instruction.  Reports instructions/cycle/CU at the measured clock-free
 // rate (ops per second / 256 CUs / 2.4e9).
 // Build: hipcc -O3 --offload-arch=gfx950 -o build/instbench tools/instbench.hip
@@ -123,36 +124,178 @@ __global__ void k_bfi(uint64_t *out, int iters)
     out[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
 
+
+__global__ void k_add_co(uint64_t *out, int iters)
+{
+    uint32_t a = threadIdx.x + 3;
+    uint32_t c[8];
+    for (int k = 0; k < 8; k++) c[k] = a * (k + 1);
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) asm volatile("v_add_co_u32 %0, s[100:101], %0, %1" : "+v"(c[k]) : "v"(a) : "s100", "s101");
+    }
+    uint64_t r = 0;
+    for (int k = 0; k < 8; k++) r ^= c[k];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+
+// v_addc_co_u32 reads a carry-in SGPR pair written once outside the loop
+__global__ void k_addc_co(uint64_t *out, int iters)
+{
+    uint32_t a = threadIdx.x + 3;
+    uint32_t c[8];
+    for (int k = 0; k < 8; k++) c[k] = a * (k + 1);
+    asm volatile("s_mov_b64 s[96:97], 0" ::: "s96", "s97");
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            asm volatile("v_addc_co_u32 %0, s[100:101], %0, %1, s[96:97]" : "+v"(c[k]) : "v"(a) : "s100", "s101");
+    }
+    uint64_t r = 0;
+    for (int k = 0; k < 8; k++) r ^= c[k];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+
+__global__ void k_cndmask(uint64_t *out, int iters)
+{
+    uint32_t a = threadIdx.x + 3;
+    uint32_t c[8];
+    for (int k = 0; k < 8; k++) c[k] = a * (k + 1);
+    asm volatile("s_mov_b64 s[96:97], 0x5555" ::: "s96", "s97");
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[96:97]" : "+v"(c[k]) : "v"(a));
+    }
+    uint64_t r = 0;
+    for (int k = 0; k < 8; k++) r ^= c[k];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+
+__global__ void k_lshl64(uint64_t *out, int iters)
+{
+    uint64_t a = threadIdx.x + 3;
+    uint64_t c[8];
+    for (int k = 0; k < 8; k++) c[k] = a * (k + 1);
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) asm volatile("v_lshlrev_b64 %0, 3, %0" : "+v"(c[k]));
+    }
+    uint64_t r = 0;
+    for (int k = 0; k < 8; k++) r ^= c[k];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+
+__global__ void k_snop(uint64_t *out, int iters)
+{
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) asm volatile("s_nop 0");
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = iters;
+}
+
+__global__ void k_sub_co(uint64_t *out, int iters)
+{
+    uint32_t a = threadIdx.x + 3;
+    uint32_t c[8];
+    for (int k = 0; k < 8; k++) c[k] = a * (k + 1);
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) asm volatile("v_sub_co_u32 %0, s[100:101], %0, %1" : "+v"(c[k]) : "v"(a) : "s100", "s101");
+    }
+    uint64_t r = 0;
+    for (int k = 0; k < 8; k++) r ^= c[k];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+
+__global__ void k_subbrev_co(uint64_t *out, int iters)
+{
+    uint32_t a = threadIdx.x + 3;
+    uint32_t c[8];
+    for (int k = 0; k < 8; k++) c[k] = a * (k + 1);
+    asm volatile("s_mov_b64 s[96:97], 0" ::: "s96", "s97");
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            asm volatile("v_subbrev_co_u32 %0, s[100:101], %0, %1, s[96:97]" : "+v"(c[k]) : "v"(a) : "s100", "s101");
+    }
+    uint64_t r = 0;
+    for (int k = 0; k < 8; k++) r ^= c[k];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+
+__global__ void k_mov(uint64_t *out, int iters)
+{
+    uint32_t a = threadIdx.x + 3;
+    uint32_t c[8];
+    for (int k = 0; k < 8; k++) c[k] = a * (k + 1);
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) asm volatile("v_mov_b32 %0, %1" : "=v"(c[k]) : "v"(c[(k + 1) & 7]));
+    }
+    uint64_t r = 0;
+    for (int k = 0; k < 8; k++) r ^= c[k];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+
+__global__ void k_cmp_gt64(uint64_t *out, int iters)
+{
+    uint64_t a = threadIdx.x + 3;
+    uint64_t c[8];
+    for (int k = 0; k < 8; k++) c[k] = a * (k + 7);
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) asm volatile("v_cmp_gt_u64 vcc, %0, %1" ::"v"(c[k]), "v"(a) : "vcc");
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = c[0];
+}
+
 typedef void (*kfn)(uint64_t *, int);
 
 int main()
 {
+    // Issue cost per wave64 instruction per SIMD at W waves per SIMD: 256
+    // threads per workgroup (one wave per SIMD), 256*W workgroups (W per CU).
+    // cycles/instr = SIMDs * clock / (wave-instructions per second), priced
+    // at the nominal 2.4 GHz and, clock-free, relative to v_add_u32 at the
+    // same W (the guide's 2-cycle reference instruction at >= 2 waves/SIMD).
     uint64_t *out;
-    (void)hipMalloc(&out, 2048 * 256 * 8);
+    (void)hipMalloc(&out, 256ull * 16 * 256 * 8);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     struct {
         const char *name;
         kfn f;
-    } ks[] = {{"v_mad_u64_u32", k_mad_u64_u32}, {"v_mad_u32_u24", k_mad_u32_u24}, {"v_mul_lo_u32", k_mul_lo_u32},
-              {"v_mul_hi_u32", k_mul_hi_u32},   {"v_lshl_add_u64", k_add64},     {"v_add_u32", k_add32},
-              {"v_cmp_lt_u64", k_cmp64},        {"v_bfi_b32", k_bfi}};
-    for (int rep = 0; rep < 2; rep++) {
+    } ks[] = {{"v_add_u32", k_add32},        {"v_mad_u64_u32", k_mad_u64_u32}, {"v_add_co_u32", k_add_co},
+              {"v_addc_co_u32", k_addc_co},   {"v_cndmask_b32", k_cndmask},     {"v_lshlrev_b64", k_lshl64},
+              {"v_lshl_add_u64", k_add64},    {"v_mad_u32_u24", k_mad_u32_u24}, {"v_mul_lo_u32", k_mul_lo_u32},
+              {"v_mul_hi_u32", k_mul_hi_u32}, {"v_cmp_lt_u64", k_cmp64},        {"v_bfi_b32", k_bfi},
+              {"v_sub_co_u32", k_sub_co},     {"v_subbrev_co_u32", k_subbrev_co}, {"v_mov_b32", k_mov},
+              {"v_cmp_gt_u64", k_cmp_gt64},   {"s_nop 0", k_snop}};
+    const int waves[] = {1, 2, 4, 8};
+    printf("{\"unit\": \"cycles per wave64 instruction per SIMD\", \"clock_GHz\": 2.4, \"rows\": [\n");
+    bool first = true;
+    for (int w : waves) {
+        double ref = 0;
         for (auto &k : ks) {
-            hipLaunchKernelGGL(k.f, dim3(2048), dim3(256), 0, 0, out, ITERS);
+            const int blocks = 256 * w;
+            hipLaunchKernelGGL(k.f, dim3(blocks), dim3(256), 0, 0, out, ITERS);
             (void)hipEventRecord(e0);
-            hipLaunchKernelGGL(k.f, dim3(2048), dim3(256), 0, 0, out, ITERS);
+            for (int r = 0; r < 4; r++) hipLaunchKernelGGL(k.f, dim3(blocks), dim3(256), 0, 0, out, ITERS);
             (void)hipEventRecord(e1);
             (void)hipEventSynchronize(e1);
             float ms;
             (void)hipEventElapsedTime(&ms, e0, e1);
-            double ops = 2048.0 * 256 * ITERS * 8;  // lane-instructions
-            double rate = ops / (ms * 1e-3);
-            if (rep)
-                printf("%-16s %8.2f T lane-op/s  = %.2f lane-op/clk/CU @2.4GHz (full rate = 128)\n", k.name,
-                       rate / 1e12, rate / 256 / 2.4e9);
+            const double winstr = 4.0 * blocks * 4 * (double)ITERS * 8;  // wave-instructions
+            const double cyc = 1024.0 * 2.4e9 / (winstr / (ms * 1e-3));
+            if (k.f == k_add32) ref = cyc;
+            printf("%s  {\"instr\": \"%s\", \"waves_per_simd\": %d, \"cycles_at_2p4GHz\": %.3f, "
+                   "\"rel_v_add_u32_x2\": %.3f}",
+                   first ? "" : ",\n", k.name, w, cyc, cyc / ref * 2.0);
+            first = false;
         }
     }
+    printf("\n]}\n");
     return 0;
 }

@@ -28,9 +28,9 @@ def per_kernel(path, counter):
 def bench_label(name):
     """rocprof kernel name -> the label bench.py / zkgpu_prof_* use."""
     base = name.split("(")[0].replace("void ", "").replace("zk::", "").strip()
-    m = re.match(r"k_ntt_pass<(\d+), (\d+),", base)
+    m = re.match(r"k_ntt_pass<(\d+), (\d+), (true|false)", base)
     if m:
-        return "k_ntt_pass<%d>" % (int(m.group(1)) + int(m.group(2)))
+        return "k_ntt_pass<%d,%s>" % (int(m.group(1)) + int(m.group(2)), "inv" if m.group(3) == "true" else "fwd")
     return base
 
 
@@ -79,12 +79,13 @@ def main():
     for lab, (n, tot) in valu.items():
         labels.setdefault(lab, {})["valu_wave_instr_per_launch"] = tot / n
     meta = {"_doc": "per-launch HBM traffic = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE half-count "
-                    "correction, MI355X_MICROARCH.md HBM); separate --pmc passes of `python3 bench.py --no-cpu "
+                    "correction, MI355X_MICROARCH.md HBM); separate --pmc passes of `python3 bench.py --workload lde --no-cpu "
                     "--steps 2 --warmup 1`; valu_wave_instr_per_launch = SQ_INSTS_VALU (wave instructions) from a separate SQ pass",
             "kernels": out, "bench_labels": labels}
-    with open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w") as f:
+    with open(os.path.join(dst, f"{tag}_lde_pmc.json"), "w") as f:
         json.dump(meta, f, indent=1)
-    shutil.copy(os.path.join(src, "prof/run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    if os.path.exists(os.path.join(src, "prof/run_kernel_stats.csv")):
+        shutil.copy(os.path.join(src, "prof/run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
     if os.path.exists(os.path.join(src, "prof_bench.json")):
         shutil.copy(os.path.join(src, "prof_bench.json"), os.path.join(dst, f"{tag}_prof_bench.json"))
     print(json.dumps(meta, indent=1)[:2000])

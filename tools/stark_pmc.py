@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-kernel summary of a 2^23 STARK proof under PMC (tools/gpu_job.sh starkpmc):
-time, VALU issue rate (SQ_INSTS_VALU / time vs 614 G wave-instr/s) and HBM
+time, VALU wave-instructions (SQ_INSTS_VALU) and HBM
 bytes/s ((2*FETCH_SIZE + WRITE_SIZE) * 1024, MI355X_MICROARCH.md gfx950
 correction), from three separate --pmc passes.  Times come from the SQ pass's
 kernel trace (PMC serialises kernels, so they are slightly inflated).
@@ -13,7 +13,6 @@ import glob
 import json
 import sys
 
-PEAK_VALU = 614.4e9
 
 
 def counters(d):
@@ -44,11 +43,14 @@ def main():
         valu = sq.get(k, {}).get("SQ_INSTS_VALU", 0.0)
         hbm = 2 * fe.get(k, {}).get("FETCH_SIZE", 0.0) * 1024 + wr.get(k, {}).get("WRITE_SIZE", 0.0) * 1024
         name = k.split("(")[0].replace("void ", "").replace("zk::", "")
-        res[name] = {"launches": n, "ms": round(sec * 1e3, 3), "valu_frac": round(valu / sec / PEAK_VALU, 3),
-                     "hbm_GBps": round(hbm / sec / 1e9, 1), "hbm_GB": round(hbm / 1e9, 3)}
+        res[name] = {"launches": n, "ms": round(sec * 1e3, 3), "valu_wave_instr_per_launch": valu / n,
+                     "valu_G_per_s": round(valu / sec / 1e9, 1),
+                     "hbm_GBps": round(hbm / sec / 1e9, 1), "hbm_GB": round(hbm / 1e9, 3),
+                     "hbm_bytes_per_launch": hbm / n}
     res = dict(sorted(res.items(), key=lambda kv: -kv[1]["ms"]))
     doc = {"_doc": "one 2^23 config-4 STARK proof (bench.py --workload stark --steps 1 --warmup 0) under rocprofv3 "
-                   "--pmc in three passes; valu_frac = SQ_INSTS_VALU / kernel time / 614.4 G wave-instr/s; "
+                   "--pmc in three passes; valu_wave_instr_per_launch = SQ_INSTS_VALU / launches (bench.py prices it against "
+                   "the measured issue peak, profiles/*_instbench.json x *_valu_mix.json); "
                    "hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024 bytes",
            "kernels": res}
     json.dump(doc, open(out, "w"), indent=1)

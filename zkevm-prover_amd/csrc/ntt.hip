@@ -421,8 +421,13 @@ static const uint64_t *otw_table(Ctx &ctx, int d, uint32_t logm, uint32_t logr, 
     return p;
 }
 
-static const char *PASS_NAMES[9] = {"", "", "", "", "k_ntt_pass<4>", "k_ntt_pass<5>",
-                                     "k_ntt_pass<6>", "k_ntt_pass<7>", "k_ntt_pass<8>"};
+// live-profiling labels: radix and direction (the forward and inverse
+// instantiations are different kernels with different traffic)
+static const char *PASS_NAMES[2][9] = {
+    {"", "", "", "", "k_ntt_pass<4,fwd>", "k_ntt_pass<5,fwd>", "k_ntt_pass<6,fwd>", "k_ntt_pass<7,fwd>",
+     "k_ntt_pass<8,fwd>"},
+    {"", "", "", "", "k_ntt_pass<4,inv>", "k_ntt_pass<5,inv>", "k_ntt_pass<6,inv>", "k_ntt_pass<7,inv>",
+     "k_ntt_pass<8,inv>"}};
 
 static void split_radix(uint32_t logn, uint32_t *npass, uint32_t rbits[NTT_MAX_PASSES])
 {
@@ -549,7 +554,7 @@ int ntt_columns(Ctx &ctx, uint64_t *dst, uint64_t dst_ld, const uint64_t *src, u
             b.ncols = (uint32_t)nc;
             prof_begin(s);
             dispatch_pass(rb, b, nc, inverse, s);
-            prof_end(PASS_NAMES[rb], 8.0 * (double)(nread + n) * (double)nc, s);
+            prof_end(PASS_NAMES[d][rb], 8.0 * (double)(nread + n) * (double)nc, s);
         }
         logm -= rb;
     }

@@ -154,7 +154,7 @@ public:
     zkgpu_stark_info info;
     std::vector<uint32_t> random_cols, zctx, ev, random_const, pu;
     std::vector<uint32_t> fri_steps;
-    Prog step0, step1, step2, step3prev, step42ns, step52ns;
+    Prog step0, step1, step2, step3prev, step3, step42ns, step52ns;
     uint64_t N = 0, NE = 0;
     uint32_t eb = 0;
     zkgpu_sections S;
@@ -186,6 +186,10 @@ public:
     {
         info = *in;
         random_cols.assign(in->random_cols, in->random_cols + in->n_random_cols);
+        if (in->n_bits_ext < in->n_bits || in->n_bits_ext > 28 || in->n_fri_steps == 0 || in->n_fri_steps > 32 ||
+            in->fri_steps[0] != in->n_bits_ext || in->q_deg == 0 || in->q_deg * 3 != in->n_cm4 ||
+            ((uint64_t)in->q_deg << in->n_bits) > (1ULL << in->n_bits_ext) || in->l_first >= in->n_const)
+            return fail("stark_create: inconsistent instance description");
         zctx.assign(in->zctx, in->zctx + 3 * in->n_zctx);
         ev.assign(in->ev, in->ev + 4 * in->n_ev);
         fri_steps.assign(in->fri_steps, in->fri_steps + in->n_fri_steps);
@@ -203,16 +207,29 @@ public:
         }
         for (uint32_t c : random_const)
             if (c >= in->n_const) return fail("stark_create: random const column %u out of range", c);
+        for (uint32_t c : random_cols)
+            if (c >= in->n_cm1) return fail("stark_create: random cm1 column %u out of range", c);
+        for (uint32_t z = 0; z < in->n_zctx; z++)
+            if (zctx[3 * z] + 3 > in->n_tmp || zctx[3 * z + 1] + 3 > in->n_tmp || zctx[3 * z + 2] + 3 > in->n_cm3)
+                return fail("stark_create: grand product %u out of range", z);
+        {
+            // evMap (section_2ns, col, dim, prime): starks.cpp:556-669 reads
+            // pol_e[k << eb] of a 2ns section, col + dim <= its width
+            const uint32_t widths_ev[5] = {in->n_cm1, in->n_cm2, in->n_cm3, in->n_cm4, in->n_const};
+            for (uint32_t e = 0; e < in->n_ev; e++) {
+                const uint32_t *q = &ev[4 * e];
+                if (q[0] < SEC_CM1_2NS || q[0] > SEC_CONST_2NS || (q[2] != 1 && q[2] != 3) || q[3] > 1 ||
+                    q[1] + q[2] > widths_ev[q[0] - SEC_CM1_2NS])
+                    return fail("stark_create: evMap entry %u out of range", e);
+            }
+        }
         step0.set(in->step0);
         step1.set(in->step1);
         step2.set(in->step2);
         step3prev.set(in->step3prev);
+        step3.set(in->step3);
         step42ns.set(in->step42ns);
         step52ns.set(in->step52ns);
-        if (in->n_bits_ext < in->n_bits || in->n_bits_ext > 28 || in->n_fri_steps == 0 || in->n_fri_steps > 32 ||
-            in->fri_steps[0] != in->n_bits_ext || in->q_deg * 3 != in->n_cm4 ||
-            ((uint64_t)in->q_deg << in->n_bits) > (1ULL << in->n_bits_ext))
-            return fail("stark_create: inconsistent instance description");
         for (uint32_t si = 1; si < in->n_fri_steps; si++)
             if (in->fri_steps[si] >= in->fri_steps[si - 1] || in->fri_steps[si - 1] - in->fri_steps[si] > 5)
                 return fail("stark_create: FRI steps must decrease by 1..5 bits");
@@ -236,7 +253,7 @@ public:
         uint64_t tn = zkgpu_gl_merkle_num_elements(NE);
         for (int t = 0; t < 4; t++)
             if (dalloc(&nodes[t], tn)) return -1;
-        if (dalloc(&const_nodes, tn) || dalloc(&qq1, 3 * NE) || dalloc(&qq2, 6 * NE) ||
+        if (dalloc(&const_nodes, tn) || dalloc(&qq1, 3 * NE) || dalloc(&qq2, (uint64_t)info.n_cm4 * NE) ||
             dalloc(&cm4_n, (uint64_t)(info.n_cm4 ? info.n_cm4 : 1) * N) || dalloc(&lev, 3 * N) ||
             dalloc(&lpev, 3 * N) || dalloc(&xdiv, 3 * NE) || dalloc(&xdivw, 3 * NE) || dalloc(&fri_pol[0], 3 * NE) ||
             dalloc(&fri_pol[1], 3 * NE))
@@ -390,6 +407,12 @@ public:
             if (!closes) return fail("calculateZ: grand product %u does not close", z);
         }
         if (tstop("STARK_STEP_3_CALCULATE_Z")) return -1;
+        // step3: post-Z expressions (starks.cpp:193-208)
+        if (!step3.instr.empty()) {
+            tstart();
+            if (run(step3, false, ch, evals.data(), 0)) return -1;
+            if (tstop("STARK_STEP_3_CALCULATE_EXPS_2")) return -1;
+        }
         if (commit(2, SEC_CM3_N, SEC_CM3_2NS, info.n_cm3, tr, roots[2], "STARK_STEP_3_LDE", "STARK_STEP_3_MERKLETREE"))
             return -1;
         // STAGE 4 (:226-296)
@@ -399,7 +422,7 @@ public:
         if (tstop("STARK_STEP_4_CALCULATE_EXPS_2NS")) return -1;
         tstart();
         CK(zkgpu_gl_ntt_dev(qq1, NE, S.sec[SEC_Q_2NS], NE, NE, 3, 1));
-        CK(zkgpu_memset_dev(qq2, 0, 6 * NE * 8));
+        CK(zkgpu_memset_dev(qq2, 0, (uint64_t)info.n_cm4 * NE * 8));
         uint64_t shift_in = pw(inv(7), N);
         CK(zkgpu_qsplit_dev(qq2, NE, qq1, NE, N, info.q_deg, shift_in));
         CK(zkgpu_gl_ntt_dev(S.sec[SEC_CM4_2NS], NE, qq2, NE, NE, info.n_cm4, 0));
@@ -448,7 +471,6 @@ public:
                 const uint64_t *base = sec == SEC_CM4_2NS ? cm4_n
                                        : sec == SEC_CONST_2NS ? S.sec[SEC_CONST_N]
                                                               : S.sec[sec - SEC_CM1_2NS + SEC_CM1_N];
-                if (sec < SEC_CM1_2NS || sec > SEC_CONST_2NS) return fail("evMap entry %u: section %u", e, sec);
                 cols[e] = base + (uint64_t)ev[4 * e + 1] * N;
                 lds[e] = N;
                 dims[e] = ev[4 * e + 2];

@@ -280,6 +280,8 @@ class ShardedStark:
         for num_c, den_c, z_c in inst.z_ctx:
             if not k.calculate_z(S[2][z_c:z_c + 3], S[3][num_c:num_c + 3], S[3][den_c:den_c + 3], N):
                 raise ValueError("calculateZ: the grand product does not close")
+        if "step3" in inst.programs and inst.programs["step3"].instr:
+            k.zxp(inst.programs["step3"], self._secs_n(), nb, ch, self.publics, eb=eb)  # starks.cpp:193
         c3, root3 = self._commit(2, inst.n_cm3)
         t.put(root3)
         lap("STARK_STEP_3")

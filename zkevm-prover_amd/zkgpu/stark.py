@@ -34,7 +34,7 @@ class _Info(ctypes.Structure):
                 ("n_ev", ctypes.c_uint32), ("ev", ctypes.c_void_p),
                 ("step1", _Prog), ("step2", _Prog), ("step3prev", _Prog), ("step42ns", _Prog), ("step52ns", _Prog),
                 ("n_random_const", ctypes.c_uint32), ("random_const", ctypes.c_void_p), ("step0", _Prog),
-                ("n_pu", ctypes.c_uint32), ("pu", ctypes.c_void_p)]
+                ("n_pu", ctypes.c_uint32), ("pu", ctypes.c_void_p), ("step3", _Prog)]
 
 
 _slib = None
@@ -95,8 +95,10 @@ class GpuStark:
         info.n_random_cols, info.random_cols = rc.size, rc.ctypes.data
         info.n_zctx, info.zctx = len(inst.z_ctx), zc.ctypes.data
         info.n_ev, info.ev = len(inst.evmap), ev.ctypes.data
-        for name in ("step0", "step1", "step2", "step3prev", "step42ns", "step52ns"):
-            prog = inst.programs[name]
+        for name in ("step0", "step1", "step2", "step3prev", "step3", "step42ns", "step52ns"):
+            prog = inst.programs.get(name)
+            if prog is None:
+                continue
             ins, opn = prog.arrays()
             ins, opn = np.ascontiguousarray(ins), np.ascontiguousarray(opn)
             self._keep += [ins, opn]

@@ -101,7 +101,7 @@ class Program:
 
 class SyntheticStark:
     def __init__(self, n_bits=10, blowup_bits=1, t=4, m=2, n_k=3, n_queries=16, fri_steps=None, n_publics=8,
-                 seed=0x5EED, n_free=0, n_lookups=2):
+                 seed=0x5EED, n_free=0, n_lookups=2, q_deg=2, with_step3=True):
         self.n_bits = n_bits
         self.n_bits_ext = n_bits + blowup_bits
         self.blowup_bits = blowup_bits
@@ -129,9 +129,17 @@ class SyntheticStark:
             tmp += 2 * d + 6
             cm3 += 3
         self.n_cm2 = cm2
-        self.n_cm3 = cm3
+        # post-Z stage-3 column (starks.cpp:193-208: step3 runs after calculateZ
+        # and writes cm3/tmpExp columns that depend on Z): W = Z_0 * a_0 + K_0
+        # (an F_p^3 column: the verifier only sees whole evaluations of Z)
+        self.with_step3 = bool(with_step3)
+        self.cm3_w = cm3 if self.with_step3 else None
+        self.n_cm3 = cm3 + (3 if self.with_step3 else 0)
         self.n_tmp = tmp
-        self.q_deg, self.q_dim = 2, 3
+        # quotient pieces: the constraints have degree <= 3, so pieces >= 2 are
+        # zero polynomials; q_deg > 2 (blowup >= 4) still exercises the split
+        assert 2 <= q_deg <= (1 << blowup_bits)
+        self.q_deg, self.q_dim = q_deg, 3
         self.n_cm4 = self.q_deg * self.q_dim
         self.n_queries = n_queries
         self.n_publics = n_publics
@@ -155,6 +163,7 @@ class SyntheticStark:
             "step1": self._prog_step1(),
             "step2": self._prog_step2(),
             "step3prev": self._prog_step3prev(),
+            "step3": self._prog_step3(),
             "step42ns": self._prog_step42ns(),
             "step52ns": self._prog_step52ns(),
         }
@@ -183,6 +192,8 @@ class SyntheticStark:
         for lk in self.lookups:
             ev.append((SEC_CM3_2NS, lk["z"], 3, 0))
             ev.append((SEC_CM3_2NS, lk["z"], 3, 1))
+        if self.with_step3:
+            ev.append((SEC_CM3_2NS, self.cm3_w, 3, 0))
         for p in range(self.q_deg):
             ev.append((SEC_CM4_2NS, 3 * p, 3, 0))
         self.evmap = ev
@@ -316,6 +327,17 @@ class SyntheticStark:
                                   p.col3(SEC_TMP_N, lk["den"]))
         return p
 
+    def _prog_step3(self):
+        """Post-Z stage-3 expressions (starks.cpp:193): W = Z_0 * a_0 + K_0."""
+        p = Program(0)
+        if not self.with_step3:
+            return p
+        t = p.tmp3()
+        z0 = self.z_ctx[0][2]
+        p.op(MUL, t, p.col3(SEC_CM3_N, z0), p.col(SEC_CM1_N, 0))
+        p.op(ADD, p.col3(SEC_CM3_N, self.cm3_w), t, p.col(SEC_CONST_N, 0))
+        return p
+
     def constraints(self, p, nxt):
         """Yield (emit_fn) for each constraint; each writes its value into a
         fresh temp and returns it.  nxt = row shift of "next row"."""
@@ -358,6 +380,14 @@ class SyntheticStark:
                 p.op(SUB, r, r, s)
                 return r
             out.append(c_z)
+        if self.with_step3:
+            def c_w():
+                r = p.tmp3()
+                p.op(MUL, r, p.col3(SEC_CM3_2NS, self.z_ctx[0][2]), p.col(SEC_CM1_2NS, 0))
+                p.op(ADD, r, r, p.col(SEC_CONST_2NS, 0))
+                p.op(SUB, r, p.col3(SEC_CM3_2NS, self.cm3_w), r)
+                return r
+            out.append(c_w)
         for k, lk in enumerate(self.lookups):
             def c_lk_first(lk=lk):
                 r = p.tmp3()
@@ -407,6 +437,8 @@ class SyntheticStark:
             cols += [(SEC_CM2_2NS, lk["h1"], lk["dim"]), (SEC_CM2_2NS, lk["h2"], lk["dim"])]
         cols += [(SEC_CM3_2NS, 3 * j, 3) for j in range(self.m)]
         cols += [(SEC_CM3_2NS, lk["z"], 3) for lk in self.lookups]
+        if self.with_step3:
+            cols += [(SEC_CM3_2NS, self.cm3_w, 3)]
         cols += [(SEC_CM4_2NS, 3 * q, 3) for q in range(self.q_deg)]
         return cols
 
