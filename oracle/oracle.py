@@ -69,6 +69,9 @@ def lib():
                                    ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                    ctypes.c_void_p, u64, ptr, ptr, ptr, ptr, ptr, ptr, ptr, u64]),
             "oc_calculate_z": (ctypes.c_int, [ptr, u64, ptr, u64, ptr, u64, u64]),
+            "oc_parser_eval": (ctypes.c_int, [ctypes.c_int, ptr, u64, ptr, u64, ctypes.c_uint32, ptr, ptr,
+                                              ctypes.c_void_p, ptr, u64, u64, u64, ctypes.c_uint32, ctypes.c_uint32,
+                                              ptr, ptr, ptr, ptr, ptr, u64, ptr, ptr, ptr, ptr]),
             "oc_evmap": (None, [ptr, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, u64, ptr,
                                 ptr, u64, ctypes.c_uint32]),
             "oc_xdivxsub": (None, [ptr, ptr, ptr, u64, ptr, u64]),
@@ -276,3 +279,19 @@ def batch_inverse3(x):
     o = np.zeros_like(x)
     lib().oc_batch_inverse3(_p(o), _p(x), x.size // 3)
     return o
+
+
+def parser_eval(parser, ops, args, sections, cpols, dom, native_dom, n_tmp1, n_tmp3, challenges, publics, evals, x,
+                zhinv, xdiv=None, xdivw=None, q=None, f=None):
+    """oracle/parser.c: the reference's AVX2 bytecode case tables, one row at a
+    time.  sections: [(offset, stride, row-major uint64 array (dom x stride))]
+    of the memory map; outputs are written in place.  Returns the status."""
+    ops = np.ascontiguousarray(ops, np.uint64)
+    args = np.ascontiguousarray(args, np.uint64)
+    off = np.array([s[0] for s in sections], np.uint64)
+    stride = np.array([s[1] for s in sections], np.uint64)
+    ptrs = (ctypes.c_void_p * len(sections))(*[s[2].ctypes.data for s in sections])
+    return lib().oc_parser_eval(parser, _p(ops), ops.size, _p(args), args.size, len(sections), _p(off), _p(stride),
+                                ctypes.cast(ptrs, ctypes.c_void_p), _p(cpols), cpols.shape[1], dom, native_dom,
+                                n_tmp1, n_tmp3, _p(challenges), _p(publics), _p(evals), _p(x), _p(zhinv), zhinv.size,
+                                *[_p(a) if a is not None else None for a in (xdiv, xdivw, q, f)])

@@ -116,7 +116,9 @@ static inline void store(const env_t *e, const zxp_operand *o, uint64_t *t1, uin
         break;
     case ZXP_COL:
     case ZXP_COL3: {
-        uint64_t *p = e->sec[o->a] + i * e->stride[o->a] + o->b;
+        /* a shifted store writes row (i + shift) mod dom (parser opcodes 101-114, 119) */
+        const uint64_t row = (i + (uint64_t)(int64_t)(int32_t)o->c + e->dom) % e->dom;
+        uint64_t *p = e->sec[o->a] + row * e->stride[o->a] + o->b;
         p[0] = gl_canon(v->v[0]);
         if (o->kind == ZXP_COL3) {
             p[1] = v->dim == 3 ? gl_canon(v->v[1]) : 0;
@@ -168,6 +170,10 @@ static void zxp_run(const void *instr_v, uint32_t n_instr, const void *opnd_v, u
         uint64_t *t3 = (uint64_t *)calloc(3 * n_tmp3 + 3, sizeof(uint64_t));
 #pragma omp for schedule(static)
         for (uint64_t i = 0; i < dom; i++) {
+            /* every row starts with zero temporaries (the compiled programs'
+             * convention; the reference's step52ns zeroes tmp2 per row) */
+            memset(t1, 0, (n_tmp1 + 1) * sizeof(uint64_t));
+            memset(t3, 0, (3 * n_tmp3 + 3) * sizeof(uint64_t));
             for (uint32_t k = 0; k < n_instr; k++) {
                 const zxp_instr *in = &instr[k];
                 val a = {{0, 0, 0}, 1};

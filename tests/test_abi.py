@@ -9,8 +9,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_symbols():
-    text = open(os.path.join(ROOT, "include", "zkgpu.h")).read()
+def header_symbols(name="zkgpu.h"):
+    text = open(os.path.join(ROOT, "include", name)).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(zkgpu_\w+)\s*\(", text)))
 
@@ -20,12 +20,28 @@ def test_library_exports_every_declared_symbol():
     if not os.path.exists(zkgpu.LIB_PATH):
         zkgpu.build()
     L = ctypes.CDLL(zkgpu.LIB_PATH)
-    syms = header_symbols()
+    syms = sorted(header_symbols("zkgpu.h") + header_symbols("zkgpu_parser.h"))
     assert len(syms) >= 20
     missing = [s for s in syms if not hasattr(L, s)]
     assert not missing, missing
     # the Python binding covers the whole ABI
     assert sorted(zkgpu.exported_symbols()) == syms
+
+
+def test_stark_library_exports_every_declared_symbol():
+    """include/zkgpu_stark.h is libzkgpu_stark.so (host/starks.cpp)."""
+    import zkgpu
+    from zkgpu import stark
+    L = ctypes.CDLL(stark.STARK_LIB)
+    syms = header_symbols("zkgpu_stark.h")
+    assert len(syms) >= 8
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+
+
+def test_every_header_is_checked():
+    names = sorted(f for f in os.listdir(os.path.join(ROOT, "include")) if f.endswith(".h"))
+    assert set(names) <= {"zkgpu.h", "zkgpu_parser.h", "zkgpu_stark.h", "zkgpu_zxp.h"}, names
 
 
 def test_library_has_gfx950_code_object():

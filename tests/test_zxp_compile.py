@@ -123,10 +123,42 @@ def test_compile_rejects_bad_programs(zkgpu_host):
     p.op(ADD, p.lit(3), p.lit(4), p.lit(5))  # writes a literal
     with pytest.raises(RuntimeError):
         zkgpu_host.zxp_compile(p, np.zeros((8, 3), np.uint64), None)
+
+
+def test_shifted_store_forwarding(oracle, zkgpu_host):
+    """The reference's stage-3 parsers store a cell of the NEXT row
+    (pols[off + ((i+1) % N) * stride], step3.parser.cpp opcodes 101-114) and
+    read it back in the same row: the compiled program forwards the stored
+    value and never re-reads a cell its row wrote.  As in the reference, the
+    shifted value equals what row i+1 stores unshifted, so the parallel
+    evaluation is deterministic; compiled == source on the oracle."""
+    from zkgpu.synthetic import Program, ADD, SUB, MUL, COPY, SEC_CM1_N, SEC_TMP_N
+    import zkgpu.synthetic as S
     p = Program(0)
-    p.op(ADD, p.col(0, 0, 1), p.col(0, 1), p.lit(5))  # writes a shifted column
-    with pytest.raises(RuntimeError):
-        zkgpu_host.zxp_compile(p, np.zeros((8, 3), np.uint64), None)
+    t = p.tmp1()
+    u = p.tmp3()
+    for sh in (1, 0):
+        p.op(MUL, p.col(SEC_TMP_N, 0, sh), p.col(SEC_CM1_N, 1, sh), p.col(SEC_CM1_N, 2, sh))  # tmp0 = c1 c2
+        p.op(MUL, u, p.col(SEC_TMP_N, 0, sh), p.chal(2))
+        p.op(ADD, p.col3(SEC_TMP_N, 1, sh), u, p.col(SEC_CM1_N, 3, sh))  # tmp1..3 = tmp0 ch2 + c3
+    p.op(ADD, t, p.col(SEC_TMP_N, 0, 1), p.col(SEC_TMP_N, 0))
+    p.op(SUB, p.col(SEC_TMP_N, 4), t, p.col(SEC_TMP_N, 2, 1))
+    p.op(MUL, p.col3(SEC_TMP_N, 5), p.col3(SEC_TMP_N, 1, 1), p.col3(SEC_TMP_N, 1))
+    cp = _check_program(oracle, zkgpu_host, p, {0: 6, 3: 8}, 64, 1, 1, 0, seed=11)
+    writes = {(o[1], o[2], o[3]) for (op, d, a, b) in cp["instr"] for o in [cp["opnd"][d]] if o[0] in (S.COL, S.COL3)}
+    assert (SEC_TMP_N, 0, 1) in writes and (SEC_TMP_N, 1, 1) in writes
+    srcs = []
+    for (op, d, a, b) in cp["instr"]:
+        if op in (4, 5):  # ZXP_DOT1 / ZXP_DOT3 (include/zkgpu_zxp.h)
+            srcs += [int(tm["src"]) for tm in cp["term"][a:a + b] if int(tm["src"]) != 0xFFFFFFFF]
+        else:
+            srcs += [a] if op == COPY else [a, b]
+    for x in srcs:
+        o = cp["opnd"][x]
+        if o[0] == S.COL:
+            assert (o[1], o[2], o[3]) not in writes, o
+        if o[0] == S.COL3:
+            assert all((o[1], o[2] + c, o[3]) not in writes for c in range(3)), o
 
 
 def test_column_write_hazard(oracle, zkgpu_host):

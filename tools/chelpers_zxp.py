@@ -16,7 +16,7 @@ Each statement of the `stepXX_first` body is one of
 with operands
     tmp_K
     params.pols[OFF + i*STRIDE]            params.pols[OFF + ((i + S)%M)*STRIDE]
-    params.pConstPols[2ns]->getElement(C,i)
+    params.pConstPols[2ns]->getElement(C,i)   getElement(C,(i+S)%N)
     params.challenges[K]  params.evals[K]  params.publicInputs[K]
     Goldilocks::fromU64(V)   params.x_n[i] / x_2ns[i]   params.zi.zhInv(i)
     params.xDivXSubXi[i] / xDivXSubWXi[i]  params.q_2ns[i * 3] / f_2ns[i * 3]
@@ -103,6 +103,9 @@ class Translator:
         m = re.fullmatch(r"params\.pConstPols(2ns)?->getElement\((\d+),\s*i\)", s)
         if m:
             return self.p.o(COL, SEC_CONST_2NS if m.group(1) else SEC_CONST_N, int(m.group(2)), 0)
+        m = re.fullmatch(r"params\.pConstPols(2ns)?->getElement\((\d+),\s*\(i\s*\+\s*(\d+)\)%(\d+)\)", s)
+        if m:  # constant at the next row(s): (i + S) % N
+            return self.p.o(COL, SEC_CONST_2NS if m.group(1) else SEC_CONST_N, int(m.group(2)), int(m.group(3)))
         m = re.fullmatch(r"params\.challenges\[(\d+)\]", s)
         if m:
             return self.p.chal(int(m.group(1)))

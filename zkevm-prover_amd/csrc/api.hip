@@ -947,8 +947,11 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
         z.pd = const_cast<uint64_t *>(pd);
         if (z.kd != DK_T1 && z.kd != DK_T3 && z.kd != DK_C1 && z.kd != DK_C3)
             return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u writes a read-only operand", k);
-        if ((z.kd == DK_C1 || z.kd == DK_C3) && z.id != 0)
-            return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u writes a shifted column", k);
+        // a shifted store (the reference's parser opcodes 101-114 / 119 write
+        // pols[off + ((i + s) % N) * stride], step3.parser.cpp) lands on row
+        // (i + s) mod 2^log_dom; a row block without wrap-around has no such row
+        if ((z.kd == DK_C1 || z.kd == DK_C3) && z.id != 0 && !wrap)
+            return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u writes a shifted column in a row block", k);
     }
     if (!use_jit) {  // interpreter temporaries live in LDS
         const uint64_t slots = (uint64_t)n_tmp1 + 3ULL * n_tmp3;

@@ -236,7 +236,7 @@ __global__ void __launch_bounds__(ZXP_THREADS) k_zxp_eval(ZxpEnv e)
         case DK_C1:
         case DK_C3:
             if (active) {
-                uint64_t *p = z.pd + i;
+                uint64_t *p = z.pd + ((i + (uint64_t)(int64_t)z.id) & e.rmask);
                 p[0] = gl_canon(r.v.v[0]);
                 if (z.kd == DK_C3) {
                     p[z.ldd] = r.dim == 3 ? gl_canon(r.v.v[1]) : 0;

@@ -19,8 +19,14 @@
 //
 // Hazards: forms refer to SSA temporaries (never overwritten) and to columns;
 // before an instruction stores a column, every pending form that reads that
-// column is materialised, so reads keep the source program's order.
+// column is materialised, so reads keep the source program's order.  A stored
+// value is first materialised in an SSA temporary; later reads of the same
+// (section, column, row shift) in the row use that temporary (store-to-load
+// forwarding), so no backend re-reads a cell its own row wrote -- including
+// the shifted stores of the reference's stage-3 parsers (step3prev / step3:
+// pols[off + ((i+1) % N) * stride] written, then read back, in one row).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <unordered_map>
 #include <vector>
@@ -131,6 +137,7 @@ struct Compiler {
     uint32_t n_ssa1 = 0, n_ssa3 = 0;
     std::vector<Form> st1, st3;  // current value of every source temporary
     std::vector<uint8_t> set1, set3;
+    std::unordered_map<OKey, Form, OKeyHash> fwd;  // {sec, col, shift, 0} -> value this row stored there
 
     uint32_t intern(uint32_t kind, uint32_t a, uint32_t b = 0, uint32_t c = 0)
     {
@@ -187,8 +194,27 @@ struct Compiler {
         switch (o.kind) {
         case ZXP_TMP1: return set1[o.a] ? st1[o.a] : constant(f3(0), 1, -1);
         case ZXP_TMP3: return set3[o.a] ? st3[o.a] : constant(f3(0), 3, -1);
-        case ZXP_COL: return identity(intern(ZXP_COL, o.a, o.b, o.c), 1);
+        case ZXP_COL: {
+            auto it = fwd.find(OKey{{o.a, o.b, o.c, 0}});
+            if (it != fwd.end()) return it->second;
+            return identity(intern(ZXP_COL, o.a, o.b, o.c), 1);
+        }
         case ZXP_COL3: {
+            bool any = false;
+            for (uint32_t j = 0; j < 3; j++) any |= fwd.count(OKey{{o.a, o.b + j, o.c, 0}}) != 0;
+            if (any) {  // sum_j X^j * component j (forwarded or read)
+                Form f = constant(f3(0), 3, -1);
+                for (uint32_t j = 0; j < 3; j++) {
+                    auto it = fwd.find(OKey{{o.a, o.b + j, o.c, 0}});
+                    const Form c = it != fwd.end() ? it->second : identity(intern(ZXP_COL, o.a, o.b + j, o.c), 1);
+                    F3 e = f3(0);
+                    e.v[j] = 1;
+                    f = combine(f, scale(c, e, 3), false);
+                }
+                f.dim = 3;
+                f.alias = -1;
+                return f;
+            }
             Form f;
             f.kind = FK_LIN;
             f.dim = 3;
@@ -405,8 +431,10 @@ struct Compiler {
                 const uint32_t ra = realize_src(I.a, A), rb = realize_src(I.b, B);
                 const int dim = std::max(A.dim, B.dim);
                 if (to_col) {
-                    column_hazard(D.a, D.b, D.b + (D.kind == ZXP_COL3 ? 3 : 1));
-                    instr.push_back(zxp_instr{I.op, intern(D.kind, D.a, D.b, 0), ra, rb});
+                    const int sd = (D.kind == ZXP_COL || dim == 1) ? 1 : 3;
+                    const uint32_t t = new_ssa(dim);
+                    instr.push_back(zxp_instr{I.op, t, ra, rb});
+                    store_col(D, t, sd);
                 } else {
                     const int sd = (D.kind == ZXP_TMP1 || dim == 1) ? 1 : 3;
                     const uint32_t t = new_ssa(sd);
@@ -417,12 +445,25 @@ struct Compiler {
             }
             if (to_col) {
                 if (D.kind == ZXP_COL) project1(R);
-                column_hazard(D.a, D.b, D.b + (D.kind == ZXP_COL3 ? 3 : 1));
-                const uint32_t d = intern(D.kind, D.a, D.b, 0);
-                if (R.alias >= 0 || R.kind == FK_CONST)
-                    instr.push_back(zxp_instr{ZXP_COPY, d, realize(R), 0});
-                else
-                    emit_dot(d, R);
+                if (R.kind == FK_CONST) {
+                    column_hazard(D.a, D.b, D.b + (D.kind == ZXP_COL3 ? 3 : 1));
+                    instr.push_back(zxp_instr{ZXP_COPY, intern(D.kind, D.a, D.b, D.c), realize(R), 0});
+                    for (uint32_t j = 0; j < (D.kind == ZXP_COL3 ? 3u : 1u); j++)
+                        fwd[OKey{{D.a, D.b + j, D.c, 0}}] = constant(f3(R.dim == 3 || j == 0 ? R.cst.v[j] : 0), 1, -1);
+                    continue;
+                }
+                const int rd = eff_dim(R);
+                uint32_t t;
+                if (R.alias >= 0 && ssa_kind[R.alias] == (uint8_t)rd) {
+                    t = (uint32_t)R.alias;
+                } else {
+                    t = new_ssa(rd);
+                    if (R.alias >= 0)
+                        instr.push_back(zxp_instr{ZXP_COPY, t, (uint32_t)R.alias, 0});
+                    else
+                        emit_dot(t, R);
+                }
+                store_col(D, t, rd);
                 continue;
             }
             if (D.kind == ZXP_TMP1) project1(R);
@@ -448,6 +489,27 @@ struct Compiler {
             return r;
         }
         return realize(f);
+    }
+
+    // store SSA temporary t (dimension td) into column operand D (row shift
+    // D.c) and remember its components for forwarding
+    void store_col(const zxp_operand &D, uint32_t t, int td)
+    {
+        const uint32_t w = D.kind == ZXP_COL3 ? 3 : 1;
+        column_hazard(D.a, D.b, D.b + w);
+        instr.push_back(zxp_instr{ZXP_COPY, intern(D.kind, D.a, D.b, D.c), t, 0});
+        for (uint32_t j = 0; j < w; j++) {
+            Form c;
+            if ((int)j < td) {
+                c.kind = FK_LIN;
+                c.dim = 1;
+                c.alias = td == 1 ? (int32_t)t : -1;
+                c.t.push_back(Term{t * 4 + j, f3(1)});
+            } else {
+                c = constant(f3(0), 1, -1);
+            }
+            fwd[OKey{{D.a, D.b + j, D.c, 0}}] = c;
+        }
     }
 
     void store_temp(const zxp_operand &D, Form f)
@@ -497,6 +559,133 @@ struct Compiler {
     }
 };
 
+
+// ---------------------------------------------------------------- scheduling
+// The source order of a large program can keep hundreds of values alive: the
+// reference's step42ns bytecode (zkevm.chelpers.step42ns.parser.hpp) first
+// computes every constraint value and only then folds them with the alpha
+// Horner chain (fused opcodes 84/87), so ~1,190 base + 174 extension
+// temporaries are live at once -- far beyond a GPU thread's registers.  The
+// program is a DAG: every temporary write is an SSA definition, column
+// stores are ordered sinks.  It is re-emitted sink by sink in depth-first
+// post-order, visiting the operand that needs the most registers first
+// (Sethi-Ullman), so each constraint is evaluated right before its use; on
+// the fork-9 step42ns this takes the peak from ~1,670 live words to ~100.
+// Memory order is kept: a column store follows every earlier read and store
+// of that column, a read follows the last earlier store of its column.
+// Values no sink depends on are dropped.
+struct Scheduled {
+    std::vector<zxp_instr> instr;
+    std::vector<zxp_operand> opnd;
+    uint32_t n_tmp1 = 0, n_tmp3 = 0;
+};
+
+static void schedule(const zxp_instr *in, uint32_t n_in, const zxp_operand *op, uint32_t n_opnd, uint32_t n_tmp1,
+                     uint32_t n_tmp3, Scheduled &out)
+{
+    out.opnd.assign(op, op + n_opnd);
+    // never-written temporaries read as zero: one shared zero slot per pool
+    const uint32_t zero1 = (uint32_t)out.opnd.size();
+    out.opnd.push_back(zxp_operand{ZXP_TMP1, 0, 0, 0});
+    const uint32_t zero3 = (uint32_t)out.opnd.size();
+    out.opnd.push_back(zxp_operand{ZXP_TMP3, 0, 0, 0});
+    uint32_t v1 = 1, v3 = 1;  // SSA versions (slot 0 of each pool = the zero temporary)
+    std::vector<int64_t> def1(n_tmp1, -1), def3(n_tmp3, -1);  // slot -> defining instruction
+    std::vector<uint32_t> dop(n_in);                          // instruction -> its SSA destination operand
+    std::vector<std::vector<uint32_t>> deps(n_in);
+    std::vector<zxp_instr> ren(in, in + n_in);
+    std::vector<uint8_t> width(n_in, 0), sink(n_in, 0);
+    struct ColState {
+        int64_t last_store = -1;
+        std::vector<uint32_t> reads;
+    };
+    std::unordered_map<uint64_t, ColState> cols;
+    auto colkey = [](uint32_t sec, uint32_t c) { return ((uint64_t)sec << 32) | c; };
+    for (uint32_t k = 0; k < n_in; k++) {
+        const zxp_instr &I = in[k];
+        auto use = [&](uint32_t x) -> uint32_t {
+            const zxp_operand &o = op[x];
+            if (o.kind == ZXP_TMP1 || o.kind == ZXP_TMP3) {
+                const int64_t d = o.kind == ZXP_TMP1 ? def1[o.a] : def3[o.a];
+                if (d < 0) return o.kind == ZXP_TMP1 ? zero1 : zero3;
+                deps[k].push_back((uint32_t)d);
+                return dop[d];
+            }
+            if (o.kind == ZXP_COL || o.kind == ZXP_COL3)
+                for (uint32_t c = 0; c < (o.kind == ZXP_COL3 ? 3u : 1u); c++) {
+                    ColState &cs = cols[colkey(o.a, o.b + c)];
+                    if (cs.last_store >= 0) deps[k].push_back((uint32_t)cs.last_store);
+                    cs.reads.push_back(k);
+                }
+            return x;
+        };
+        ren[k].a = use(I.a);
+        if (I.op != ZXP_COPY) ren[k].b = use(I.b);
+        const zxp_operand &D = op[I.dst];
+        if (D.kind == ZXP_TMP1 || D.kind == ZXP_TMP3) {
+            const bool t3 = D.kind == ZXP_TMP3;
+            dop[k] = (uint32_t)out.opnd.size();
+            out.opnd.push_back(zxp_operand{D.kind, t3 ? v3++ : v1++, 0, 0});
+            (t3 ? def3[D.a] : def1[D.a]) = k;
+            width[k] = t3 ? 3 : 1;
+            ren[k].dst = dop[k];
+        } else {  // column store: an ordered sink
+            sink[k] = 1;
+            for (uint32_t c = 0; c < (D.kind == ZXP_COL3 ? 3u : 1u); c++) {
+                ColState &cs = cols[colkey(D.a, D.b + c)];
+                if (cs.last_store >= 0) deps[k].push_back((uint32_t)cs.last_store);
+                for (uint32_t r : cs.reads)
+                    if (r != k) deps[k].push_back(r);
+                cs.reads.clear();
+                cs.last_store = k;
+            }
+        }
+        std::sort(deps[k].begin(), deps[k].end());
+        deps[k].erase(std::unique(deps[k].begin(), deps[k].end()), deps[k].end());
+    }
+    // register need, bottom-up (deps have smaller indices)
+    std::vector<uint32_t> need(n_in, 0);
+    std::vector<uint32_t> order;
+    for (uint32_t k = 0; k < n_in; k++) {
+        std::vector<uint32_t> &d = deps[k];
+        std::stable_sort(d.begin(), d.end(), [&](uint32_t x, uint32_t y) { return need[x] > need[y]; });
+        uint32_t held = 0, nd = width[k];
+        for (uint32_t c : d) {
+            nd = std::max(nd, held + need[c]);
+            held += width[c];
+        }
+        need[k] = nd;
+    }
+    // emit: sinks in source order, each after its unscheduled dependencies
+    // (iterative depth-first post-order, highest need first)
+    std::vector<uint8_t> done(n_in, 0);
+    std::vector<std::pair<uint32_t, uint32_t>> stack;
+    for (uint32_t s = 0; s < n_in; s++) {
+        if (!sink[s] || done[s]) continue;
+        stack.push_back({s, 0});
+        while (!stack.empty()) {
+            auto &top = stack.back();
+            const uint32_t k = top.first;
+            if (top.second < deps[k].size()) {
+                const uint32_t c = deps[k][top.second++];
+                if (!done[c]) {
+                    done[c] = 2;  // on the stack (a DAG: no cycles)
+                    stack.push_back({c, 0});
+                }
+                continue;
+            }
+            done[k] = 1;
+            order.push_back(k);
+            stack.pop_back();
+        }
+    }
+    out.instr.clear();
+    out.instr.reserve(order.size());
+    for (uint32_t k : order) out.instr.push_back(ren[k]);
+    out.n_tmp1 = v1;
+    out.n_tmp3 = v3;
+}
+
 struct Out {
     std::vector<zxp_instr> instr;
     std::vector<zxp_operand> opnd;
@@ -545,8 +734,21 @@ extern "C" int zkgpu_zxp_compile(const void *instr, uint32_t n_instr, const void
         const uint32_t dk = op[in[k].dst].kind;
         if (dk != ZXP_TMP1 && dk != ZXP_TMP3 && dk != ZXP_COL && dk != ZXP_COL3)
             return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u writes a read-only operand", k);
-        if ((dk == ZXP_COL || dk == ZXP_COL3) && op[in[k].dst].c != 0)
-            return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u writes a shifted column", k);
+    }
+    // reschedule for register pressure (ZKGPU_ZXP_SCHED=0: source order)
+    static const int sched_on = [] {
+        const char *e = getenv("ZKGPU_ZXP_SCHED");
+        return e ? atoi(e) : 1;
+    }();
+    Scheduled sp;
+    if (sched_on) {
+        schedule(in, n_instr, op, n_opnd, n_tmp1, n_tmp3, sp);
+        in = sp.instr.data();
+        n_instr = (uint32_t)sp.instr.size();
+        op = sp.opnd.data();
+        n_opnd = (uint32_t)sp.opnd.size();
+        n_tmp1 = sp.n_tmp1;
+        n_tmp3 = sp.n_tmp3;
     }
     Compiler c;
     c.in = in;

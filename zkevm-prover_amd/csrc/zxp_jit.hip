@@ -14,8 +14,8 @@
 // process by source text).  csrc/gl_device.hpp is embedded verbatim, so the
 // field arithmetic is the same code the interpreter (k_zxp_eval) runs.
 //
-// Unsupported shapes (a program that reads a column it writes at a nonzero
-// row shift) return 1 and the caller runs the interpreter.
+// Unsupported shapes (a program that reads a column it writes at a row shift
+// it did not write first) return 1 and the caller runs the interpreter.
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
@@ -266,27 +266,36 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         cp.push_back(S->sec[sec] + (uint64_t)col * S->ld[sec]);
         return slot[key] = (uint32_t)cp.size() - 1;
     };
-    // columns written by the program (stores deferred; shift-0 reads forward)
-    std::vector<uint8_t> written_any;
-    auto mark = [&](uint32_t j) {
-        if (j >= written_any.size()) written_any.resize(j + 1, 0);
-        written_any[j] = 1;
-    };
+    // cells written by the program: (column slot, row shift) -> register w<r>;
+    // stores are deferred to the end of the row and land on row (i + shift) & m
+    std::map<std::pair<uint32_t, int32_t>, uint32_t> wreg;
+    std::vector<std::pair<uint32_t, int32_t>> wcell;  // register -> (slot, shift)
+    std::vector<uint8_t> written_any;                  // per slot, at any shift
     for (uint32_t k = 0; k < in.n_instr; k++) {
         const zxp_operand &d = in.opnd[in.ins[k].dst];
         if (d.kind == ZXP_COL || d.kind == ZXP_COL3)
-            for (uint32_t c = 0; c < (d.kind == ZXP_COL3 ? 3u : 1u); c++) mark(col_slot(d.a, d.b + c));
+            for (uint32_t c = 0; c < (d.kind == ZXP_COL3 ? 3u : 1u); c++) {
+                const uint32_t j = col_slot(d.a, d.b + c);
+                const auto key = std::make_pair(j, (int32_t)d.c);
+                if (!wreg.count(key)) {
+                    wreg[key] = (uint32_t)wcell.size();
+                    wcell.push_back(key);
+                }
+                if (j >= written_any.size()) written_any.resize(j + 1, 0);
+                written_any[j] = 1;
+            }
     }
     auto is_written = [&](uint32_t j) { return j < written_any.size() && written_any[j]; };
-    std::vector<uint8_t> wlive;  // written so far (in program order)
+    std::vector<uint8_t> wlive(wcell.size(), 0);  // written so far (in program order)
     auto col_read = [&](uint32_t sec, uint32_t col, int32_t sh, std::string &e) -> int {
         const uint32_t j = col_slot(sec, col);
         if (is_written(j)) {
-            if (sh != 0) return 1;  // cross-row read of a written column: interpreter
-            if (j < wlive.size() && wlive[j]) {
-                e = "w" + std::to_string(j);
+            auto it = wreg.find(std::make_pair(j, sh));
+            if (it != wreg.end() && wlive[it->second]) {
+                e = "w" + std::to_string(it->second);
                 return 0;
             }
+            if (sh != 0) return 1;  // cross-row read of a written column: interpreter
         }
         e = "C(" + std::to_string(j) + "," + std::to_string(sh) + ")";
         return 0;
@@ -380,24 +389,20 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                 appendf(body, "b%u = gl3{{%s, 0, 0}};\n", d.a, r.e.c_str());
             return 0;
         case ZXP_COL: {
-            const uint32_t j = col_slot(d.a, d.b);
+            const uint32_t j = wreg.at(std::make_pair(col_slot(d.a, d.b), (int32_t)d.c));
             appendf(body, "w%u = %s%s;\n", j, r.e.c_str(), r.dim == 3 ? ".v[0]" : "");
-            if (j >= wlive.size()) wlive.resize(j + 1, 0);
             wlive[j] = 1;
             return 0;
         }
         case ZXP_COL3: {
             uint32_t j[3];
-            for (int c = 0; c < 3; c++) j[c] = col_slot(d.a, d.b + c);
+            for (int c = 0; c < 3; c++) j[c] = wreg.at(std::make_pair(col_slot(d.a, d.b + c), (int32_t)d.c));
             if (r.dim == 3)
                 appendf(body, "{ const gl3 t_ = %s; w%u = t_.v[0]; w%u = t_.v[1]; w%u = t_.v[2]; }\n", r.e.c_str(),
                         j[0], j[1], j[2]);
             else
                 appendf(body, "w%u = %s; w%u = 0; w%u = 0;\n", j[0], r.e.c_str(), j[1], j[2]);
-            for (int c = 0; c < 3; c++) {
-                if (j[c] >= wlive.size()) wlive.resize(j[c] + 1, 0);
-                wlive[j[c]] = 1;
-            }
+            for (int c = 0; c < 3; c++) wlive[j[c]] = 1;
             return 0;
         }
         default: return 1;
@@ -491,8 +496,8 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                 if (tm.src == ZXP_TERM_ONE) return false;
                 const zxp_operand &o = in.opnd[tm.src];
                 if (o.kind != ZXP_COL) return false;
-                const uint32_t j = col_slot(o.a, o.b);
-                return !(is_written(j) && j < wlive.size() && wlive[j]);
+                auto it = wreg.find(std::make_pair(col_slot(o.a, o.b), (int32_t)o.c));
+                return !(it != wreg.end() && wlive[it->second]);
             };
             uint32_t n_mem = 0;
             for (uint32_t t = I.a; t < I.a + I.b; t++) n_mem += memcol(in.terms[t]);
@@ -607,15 +612,19 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     src += k_kernel_head;
     for (uint32_t s = 0; s < in.n_tmp1; s++) appendf(src, "uint64_t a%u = 0;\n", s);
     for (uint32_t s = 0; s < in.n_tmp3; s++) appendf(src, "gl3 b%u = gl3{{0, 0, 0}};\n", s);
-    for (uint32_t j = 0; j < written_any.size(); j++)
-        if (written_any[j]) appendf(src, "uint64_t w%u = 0;\n", j);
+    for (uint32_t r = 0; r < wcell.size(); r++) appendf(src, "uint64_t w%u = 0;\n", r);
     if (uses_x)
         appendf(src, "const uint64_t ex_ = i << (%u - p.logomega);\n"
                      "const uint64_t xv = gl_mul(p.x_start, gl_mul(gload(p.tw_lo + (ex_ & %lluULL)), gload(p.tw_hi + (ex_ >> %u))));\n",
                 TW_MAX_LOG, (unsigned long long)(TW_LEVEL_SIZE - 1), TW_LEVEL_BITS);
     src += body;
-    for (uint32_t j = 0; j < written_any.size(); j++)
-        if (written_any[j]) appendf(src, "gstore(const_cast<uint64_t *>(p.cp[%u]) + i, gl_canon(w%u));\n", j, j);
+    for (uint32_t r = 0; r < wcell.size(); r++) {
+        if (wcell[r].second == 0)
+            appendf(src, "gstore(const_cast<uint64_t *>(p.cp[%u]) + i, gl_canon(w%u));\n", wcell[r].first, r);
+        else
+            appendf(src, "gstore(const_cast<uint64_t *>(p.cp[%u]) + ((i + (uint64_t)(%d)) & m), gl_canon(w%u));\n",
+                    wcell[r].first, wcell[r].second, r);
+    }
     src += "#undef C\n}\n";
     return 0;
 }

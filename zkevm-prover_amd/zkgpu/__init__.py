@@ -90,6 +90,9 @@ _SIGS = {
     "zkgpu_prof_query": (ctypes.c_int, [ctypes.c_char_p, pu64, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_double)]),
     "zkgpu_prof_kernels": (ctypes.c_int, [ctypes.c_char_p, u64]),
+    # include/zkgpu_parser.h (bindings in zkgpu/parser.py)
+    "zkgpu_parser_convert": (ctypes.c_int, [u32, vp, u64, vp, u64, vp, u32, u32, u32, vp]),
+    "zkgpu_steps_parser_eval": (ctypes.c_int, [u32, vp, u64, vp, u64, vp, u32, u32, u32, vp]),
 }
 
 
