@@ -1,0 +1,105 @@
+"""Steps bytecode on the GPU (include/zkgpu_parser.h) vs the oracle's
+case-table interpreter (oracle/parser.c), bit for bit.
+
+The reference's fork-9 programs cannot travel to the GPU box; the programs
+here are built by zkgpu/synthetic_bytecode.py with the shape of the
+reference's step42ns (its opcode histogram, temporaries, the fork-9 memory
+map, next-row reads at shift 2 on the 2^24 domain: tests/golden/
+zkevm_bytecode_shape.json) and go through the same product converter.  On the
+CPU, tests/test_parser.py checks the converter on the reference's own five
+programs.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+P = 0xFFFFFFFF00000001
+SEC_CONST_2NS, SEC_Q_2NS = 9, 10
+
+
+def _rand(rng, shape):
+    return rng.integers(0, P, size=shape, dtype=np.uint64)
+
+
+@pytest.mark.parametrize("log_dom,jit", [(12, "1"), (16, "0")])
+def test_step42ns_shaped_program_gpu_equals_oracle(oracle, zkgpu, log_dom, jit, monkeypatch):
+    """2^12: the LDS interpreter; 2^16 with ZKGPU_ZXP_JIT=0: the interpreter on
+    a multi-workgroup domain (the compiled kernel is test_step42ns_shaped_jit)"""
+    import torch
+    monkeypatch.setenv("ZKGPU_ZXP_JIT", jit)
+    import zkgpu.parser as zp
+    import zkgpu.synthetic_bytecode as sb
+    shape = sb.load_shape()
+    ops, args = sb.generate("step42ns", seed=1)
+    secs = sb.sections(shape)
+    prog = zp.convert(zp.STEP42NS, ops, args, secs, shape["n_bits"], shape["n_bits_ext"])
+    dom = 1 << log_dom
+    rng = np.random.default_rng(log_dom)
+    S = {sec: _rand(rng, (dom, w)) for sec, _, w in secs if sec >= 5}
+    const = _rand(rng, (dom, shape["n_const"]))
+    chal = _rand(rng, (8, 3))
+    pub = _rand(rng, 48)
+    evals = _rand(rng, (4, 3))
+    # GPU: column-major device sections, the x / zhInv of a 2^log_dom coset domain
+    dsecs = {sec: (zkgpu.to_device(np.ascontiguousarray(a.T)), dom, a.shape[1]) for sec, a in S.items()}
+    dsecs[SEC_CONST_2NS] = (zkgpu.to_device(np.ascontiguousarray(const.T)), dom, const.shape[1])
+    q = torch.zeros((3, dom), dtype=torch.int64, device="cuda:0")
+    dsecs[SEC_Q_2NS] = (q, dom, 3)
+    zkgpu.zxp_eval_dev(prog, dsecs, log_dom, chal, pub, evals, extend_bits=1, x_start=7)
+    torch.cuda.synchronize()
+    got = zkgpu.from_device(q).T
+    # oracle: the same x_i = 7 w^i and zhInv of the 2^log_dom domain
+    x = np.zeros(dom, np.uint64)
+    oracle.lib().oc_powers(oracle._p(x), 7, oracle.gl_w(log_dom), dom)
+    n = dom >> 1
+    zh = np.array([pow((pow(7, n, P) * pow(P - 1, i, P) - 1) % P, P - 2, P) for i in range(2)], np.uint64)
+    qref = np.zeros((dom, 3), np.uint64)
+    off = {sec: o for sec, o, _ in secs}
+    sections = [(off[sec], a.shape[1], a) for sec, a in S.items()]
+    rc = oracle.parser_eval(3, ops, args, sections, const, dom, 1 << shape["n_bits_ext"], 1196, 175, chal, pub,
+                            evals, x, zh, q=qref)
+    assert rc == 0
+    assert qref.any()
+    assert np.array_equal(got, qref)
+
+
+def test_steps_parser_eval_host_dropin(oracle, zkgpu):
+    """zkgpu_steps_parser_eval on the reference's host layout (one flat
+    row-major memory map, StepsParams.pols, sections at mapOffsets) == the
+    oracle parser on the same buffer, for a 2^13-row extended domain."""
+    import copy
+    import zkgpu.parser as zp
+    import zkgpu.synthetic_bytecode as sb
+    shape = copy.deepcopy(sb.load_shape())
+    shape["n_bits"], shape["n_bits_ext"] = 12, 13
+    dom = 1 << shape["n_bits_ext"]
+    base = 0
+    for m in shape["map"]:  # a compact map: the 2ns sections back to back, the rest unused
+        if m["zxp_section"] >= 5:
+            m["offset"] = base
+            base += dom * m["width"]
+        else:
+            m["offset"] = 1 << 40
+    ops, args = sb.generate("step42ns", seed=3, shape=shape)
+    secs = sb.sections(shape)
+    rng = np.random.default_rng(5)
+    pols = _rand(rng, base)
+    const = _rand(rng, (dom, shape["n_const"]))
+    chal = _rand(rng, (8, 3))
+    pub = _rand(rng, 48)
+    q = np.zeros((dom, 3), np.uint64)
+    zp.steps_eval(zp.STEP42NS, ops, args, secs, shape["n_bits"], shape["n_bits_ext"], pols, const, chal, pub,
+                  q_2ns=q)
+    x = np.zeros(dom, np.uint64)
+    oracle.lib().oc_powers(oracle._p(x), 7, oracle.gl_w(shape["n_bits_ext"]), dom)
+    n = dom >> 1
+    zh = np.array([pow((pow(7, n, P) * pow(P - 1, i, P) - 1) % P, P - 2, P) for i in range(2)], np.uint64)
+    qref = np.zeros((dom, 3), np.uint64)
+    sections = [(o, w, pols[o:o + dom * w].reshape(dom, w)) for sec, o, w in secs if sec >= 5]
+    rc = oracle.parser_eval(3, ops, args, sections, const, dom, dom, 1196, 175, chal, pub, np.zeros((4, 3), np.uint64),
+                            x, zh, q=qref)
+    assert rc == 0 and qref.any()
+    assert np.array_equal(q, qref)

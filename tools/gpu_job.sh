@@ -3,7 +3,7 @@
 # stops at the first fault / abort / segfault / timeout (exit >= 124 or
 # signal), but continues past an ordinary test failure (exit 1).
 # Usage: tools/gpu_job.sh <step>...
-#   steps: tests large smoke bench instbench prof pmc starkpmc cpufull merkle commit sharded
+#   steps: tests large smoke bench instbench bwbench parser prof pmc starkpmc cpufull merkle commit sharded
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOTDIR=$(pwd)
@@ -49,6 +49,16 @@ for step in "$@"; do
     instbench)
         timeout -k 10 120 build/instbench > gpurun_out/instbench.json 2> gpurun_out/instbench.err
         ok_or_stop $? "instbench"
+        ;;
+    bwbench)
+        timeout -k 10 120 build/bwbench > gpurun_out/bwbench.json 2> gpurun_out/bwbench.err
+        ok_or_stop $? "bwbench"
+        cat gpurun_out/bwbench.json
+        ;;
+    parser)
+        timeout -k 10 600 $PYT tests/test_gpu_parser.py > gpurun_out/pytest_parser.log 2>&1
+        ok_or_stop $? "pytest parser"
+        tail -5 gpurun_out/pytest_parser.log
         ;;
     cpufull)
         timeout -k 10 1000 python bench.py --cpu-full > gpurun_out/cpu_full_stark.json 2> gpurun_out/cpu_full.err

@@ -19,6 +19,10 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <dlfcn.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -58,6 +62,7 @@ struct JitParams {
     uint64_t x_start, rmask;
     uint32_t logdom, logomega, zmask;
     uint32_t nkl;  // limb words staged in LDS (0: read from p.kl)
+    uint32_t one;  // always 1: the uniform branch that closes each code block (compile time)
 };
 
 // DOT limb tables up to this size are staged in LDS per workgroup: read from
@@ -83,6 +88,7 @@ struct JitParams {
     uint64_t x_start, rmask;
     uint32_t logdom, logomega, zmask;
     uint32_t nkl;
+    uint32_t one;
 };
 // long column runs of a DOT: a loop over table terms, ZKJIT_UNROLL loads in flight
 template <int D>
@@ -113,6 +119,12 @@ __device__ __forceinline__ void dot_cols(Dot3 &d0, Dot3 &d1, Dot3 &d2, const Jit
         }
     }
 }
+__device__ __forceinline__ int zk_one()
+{
+    int c;
+    asm volatile("s_mov_b32 %0, 1" : "=s"(c));
+    return c;
+}
 extern "C" __global__ void __launch_bounds__(256) ZKJIT_WAVES zxp_jit(const JitParams p)
 {
 #if ZKJIT_KL_LDS
@@ -130,6 +142,14 @@ extern "C" __global__ void __launch_bounds__(256) ZKJIT_WAVES zxp_jit(const JitP
     if (i >= (1ULL << p.logdom)) return;
     const uint64_t m = p.rmask;
 #define C(j, sh) gload(p.cp[j] + ((i + (uint64_t)(sh)) & m))
+// a global limb table is re-based in every code block (an opaque copy of K):
+// with thousands of loads off one base register, SIFoldOperands dominated
+// the compile (48 s of 100 for step3prev)
+#if ZKJIT_KL_LDS
+#define ZK_KREFRESH
+#else
+#define ZK_KREFRESH asm volatile("" : "+s"(K));
+#endif
 )";
 
 void appendf(std::string &s, const char *fmt, ...)
@@ -197,8 +217,23 @@ int rtc_compile(const std::string &src, std::vector<char> &code)
         const int o = e ? atoi(e) : (klds ? 2 : 1);
         return std::string("-O") + std::to_string(o >= 0 && o <= 3 ? o : 1);
     }();
-    const char *opts[] = {"--offload-arch=gfx950", olev.c_str(), "-std=c++17"};
-    const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+    // The GCN scheduler's re-scheduling stages (unclustered high-pressure and
+    // clustered low-occupancy) re-run the scheduler over every region and
+    // doubled the compile time of the large programs; register pressure is
+    // already bounded by the ZXP scheduler (csrc/zxp_compile.cpp), so they
+    // are off unless ZKGPU_ZXP_JIT_RESCHED=1.
+    static const bool resched = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_RESCHED");
+        return e && atoi(e) != 0;
+    }();
+    std::vector<const char *> opts = {"--offload-arch=gfx950", olev.c_str(), "-std=c++17"};
+    if (!resched) {
+        opts.push_back("-mllvm");
+        opts.push_back("-amdgpu-disable-unclustered-high-rp-reschedule=1");
+        opts.push_back("-mllvm");
+        opts.push_back("-amdgpu-disable-clustered-low-occupancy-reschedule=1");
+    }
+    const hiprtcResult r = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     if (r != HIPRTC_SUCCESS) {
         size_t ls = 0;
         hiprtcGetProgramLogSize(prog, &ls);
@@ -215,6 +250,90 @@ int rtc_compile(const std::string &src, std::vector<char> &code)
     return cs ? 0 : set_error(ZKGPU_ERR_ARG, "zxp jit: empty code object");
 }
 
+// On-disk code-object cache: a program's kernel depends only on its
+// structure (the source text) and the compiler, so compiled objects are kept
+// in ZKGPU_JIT_CACHE (default: <libzkgpu dir>/../jitcache, created on demand;
+// "0" disables) under a hash of source + options + hiprtc version.  build()
+// fills it ahead of time for the known circuits (the reference ships its
+// expression code compiled, chelpers/*.cpp).
+static std::string cache_dir()
+{
+    static const std::string dir = [] {
+        const char *e = getenv("ZKGPU_JIT_CACHE");
+        if (e) return std::string(strcmp(e, "0") ? e : "");
+        Dl_info info;
+        if (dladdr((void *)&cache_dir, &info) && info.dli_fname) {
+            std::string so = info.dli_fname;
+            const size_t sl = so.rfind('/');
+            if (sl != std::string::npos) return so.substr(0, sl) + "/../jitcache";
+        }
+        return std::string();
+    }();
+    return dir;
+}
+
+static std::string cache_key(const std::string &src)
+{
+    int major = 0, minor = 0;
+    hiprtcVersion(&major, &minor);
+    uint64_t h1 = 1469598103934665603ULL, h2 = 0x9E3779B97F4A7C15ULL;
+    auto mix = [&](const char *p, size_t n) {
+        for (size_t i = 0; i < n; i++) {
+            h1 = (h1 ^ (uint8_t)p[i]) * 1099511628211ULL;
+            h2 = (h2 + (uint8_t)p[i]) * 0xBF58476D1CE4E5B9ULL;
+            h2 ^= h2 >> 29;
+        }
+    };
+    mix(src.data(), src.size());
+    char opt[96];
+    snprintf(opt, sizeof(opt), "hiprtc%d.%d opt%s resched%s", major, minor,
+             getenv("ZKGPU_ZXP_JIT_OPT") ? getenv("ZKGPU_ZXP_JIT_OPT") : "-",
+             getenv("ZKGPU_ZXP_JIT_RESCHED") ? getenv("ZKGPU_ZXP_JIT_RESCHED") : "-");
+    mix(opt, strlen(opt));
+    char key[64];
+    snprintf(key, sizeof(key), "zxp_%016llx%016llx.co", (unsigned long long)h1, (unsigned long long)h2);
+    return key;
+}
+
+static bool cache_load(const std::string &src, std::vector<char> &code)
+{
+    const std::string dir = cache_dir();
+    if (dir.empty()) return false;
+    FILE *f = fopen((dir + "/" + cache_key(src)).c_str(), "rb");
+    if (!f) return false;
+    fseek(f, 0, SEEK_END);
+    const long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    code.resize(n > 0 ? (size_t)n : 0);
+    const bool ok = n > 0 && fread(code.data(), 1, (size_t)n, f) == (size_t)n;
+    fclose(f);
+    return ok;
+}
+
+static void cache_store(const std::string &src, const std::vector<char> &code)
+{
+    const std::string dir = cache_dir();
+    if (dir.empty()) return;
+    mkdir(dir.c_str(), 0775);
+    const std::string path = dir + "/" + cache_key(src), tmp = path + ".tmp" + std::to_string(getpid());
+    FILE *f = fopen(tmp.c_str(), "wb");
+    if (!f) return;
+    const bool ok = fwrite(code.data(), 1, code.size(), f) == code.size();
+    fclose(f);
+    if (ok) rename(tmp.c_str(), path.c_str());
+    else unlink(tmp.c_str());
+}
+
+// source -> code object: the disk cache, else hiprtc (and fill the cache)
+int code_object(const std::string &src, std::vector<char> &code)
+{
+    if (cache_load(src, code)) return 0;
+    int rc;
+    if ((rc = rtc_compile(src, code))) return rc;
+    cache_store(src, code);
+    return 0;
+}
+
 int compile(const std::string &src, hipFunction_t *out)
 {
     Cache &c = cache();
@@ -226,7 +345,7 @@ int compile(const std::string &src, hipFunction_t *out)
     }
     std::vector<char> code;
     int rc;
-    if ((rc = rtc_compile(src, code))) return rc;
+    if ((rc = code_object(src, code))) return rc;
     hipModule_t mod;
     if ((rc = check_hip(hipModuleLoadData(&mod, code.data()), "zxp jit: hipModuleLoadData"))) return rc;
     hipFunction_t f;
@@ -419,6 +538,23 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         size_t kt;
     };
     std::vector<std::vector<Stream>> stream(in.n_instr);
+    std::vector<uint8_t> streamed_term;  // per DOT term index: accumulated at the source's definition
+    // Streaming a term opens the DOT's accumulators (3 or 9 words) at the
+    // source's definition: for a source defined long before its DOT that
+    // holds more registers than keeping the source (1 or 3 words) -- the
+    // fork-9 step42ns peaked at ~1,300 live words with unbounded streaming
+    // against ~110 without.  Only sources defined at most STREAM_SPAN
+    // instructions before their DOT are streamed.
+    static const int64_t stream_span = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_STREAM_SPAN");
+        return (int64_t)(e ? atol(e) : 24);
+    }();
+    {
+        uint32_t nt = 0;
+        for (uint32_t k = 0; k < in.n_instr; k++)
+            if (in.ins[k].op == ZXP_DOT1 || in.ins[k].op == ZXP_DOT3) nt = std::max(nt, in.ins[k].a + in.ins[k].b);
+        streamed_term.assign(nt, 0);
+    }
     std::vector<size_t> dot_k0(in.n_instr, 0);
     std::vector<uint32_t> first_use(in.n_instr, UINT32_MAX);  // declaration point of DOT k's accumulators
     {
@@ -446,6 +582,8 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                     if (o.kind != ZXP_TMP1 && o.kind != ZXP_TMP3) continue;
                     const int64_t d = o.kind == ZXP_TMP1 ? last1[o.a] : last3[o.a];
                     if (d < 0) continue;  // never written: the value is 0
+                    if ((int64_t)k - d > stream_span) continue;  // read at the DOT instead
+                    streamed_term[t] = 1;
                     Stream st;
                     st.dot = k;
                     st.three = three;
@@ -464,18 +602,44 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     std::vector<std::vector<uint32_t>> declare_at(in.n_instr);
     for (uint32_t k = 0; k < in.n_instr; k++)
         if (first_use[k] != UINT32_MAX) declare_at[first_use[k]].push_back(k);
+    // DOT accumulators are declared at function scope (the body is split into
+    // blocks, below) and initialised where the first term arrives
+    std::string dot_decls;
     auto emit_declarations = [&](uint32_t at) {
         for (uint32_t k : declare_at[at]) {
             const size_t k0 = dot_k0[k];
-            if (in.ins[k].op == ZXP_DOT3)
-                appendf(body, "Dot3 D%u_0(K + %zu), D%u_1(K + %zu), D%u_2(K + %zu);\n", k, k0, k, k0 + 4, k,
-                        k0 + 8);
-            else
-                appendf(body, "Dot3 D%u_0(K + %zu);\n", k, k0);
+            if (in.ins[k].op == ZXP_DOT3) {
+                appendf(dot_decls, "Dot3 D%u_0, D%u_1, D%u_2;\n", k, k, k);
+                appendf(body, "D%u_0 = Dot3(K + %zu); D%u_1 = Dot3(K + %zu); D%u_2 = Dot3(K + %zu);\n", k, k0, k,
+                        k0 + 4, k, k0 + 8);
+            } else {
+                appendf(dot_decls, "Dot3 D%u_0;\n", k);
+                appendf(body, "D%u_0 = Dot3(K + %zu);\n", k, k0);
+            }
         }
     };
+    // Compile time: LLVM's instruction selection and machine scheduler are
+    // superlinear in basic-block size (a 600-instruction program took ~60 s
+    // as one block).  Every ZKGPU_ZXP_JIT_BLOCK instructions the body opens a
+    // new block behind a uniform branch on an opaque 1 (zk_one(): an
+    // s_mov_b32 the optimiser cannot see through, so it cannot merge the
+    // blocks back), so each block is compiled on its own.
+    static const size_t block = [] {  // source bytes per block
+        const char *e = getenv("ZKGPU_ZXP_JIT_BLOCK");
+        const long b = e ? atol(e) : 4096;
+        return (size_t)(b > 0 ? b : 1L << 40);
+    }();
+    size_t block_start = 0;
+    auto maybe_split = [&] {
+        if (body.size() - block_start >= block) {
+            body += "}\nif (zk_one()) { ZK_KREFRESH\n";
+            block_start = body.size();
+        }
+    };
+    body += "if (zk_one()) {\n";
     auto emit_streams = [&](uint32_t at) {
         for (const Stream &st : stream[at]) {
+            maybe_split();
             if (st.three)
                 appendf(body,
                         "{ const uint64_t v_ = %s; D%u_0.term_al(v_, K + %zu); D%u_1.term_al(v_, K + %zu); "
@@ -487,6 +651,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     };
     for (uint32_t k = 0; k < in.n_instr; k++) {
         const zxp_instr &I = in.ins[k];
+        maybe_split();
         emit_declarations(k);
         if (I.op == ZXP_DOT1 || I.op == ZXP_DOT3) {
             const bool three = I.op == ZXP_DOT3;
@@ -527,9 +692,23 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                 const zxp_operand &o = in.opnd[tm.src];
                 if (o.kind != ZXP_COL) {
                     if (o.kind != ZXP_TMP1 && o.kind != ZXP_TMP3) return 1;
-                    continue;  // streamed at the temporary's definition
+                    if (streamed_term[t]) continue;  // accumulated at the temporary's definition
+                    maybe_split();
+                    const std::string v = o.kind == ZXP_TMP1
+                                              ? "a" + std::to_string(o.a)
+                                              : "b" + std::to_string(o.a) + ".v[" + std::to_string(tm.comp) + "]";
+                    const size_t kt = limbs6x3(tm.coef);
+                    if (three)
+                        appendf(body,
+                                "{ const uint64_t v_ = %s; D%u_0.term_al(v_, K + %zu); D%u_1.term_al(v_, K + %zu); "
+                                "D%u_2.term_al(v_, K + %zu); }\n",
+                                v.c_str(), k, kt, k, kt + 8, k, kt + 16);
+                    else
+                        appendf(body, "D%u_0.term_al(%s, K + %zu);\n", k, v.c_str(), kt);
+                    continue;
                 }
                 if (loop && memcol(tm)) continue;
+                maybe_split();
                 std::string e;
                 if (col_read(o.a, o.b, (int32_t)o.c, e)) return 1;
                 const size_t kt = limbs6x3(tm.coef);
@@ -617,7 +796,9 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         appendf(src, "const uint64_t ex_ = i << (%u - p.logomega);\n"
                      "const uint64_t xv = gl_mul(p.x_start, gl_mul(gload(p.tw_lo + (ex_ & %lluULL)), gload(p.tw_hi + (ex_ >> %u))));\n",
                 TW_MAX_LOG, (unsigned long long)(TW_LEVEL_SIZE - 1), TW_LEVEL_BITS);
+    src += dot_decls;
     src += body;
+    src += "}\n";
     for (uint32_t r = 0; r < wcell.size(); r++) {
         if (wcell[r].second == 0)
             appendf(src, "gstore(const_cast<uint64_t *>(p.cp[%u]) + i, gl_canon(w%u));\n", wcell[r].first, r);
@@ -671,6 +852,7 @@ int zxp_jit_run(const ZxpJitIn &in, hipStream_t s)
     p.zmask = in.zmask;
     const bool klds = jit_kl_lds(kl.size());
     p.nkl = klds ? (uint32_t)kl.size() : 0;
+    p.one = 1;
     void *args[] = {&p};
     const uint64_t dom = 1ULL << in.log_dom;
     prof_begin(s);
@@ -730,8 +912,18 @@ extern "C" int zkgpu_zxp_jit_source(const void *instr, uint32_t n_instr, const v
         buf[n] = 0;
     }
     if (rtc_check) {
+        // compile (or find in the disk cache); rtc_check == 2 also writes the
+        // code object to $ZKGPU_ZXP_JIT_DUMP (register / scratch inspection)
         std::vector<char> code;
-        if ((rc = rtc_compile(src, code))) return rc;
+        if ((rc = code_object(src, code))) return rc;
+        const char *dump = getenv("ZKGPU_ZXP_JIT_DUMP");
+        if (rtc_check == 2 && dump) {
+            FILE *f = fopen(dump, "wb");
+            if (f) {
+                fwrite(code.data(), 1, code.size(), f);
+                fclose(f);
+            }
+        }
     }
     return (int)std::min<size_t>(src.size(), 0x7FFFFFFF);
 }

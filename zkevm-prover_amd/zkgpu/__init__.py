@@ -417,7 +417,7 @@ def zxp_jit_source(prog, challenges, publics, evals=None, rtc_check=False):
     rc = lib().zkgpu_zxp_jit_source(ins.ctypes.data, ins.shape[0], opn.ctypes.data, opn.shape[0],
                                     max(prog.n_tmp1, 1), max(prog.n_tmp3, 1), ch.ctypes.data, pub.ctypes.data,
                                     pub.size if publics is not None else 0, ev.ctypes.data, ev.size // 3,
-                                    buf, len(buf), 1 if rtc_check else 0)
+                                    buf, len(buf), int(rtc_check))
     if rc < 0:
         _check(rc, "zkgpu_zxp_jit_source")
     return buf.value.decode()
