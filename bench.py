@@ -333,7 +333,7 @@ def lde_measure(args, dev, torch, world, dist):
 
     elapsed, kernels = timed(step, steps, 2 if args.workload != "lde" else args.warmup, world, dist, torch)
     elapsed = max_over_ranks(elapsed, world, dist, torch, dev)
-    passes = {k: v for k, v in kernels.items() if k.startswith("k_ntt_pass") or k == "k_ntt_small"}
+    passes = {k: v for k, v in kernels.items() if k.startswith(("k_ntt_pass", "k_lde_")) or k == "k_ntt_small"}
     dev_ms = sum(v[1] for v in passes.values()) / steps
     alg = 24.0 * n * C if args.blowup_bits == 1 else 8.0 * (n + ne) * C
     achieved = alg / (dev_ms * 1e-3) / 1e9
@@ -341,7 +341,7 @@ def lde_measure(args, dev, torch, world, dist):
     traffic, src = (None, None)
     if args.log_n == 23 and C == 100 and args.blowup_bits == 1:
         traffic, src = lde_traffic_per_lde(launches)
-    roof = {"kernel": "extendPol = k_ntt_pass chain (%s per LDE)"
+    roof = {"kernel": "extendPol = NTT pass chain (%s per LDE)"
                       % ", ".join("%g x %s" % (launches[k], k) for k in sorted(launches)),
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),

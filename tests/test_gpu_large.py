@@ -19,8 +19,11 @@ def rand_cols(torch, ncols, n, seed):
     return torch.randint(0, 2**63 - 1, (ncols, n), dtype=torch.int64, device="cuda:0", generator=g)
 
 
-def test_lde_2p23_vs_oracle(oracle, zkgpu):
+@pytest.mark.parametrize("lde3", ["0", "1"])
+def test_lde_2p23_vs_oracle(oracle, zkgpu, lde3, monkeypatch):
+    """both LDE paths at the bench size (lde3 = the 3-pass LDE)"""
     import torch
+    monkeypatch.setenv("ZKGPU_LDE3", lde3)
     n, ne, C = 1 << 23, 1 << 24, 3
     zkgpu.set_stream(torch.cuda.current_stream())
     x = rand_cols(torch, C, n, 1)

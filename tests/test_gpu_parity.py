@@ -39,19 +39,26 @@ def test_ntt_noncanonical(oracle, zkgpu):
 
 
 @pytest.mark.parametrize("logn,blow,ncols", [(0, 1, 1), (3, 1, 2), (10, 1, 3), (12, 1, 4), (13, 1, 2),
-                                             (14, 2, 3), (16, 1, 8), (18, 1, 2)])
-def test_extend_pol_vs_oracle(oracle, zkgpu, logn, blow, ncols):
+                                             (14, 2, 3), (16, 1, 8), (17, 1, 2), (18, 1, 2), (19, 1, 3),
+                                             (20, 1, 2), (21, 1, 1), (22, 1, 1)])
+@pytest.mark.parametrize("lde3", ["0", "1"])
+def test_extend_pol_vs_oracle(oracle, zkgpu, logn, blow, ncols, lde3, monkeypatch):
+    """both LDE paths: the 6-pass NTT chain and (2^18..2^24, blowup 1) the
+    3-pass LDE of ntt.hip (ZKGPU_LDE3=1)"""
+    monkeypatch.setenv("ZKGPU_LDE3", lde3)
     rng = np.random.default_rng(200 + logn)
     x = rand_gl(rng, (1 << logn, ncols))
     ne = 1 << (logn + blow)
     assert np.array_equal(zkgpu.extend_pol(x, ne), oracle.extend_pol(x, ne))
 
 
-def test_extend_pol_dev_column_major(oracle, zkgpu):
-    """Device-resident SoA path with padded leading dimensions."""
+@pytest.mark.parametrize("logn,ncols,lde3", [(15, 5, "0"), (18, 3, "1"), (20, 7, "1"), (20, 2, "0")])
+def test_extend_pol_dev_column_major(oracle, zkgpu, logn, ncols, lde3, monkeypatch):
+    """Device-resident SoA path with padded leading dimensions (lde3: the
+    3-pass LDE of ntt.hip)."""
     import torch
-    rng = np.random.default_rng(9)
-    logn, ncols = 15, 5
+    monkeypatch.setenv("ZKGPU_LDE3", lde3)
+    rng = np.random.default_rng(9 + logn)
     n, ne = 1 << logn, 1 << (logn + 1)
     x = rand_gl(rng, (n, ncols))
     ld_in, ld_out = n + 64, ne + 128

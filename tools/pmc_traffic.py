@@ -31,6 +31,9 @@ def bench_label(name):
     m = re.match(r"k_ntt_pass<(\d+), (\d+), (true|false)", base)
     if m:
         return "k_ntt_pass<%d,%s>" % (int(m.group(1)) + int(m.group(2)), "inv" if m.group(3) == "true" else "fwd")
+    m = re.match(r"k_lde_strided<(\d+), (true|false)", base)
+    if m:  # P1 = inverse, P3 = forward (ntt.hip 3-pass LDE)
+        return "k_lde_%s<%s>" % ("p1" if m.group(2) == "true" else "p3", m.group(1))
     return base
 
 

@@ -141,8 +141,17 @@ static int extend_pol_dev(uint64_t *out, uint64_t ld_out, const uint64_t *in, ui
     if (env && atoll(env) > 0) batch = (uint64_t)atoll(env);
     if (batch > ncols) batch = ncols;
     uint64_t *coef = workspace(0, batch * n * sizeof(uint64_t));
+    if (!coef) return ZKGPU_ERR_OOM;
+    if (lde3_supported(logn, loge)) {
+        for (uint64_t c0 = 0; c0 < ncols; c0 += batch) {
+            const uint64_t nc = ncols - c0 < batch ? ncols - c0 : batch;
+            if ((rc = lde3_columns(c, out + c0 * ld_out, ld_out, in + c0 * ld_in, ld_in, coef, logn, nc, c.stream)))
+                return rc;
+        }
+        return 0;
+    }
     uint64_t *tmp = workspace(1, batch * n_ext * sizeof(uint64_t));
-    if (!coef || !tmp) return ZKGPU_ERR_OOM;
+    if (!tmp) return ZKGPU_ERR_OOM;
     uint32_t post_bits = logn < POST_BITS ? logn : POST_BITS;
     for (uint64_t c0 = 0; c0 < ncols; c0 += batch) {
         uint64_t nc = ncols - c0 < batch ? ncols - c0 : batch;

@@ -581,4 +581,402 @@ void fill_powers(uint64_t *out, uint64_t base, uint64_t step, uint64_t scale, ui
     hipLaunchKernelGGL(k_fill_powers, dim3(blocks), dim3(256), 0, s, out, base, step, scale, count);
 }
 
+
+// ================================================================ 3-pass LDE
+// extendPol for n_ext = 2n (the zkEVM blowup), n = RA * RB with RB = 4096 and
+// RA = 2^LA, 6 <= LA <= 12 (n = 2^18 .. 2^24).  DESIGN.md "LDE".
+//
+// The 2n-point NTT of the zero-padded coset coefficients splits into two
+// n-point NTTs (part p = 0, 1):  X[2k + p] = NTT_n(c_i * F_p^i / n)[k] with
+// F_p = 7 * omega_2n^p, c = INTT-unscaled coefficients.  With the four-step
+// index maps i = jB + RB*jA (evaluations in), c = kA + RA*kB (coefficients)
+// and k = k' + RB*k'' (evaluations out):
+//   P1 (strided):    INTT over jA for each jB, * omega_n^-(jB kA),
+//                    T1[kA*RB + jB]                              read n, write n
+//   P2 (contiguous): block kA: INTT over jB -> coefficients kA + RA*kB,
+//                    * F_p^c / n, NTT over kB -> k' (both parts),
+//                    * omega_n^(kA k'), T2[kA*2RB + 2k' + p]      read n, write 2n
+//   P3 (strided):    for each q = 2k' + p: NTT over kA -> k'',
+//                    out[q + 2RB*k''] (natural order, in place)  read 2n, write 2n
+// 9n element moves = 3x the algorithmic 3n, against 17n for
+// INTT + zero-padded NTT as two 3-pass transforms.  Every global access is a
+// run of >= 128 bytes: P1 / P3 move 16 consecutive groups per row (LA = 11),
+// P2 whole 4096-element blocks.
+constexpr int LDE_LB = 12;
+constexpr uint64_t LDE_RB = 1ULL << LDE_LB;
+constexpr int SP_THREADS = 256;  // strided passes: 64 values per thread, 2 workgroups per CU
+
+struct StridedArgs {
+    const uint64_t *src;
+    uint64_t src_ld;  // column stride
+    uint64_t *dst;
+    uint64_t dst_ld;
+    uint64_t row_stride;    // distance of consecutive sub-DFT elements, in and out
+    const uint64_t *tw_r;   // omega_R^e, e < R (this direction)
+    const uint64_t *otw;    // P1: omega_n^-(jB kA) at [kA * RB + jB]; null = none (P3)
+    uint32_t canon;         // 1 = canonical output (P3)
+    uint32_t ncols;
+    uint32_t units;         // workgroups per column
+    uint32_t xcd;           // 1 = XCD-aware order (below)
+};
+
+// One sub-DFT of size R = 2^LA = 64 * T per group; G = 256 / T groups
+// (consecutive positions along the row, the fastest lane index) per workgroup.
+//   stage 1: thread (g, t) holds x[t + T*j1], j1 < 64: radix-64 in registers
+//            (DIF, twiddles powers of 2 only), * omega_R^(t k1)
+//   LDS:     transpose in two 32-bit halves (word k1*ROW + t*G + g; the G
+//            pad words per k1 row keep both access patterns conflict-free)
+//   stage 2: thread (g, t) holds k1 = t + T*m (m < 64/T), j2 < T:
+//            64/T radix-T DFTs -> X[k1 + 64 k2]
+template <int LA, bool INV>
+__global__ void __launch_bounds__(SP_THREADS) k_lde_strided(StridedArgs a)
+{
+    constexpr int LT = LA - 6, T = 1 << LT, G = SP_THREADS / T, M = 64 / T;
+    constexpr int ROW = T * G + (G < 32 ? G : 0);
+    __shared__ uint32_t lds[64 * ROW];
+    // xcd: workgroup b runs on XCD b % 8; give each XCD a contiguous range of
+    // (column, unit) with units fastest, so that the workgroups sharing 128-byte
+    // lines (neighbouring units) run at the same time behind the same L2.
+    // Otherwise columns fastest (the outer-twiddle slice of a unit stays in L2).
+    uint32_t col;
+    uint64_t unit;
+    if (a.xcd) {
+        const uint32_t nb = gridDim.x, b = blockIdx.x;
+        const uint32_t lb = (b & 7) * (nb >> 3) + (b >> 3);
+        col = lb / a.units;
+        unit = lb % a.units;
+    } else {
+        col = blockIdx.x % a.ncols;
+        unit = blockIdx.x / a.ncols;
+    }
+    const uint64_t g0 = unit * G;
+    const int tid = threadIdx.x, g = tid % G, t = tid / G;
+    const uint64_t rs = a.row_stride;
+    const uint64_t *src = a.src + (uint64_t)col * a.src_ld + g0 + g;
+    uint64_t v[64];
+#pragma unroll
+    for (int j1 = 0; j1 < 64; j1++) v[j1] = src[(uint64_t)(t + T * j1) * rs];
+    dft_regs<6, INV>(v);
+    if constexpr (T > 1) {
+#pragma unroll
+        for (int r = 1; r < 64; r++) v[r] = gl_mul(v[r], a.tw_r[t * brev_c(r, 6)]);
+    }
+    // transpose, low words then high words (the low half of v[] takes the
+    // new low word as soon as its old one is in LDS)
+    const int wb = t * G + g;
+#pragma unroll
+    for (int r = 0; r < 64; r++) lds[brev_c(r, 6) * ROW + wb] = (uint32_t)v[r];
+    __syncthreads();
+    uint32_t nl[64];
+#pragma unroll
+    for (int m = 0; m < M; m++)
+#pragma unroll
+        for (int j2 = 0; j2 < T; j2++) nl[m * T + j2] = lds[(t + T * m) * ROW + j2 * G + g];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 64; r++) lds[brev_c(r, 6) * ROW + wb] = (uint32_t)(v[r] >> 32);
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < M; m++)
+#pragma unroll
+        for (int j2 = 0; j2 < T; j2++)
+            v[m * T + j2] = ((uint64_t)lds[(t + T * m) * ROW + j2 * G + g] << 32) | nl[m * T + j2];
+#pragma unroll
+    for (int m = 0; m < M; m++) dft_regs<LT, INV>(v + m * T);
+    uint64_t *dst = a.dst + (uint64_t)col * a.dst_ld + g0 + g;
+    const uint64_t *otw = a.otw ? a.otw + g0 + g : nullptr;
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+#pragma unroll
+        for (int r = 0; r < T; r++) {
+            const uint64_t k = (uint64_t)(t + T * m) + 64 * (uint64_t)brev_c(r, LT);
+            uint64_t x = v[m * T + r];
+            if (otw) x = gl_mul(x, otw[k * LDE_RB]);
+            dst[k * rs] = a.canon ? gl_canon(x) : x;
+        }
+    }
+}
+
+struct MidArgs {
+    const uint64_t *src;  // T1, column stride src_ld
+    uint64_t src_ld;
+    uint64_t *dst;  // T2 (the output buffer), column stride dst_ld
+    uint64_t dst_ld;
+    const uint64_t *tw16[2];   // omega_4096^e, e < 4096 (forward, inverse)
+    const uint64_t *tw256[2];  // omega_256^e, e < 256
+    const uint64_t *fs;        // [p][kA][k]: F_p^(kA + 256 RA k) / n, k < 16
+    const uint64_t *twa[2];    // [p][k2 * 256 + t]: F_p^(RA t) omega_4096^(t k2)
+    const uint64_t *otw;       // omega_n^(kA k') at [kA * RB + k']
+    uint64_t nblk;             // ncols * RA
+    uint32_t ncols;
+};
+
+constexpr int MID_LDS = 16 * 272;  // u64 per block
+
+// 4096-point DFT of one block by 256 threads, 16 values each, radix 16^3:
+// in  thread t holds x[t + 256 j] at v[j];
+// out thread t holds X[t + 256 k] at v[brev4(k)].
+//   A: DFT over j -> k2, * omega_4096^(t k2), LDS [k2*272 + t]
+//   B: thread (j0, k2) = (t & 15, t >> 4) reads j1 < 16 (t = j0 + 16 j1),
+//      DFT -> k1, * omega_256^(j0 k1), LDS [j0*257 + k1*16 + k2]
+//   C: thread (k2, k1) = (t & 15, t >> 4) reads j0 < 16, DFT -> k0:
+//      X[k2 + 16 k1 + 256 k0]
+// (pads 272 / 257: conflict-free ds_write_b64 16-lane and ds_read_b64 32-lane groups)
+// TA: tw16 is a per-element stage-A table [k2 * 256 + t] (the LDE's
+// F_p^(RA t) coset factor folded into omega_4096^(t k2)), else omega_4096^e.
+template <bool INV, bool TA>
+__device__ __forceinline__ void dft4096_block(uint64_t *v, uint64_t *L, int t, const uint64_t *tw16,
+                                              const uint64_t *tw256)
+{
+    // sched_barrier: keeps the compiler from hoisting the next stage's
+    // twiddle loads over the current stage (register pressure)
+    dft_regs<4, INV>(v);
+    if constexpr (TA) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) v[r] = gl_mul(v[r], tw16[(brev_c(r, 4) << 8) + t]);
+    } else {
+#pragma unroll
+        for (int r = 1; r < 16; r++) v[r] = gl_mul(v[r], tw16[t * brev_c(r, 4)]);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; r++) L[brev_c(r, 4) * 272 + t] = v[r];
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+    const int lo = t & 15, hi = t >> 4;
+#pragma unroll
+    for (int j1 = 0; j1 < 16; j1++) v[j1] = L[hi * 272 + lo + 16 * j1];
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+    dft_regs<4, INV>(v);
+#pragma unroll
+    for (int r = 1; r < 16; r++) v[r] = gl_mul(v[r], tw256[lo * brev_c(r, 4)]);
+#pragma unroll
+    for (int r = 0; r < 16; r++) L[lo * 257 + brev_c(r, 4) * 16 + hi] = v[r];
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j0 = 0; j0 < 16; j0++) v[j0] = L[j0 * 257 + hi * 16 + lo];
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+    dft_regs<4, INV>(v);
+}
+
+// P2: one block (kA, column) per workgroup, columns fastest (VGPRs: 16
+// values + the 16 coefficients kept for the second part + the first part's
+// 16 results, stored with the second's as pairs)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_lde_mid(MidArgs a)
+{
+    __shared__ uint64_t L[MID_LDS];
+    const int t = threadIdx.x;
+    const uint64_t blk = blockIdx.x;
+    const uint32_t col = (uint32_t)(blk % a.ncols);
+    const uint64_t kA = blk / a.ncols;
+    const uint64_t *src = a.src + (uint64_t)col * a.src_ld + kA * LDE_RB + t;
+    uint64_t v[16], c[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) v[j] = src[256 * j];
+    dft4096_block<true, false>(v, L, t, a.tw16[1], a.tw256[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    // v[brev4(k)] = coefficient kA + RA * (t + 256 k), unscaled
+#pragma unroll
+    for (int k = 0; k < 16; k++) c[k] = v[brev_c(k, 4)];
+    uint64_t *dst = a.dst + (uint64_t)col * a.dst_ld + kA * 2 * LDE_RB + 2 * t;
+    const uint64_t *otw = a.otw + kA * LDE_RB + t;
+    const uint64_t RA = a.nblk / a.ncols;
+    uint64_t z0[16];
+    for (int p = 0; p < 2; p++) {
+        // coefficient kA + RA (t + 256 k) times F_p^c / n = S_p[kA][k] (block-uniform,
+        // scalar loads) * F_p^(RA t) (folded into the stage-A table)
+        const uint64_t *S = a.fs + ((uint64_t)p * RA + kA) * 16;
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = gl_mul(c[k], S[k]);
+        dft4096_block<false, true>(v, L, t, a.twa[p], a.tw256[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (p == 0) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) z0[k] = v[k];
+        }
+    }
+    // rows 2 (t + 256 k) + {0, 1}: one 16-byte store per pair (whole lines;
+    // part-by-part 8-byte stores left half-written lines to the L2)
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint64_t w = otw[256 * k];
+        HIP_vector_type<unsigned long long, 2> pr;
+        pr.x = gl_mul(z0[brev_c(k, 4)], w);
+        pr.y = gl_mul(v[brev_c(k, 4)], w);
+        *reinterpret_cast<HIP_vector_type<unsigned long long, 2> *>(dst + 512 * k) = pr;
+    }
+}
+
+// ---- host side
+struct Lde3Tables {
+    uint32_t logn = 0;
+    uint64_t *pow16[2] = {nullptr, nullptr}, *pow256[2] = {nullptr, nullptr}, *powR[2] = {nullptr, nullptr};
+    uint64_t *fs = nullptr, *twa = nullptr;
+};
+
+// fs[p][kA][k] = F_p^(kA + 256 RA k) / n
+__global__ void k_lde_fs(uint64_t *fs, uint64_t F, uint64_t ninv, uint64_t RA)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= RA * 16) return;
+    const uint64_t kA = i >> 4, k = i & 15;
+    fs[i] = gl_canon(gl_mul(ninv, gl_pow(F, kA + 256 * RA * k)));
+}
+
+// twa[p][k2 * 256 + t] = F_p^(RA t) * omega_4096^(t k2)
+__global__ void k_lde_twa(uint64_t *twa, uint64_t F, uint64_t w4096, uint64_t RA)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 4096) return;
+    const uint64_t k2 = i >> 8, t = i & 255;
+    twa[i] = gl_canon(gl_mul(gl_pow(F, RA * t), gl_pow(w4096, t * k2)));
+}
+static Lde3Tables g_lde3;
+
+static int lde3_tables(Ctx &ctx, uint32_t logn, hipStream_t s)
+{
+    Lde3Tables &T = g_lde3;
+    if (T.logn == logn) return 0;
+    const uint32_t la = logn - LDE_LB;
+    const uint64_t RA = 1ULL << la, n = 1ULL << logn;
+    auto alloc = [&](uint64_t **p, uint64_t count) -> int {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+        if (hipMalloc((void **)p, count * 8) != hipSuccess) return set_error(ZKGPU_ERR_OOM, "lde tables");
+        return 0;
+    };
+    int rc;
+    for (int d = 0; d < 2; d++) {
+        const uint64_t w16 = d ? h_inv(h_w(12)) : h_w(12), w256 = d ? h_inv(h_w(8)) : h_w(8),
+                       wR = d ? h_inv(h_w(la)) : h_w(la);
+        if ((rc = alloc(&T.pow16[d], 4096)) || (rc = alloc(&T.pow256[d], 256)) || (rc = alloc(&T.powR[d], RA)))
+            return rc;
+        fill_powers(T.pow16[d], w16, 1, 1, 4096, s);
+        fill_powers(T.pow256[d], w256, 1, 1, 256, s);
+        fill_powers(T.powR[d], wR, 1, 1, RA, s);
+    }
+    // F_p = 7 * omega_2n^p
+    if ((rc = alloc(&T.fs, 2 * RA * 16)) || (rc = alloc(&T.twa, 2 * 4096))) return rc;
+    const uint64_t ninv = h_inv(n);
+    for (int p = 0; p < 2; p++) {
+        const uint64_t F = p ? h_mul(7, h_w(logn + 1)) : 7;
+        hipLaunchKernelGGL(k_lde_fs, dim3((uint32_t)((RA * 16 + 255) / 256)), dim3(256), 0, s, T.fs + p * RA * 16, F,
+                           ninv, RA);
+        hipLaunchKernelGGL(k_lde_twa, dim3(16), dim3(256), 0, s, T.twa + p * 4096, F, h_w(12), RA);
+    }
+    if ((rc = check_launch("lde tables"))) return rc;
+    T.logn = logn;
+    return 0;
+}
+
+template <int LA>
+static void launch_strided(const StridedArgs &a, uint64_t units, int inverse, hipStream_t s)
+{
+    const dim3 grid((uint32_t)(units * a.ncols));
+    if (inverse) hipLaunchKernelGGL((k_lde_strided<LA, true>), grid, dim3(SP_THREADS), 0, s, a);
+    else hipLaunchKernelGGL((k_lde_strided<LA, false>), grid, dim3(SP_THREADS), 0, s, a);
+}
+
+static void dispatch_strided(uint32_t la, StridedArgs a, uint64_t groups, int inverse, hipStream_t s)
+{
+    const uint64_t units = groups / (SP_THREADS >> (la - 6));
+    static const int xcd_env = [] {  // measured slower (46.3 vs 48.0 Gelem/s): off unless asked for
+        const char *e = getenv("ZKGPU_LDE3_XCD");
+        return e ? atoi(e) : 0;
+    }();
+    a.units = (uint32_t)units;
+    a.xcd = (xcd_env && (units * a.ncols) % 8 == 0) ? 1u : 0u;
+    switch (la) {
+    case 6: launch_strided<6>(a, units, inverse, s); break;
+    case 7: launch_strided<7>(a, units, inverse, s); break;
+    case 8: launch_strided<8>(a, units, inverse, s); break;
+    case 9: launch_strided<9>(a, units, inverse, s); break;
+    case 10: launch_strided<10>(a, units, inverse, s); break;
+    case 11: launch_strided<11>(a, units, inverse, s); break;
+    case 12: launch_strided<12>(a, units, inverse, s); break;
+    default: break;
+    }
+}
+
+// ZKGPU_LDE3=1 selects the 3-pass LDE where it applies (read per call).
+// Measured on MI355X (2^23 -> 2^24 x 100, DESIGN.md "LDE"): 35.2 ms against
+// 33.5 ms for the 6-pass path with a third of its HBM traffic; both are VALU
+// bound, so the 6-pass path stays the default.
+bool lde3_supported(uint32_t logn, uint32_t loge)
+{
+    const char *e = getenv("ZKGPU_LDE3");
+    const bool enabled = e && atoi(e) != 0;
+    return enabled && loge == logn + 1 && logn >= LDE_LB + 6 && logn <= LDE_LB + 12;
+}
+
+static const char *P1_NAMES[13] = {"", "", "", "", "", "", "k_lde_p1<6>", "k_lde_p1<7>", "k_lde_p1<8>", "k_lde_p1<9>",
+                                   "k_lde_p1<10>", "k_lde_p1<11>", "k_lde_p1<12>"};
+static const char *P3_NAMES[13] = {"", "", "", "", "", "", "k_lde_p3<6>", "k_lde_p3<7>", "k_lde_p3<8>", "k_lde_p3<9>",
+                                   "k_lde_p3<10>", "k_lde_p3<11>", "k_lde_p3<12>"};
+
+// out (2n rows, column stride ld_out >= 2n) = extendPol(in); t1: n words per column
+int lde3_columns(Ctx &ctx, uint64_t *out, uint64_t ld_out, const uint64_t *in, uint64_t ld_in, uint64_t *t1,
+                 uint32_t logn, uint64_t ncols, hipStream_t s)
+{
+    if (logn < LDE_LB + 6 || logn > LDE_LB + 12) return set_error(ZKGPU_ERR_ARG, "lde3: unsupported size 2^%u", logn);
+    if (ncols == 0) return 0;
+    int rc;
+    if ((rc = lde3_tables(ctx, logn, s))) return rc;
+    const uint32_t la = logn - LDE_LB;
+    const uint64_t n = 1ULL << logn, RA = 1ULL << la;
+    const uint64_t *otw_inv = otw_table(ctx, 1, logn, la, s), *otw_fwd = otw_table(ctx, 0, logn, la, s);
+    if (!otw_inv || !otw_fwd) return set_error(ZKGPU_ERR_OOM, "lde3: twiddle tables");
+    // at most 65535 columns and 2^31 workgroups per launch
+    const uint64_t cmax = std::min<uint64_t>(65535, (1ULL << 31) / (2 * LDE_RB));
+    for (uint64_t c0 = 0; c0 < ncols; c0 += cmax) {
+        const uint32_t nc = (uint32_t)std::min<uint64_t>(cmax, ncols - c0);
+        StridedArgs p1;
+        p1.src = in + c0 * ld_in;
+        p1.src_ld = ld_in;
+        p1.dst = t1;
+        p1.dst_ld = n;
+        p1.row_stride = LDE_RB;
+        p1.tw_r = g_lde3.powR[1];
+        p1.otw = otw_inv;
+        p1.canon = 0;
+        p1.ncols = nc;
+        prof_begin(s);
+        dispatch_strided(la, p1, LDE_RB, 1, s);
+        prof_end(P1_NAMES[la], 16.0 * (double)n * nc, s);
+        MidArgs m;
+        m.src = t1;
+        m.src_ld = n;
+        m.dst = out + c0 * ld_out;
+        m.dst_ld = ld_out;
+        for (int d = 0; d < 2; d++) {
+            m.tw16[d] = g_lde3.pow16[d];
+            m.tw256[d] = g_lde3.pow256[d];
+            m.twa[d] = g_lde3.twa + d * 4096;
+        }
+        m.fs = g_lde3.fs;
+        m.otw = otw_fwd;
+        m.nblk = RA * nc;
+        m.ncols = nc;
+        prof_begin(s);
+        hipLaunchKernelGGL(k_lde_mid, dim3((uint32_t)m.nblk), dim3(256), 0, s, m);
+        prof_end("k_lde_mid", 24.0 * (double)n * nc, s);
+        StridedArgs p3;
+        p3.src = out + c0 * ld_out;
+        p3.src_ld = ld_out;
+        p3.dst = out + c0 * ld_out;
+        p3.dst_ld = ld_out;
+        p3.row_stride = 2 * LDE_RB;
+        p3.tw_r = g_lde3.powR[0];
+        p3.otw = nullptr;
+        p3.canon = 1;
+        p3.ncols = nc;
+        prof_begin(s);
+        dispatch_strided(la, p3, 2 * LDE_RB, 0, s);
+        prof_end(P3_NAMES[la], 32.0 * (double)n * nc, s);
+    }
+    return check_launch("lde3");
+}
+
 }  // namespace zk

@@ -64,6 +64,10 @@ int ntt_columns(Ctx &c, uint64_t *dst, uint64_t dst_ld, const uint64_t *src, uin
 void rows_to_cols(const uint64_t *in, uint64_t *out, uint64_t nrows, uint64_t ncols, uint64_t ld, hipStream_t s);
 void cols_to_rows(const uint64_t *in, uint64_t *out, uint64_t nrows, uint64_t ncols, uint64_t ld, hipStream_t s);
 void fill_powers(uint64_t *out, uint64_t base, uint64_t step, uint64_t scale, uint64_t count, hipStream_t s);
+// 3-pass LDE 2^logn -> 2^(logn+1) (ntt.hip "3-pass LDE"); t1: 2^logn words per column
+bool lde3_supported(uint32_t logn, uint32_t loge);
+int lde3_columns(Ctx &c, uint64_t *out, uint64_t ld_out, const uint64_t *in, uint64_t ld_in, uint64_t *t1,
+                 uint32_t logn, uint64_t ncols, hipStream_t s);
 
 // ---- poseidon.hip
 int poseidon_batch(uint64_t *out, const uint64_t *in, uint64_t n, int full, hipStream_t s);
