@@ -226,7 +226,7 @@ def valu_peak(kernel):
     cost = {}
     for r in ib["rows"]:
         if r["waves_per_simd"] == 8:
-            cost[r["instr"]] = r["cycles_at_2p4GHz"]
+            cost[r["instr"]] = r.get("cycles", r.get("cycles_at_2p4GHz"))
     base = cost.get("v_add_u32")
     km = (mix or {}).get("kernels", {}).get(kernel)
     if not km:
