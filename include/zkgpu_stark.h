@@ -68,6 +68,13 @@ int zkgpu_stark_witness(void *handle);
 /* load cm1_n from a host row-major buffer (n rows x n_cm1), the reference's
  * commit-pols layout (commit_pols.hpp:18) */
 int zkgpu_stark_set_cm1(void *handle, const uint64_t *rows);
+/* load the constant polynomials from a host row-major buffer (n rows x
+ * n_const), the reference's .const file (ConstantPolsStarks, starks.hpp:94-116);
+ * recomputes their LDE, tree and verkey */
+int zkgpu_stark_set_const(void *handle, const uint64_t *rows);
+/* set the public inputs (n_publics values; prover.cpp:480-560 computes them
+ * from the executor's Main columns) */
+int zkgpu_stark_set_publics(void *handle, const uint64_t *publics);
 uint64_t zkgpu_stark_proof_len(void *handle);
 int zkgpu_stark_prove(void *handle, uint64_t *proof_out);
 int zkgpu_stark_verkey(void *handle, uint64_t out[4]);

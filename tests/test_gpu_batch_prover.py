@@ -1,0 +1,50 @@
+"""The batch-proof driver end to end on the GPU: the reference's input files
+(starkinfo JSON, constant polynomials, constant tree, committed trace,
+publics) -> zkgpu_batch_prover -> batch_proof.zkin.json byte-identical to the
+oracle's proof in proof2zkinStark layout (tests/test_starkinfo.py checks the
+loader and writers on the CPU)."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from test_starkinfo import DRIVER
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("kw", [dict(n_bits=10, t=4, m=2, n_queries=16),
+                                dict(n_bits=9, blowup_bits=2, t=3, m=1, n_lookups=1, q_deg=4, n_queries=12)])
+def test_batch_prover_drop_in(oracle, tmp_path, kw):
+    import zkgpu.starkinfo as zs
+    from oracle.stark_prover import OracleStark
+    from zkgpu.synthetic import SyntheticStark
+    inst = SyntheticStark(**kw)
+    o = OracleStark(inst)
+    o.witness()
+    proof = o.prove()
+    cfg = zs.write_inputs(str(tmp_path), inst, o.S[4], o.S[9], o.const_nodes, o.S[0], o.publics)
+    r = subprocess.run([DRIVER, cfg], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = tmp_path / "out"
+    assert (out / "batch_proof.zkin.json").read_text() == zs.zkin_text(proof, o.publics, inst.n_cm2, inst.n_cm3)
+    full = json.loads((out / "batch_proof.proof.json").read_text())
+    assert full["root1"] == proof["root1"] and full["evals"] == proof["evals"]
+
+
+def test_batch_prover_rejects_wrong_const_tree(oracle, tmp_path):
+    """a constant tree whose root is not the tree of the constant file fails loudly"""
+    import zkgpu.starkinfo as zs
+    from oracle.stark_prover import OracleStark
+    from zkgpu.synthetic import SyntheticStark
+    inst = SyntheticStark(n_bits=8, t=2, m=1, n_queries=8)
+    o = OracleStark(inst)
+    o.witness()
+    nodes = o.const_nodes.copy()
+    nodes[-1] ^= 1
+    cfg = zs.write_inputs(str(tmp_path), inst, o.S[4], o.S[9], nodes, o.S[0], o.publics)
+    r = subprocess.run([DRIVER, cfg], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1 and "zkevmConstantsTree" in r.stderr, r.stderr
+    assert not os.path.exists(tmp_path / "out" / "batch_proof.zkin.json")

@@ -316,6 +316,29 @@ public:
         return 0;
     }
 
+    // constant polynomials from the reference's .const file layout (N rows x
+    // nConstants, ConstantPolsStarks, starks.hpp:94-116), their LDE and tree
+    int set_const(const uint64_t *rows)
+    {
+        void *tmp = nullptr;
+        CK(zkgpu_dev_malloc(&tmp, (uint64_t)(info.n_const ? info.n_const : 1) * N * 8));
+        int rc = zkgpu_memcpy_h2d(tmp, rows, (uint64_t)info.n_const * N * 8);
+        if (!rc) rc = zkgpu_rows_to_cols_dev(S.sec[SEC_CONST_N], N, (const uint64_t *)tmp, N, info.n_const);
+        if (!rc) rc = zkgpu_synchronize();
+        zkgpu_dev_free(tmp);
+        if (rc) return fail("set_const: %s", zkgpu_last_error());
+        CK(zkgpu_gl_extend_pol_dev(S.sec[SEC_CONST_2NS], NE, S.sec[SEC_CONST_N], N, NE, N, info.n_const));
+        CK(zkgpu_gl_merkletree_dev(const_nodes, S.sec[SEC_CONST_2NS], NE, info.n_const, NE));
+        CK(zkgpu_memcpy_d2h(verkey, const_nodes + zkgpu_gl_merkle_num_elements(NE) - 4, 32));
+        return 0;
+    }
+
+    int set_publics(const uint64_t *p)
+    {
+        for (uint32_t k = 0; k < info.n_publics; k++) publics[k] = p[k] % P;
+        return 0;
+    }
+
     uint32_t q() const { return info.n_queries; }
 
     uint64_t proof_len() const
@@ -599,6 +622,8 @@ int zkgpu_stark_create(void **handle, const zkgpu_stark_info *info)
 
 int zkgpu_stark_witness(void *h) { return ((Starks *)h)->witness(); }
 int zkgpu_stark_set_cm1(void *h, const uint64_t *rows) { return ((Starks *)h)->set_cm1(rows); }
+int zkgpu_stark_set_const(void *h, const uint64_t *rows) { return ((Starks *)h)->set_const(rows); }
+int zkgpu_stark_set_publics(void *h, const uint64_t *publics) { return ((Starks *)h)->set_publics(publics); }
 uint64_t zkgpu_stark_proof_len(void *h) { return ((Starks *)h)->proof_len(); }
 int zkgpu_stark_prove(void *h, uint64_t *out) { return ((Starks *)h)->prove(out); }
 int zkgpu_stark_verkey(void *h, uint64_t out[4])
