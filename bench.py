@@ -61,11 +61,13 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-lde", action="store_true", help="skip the secondary LDE measurement (stark workload)")
     ap.add_argument("--lde-steps", type=int, default=10)
-    ap.add_argument("--workload", choices=["stark", "lde", "merkle", "commit", "stark-sharded"], default="stark",
+    ap.add_argument("--workload", choices=["stark", "lde", "merkle", "commit", "stark-sharded", "step42ns"],
+                    default="stark",
                     help="stark = configs[3] (headline: full synthetic STARK proof, 2^23 trace); lde = configs[1] "
                          "(2^23 -> 2^24 x 100 LDE); merkle = configs[2] (2^23 x 100 Poseidon tree); commit = "
                          "configs[4]'s commit step (one trace column-sharded over the ranks); stark-sharded = "
-                         "configs[4] (one proof over all ranks, strong scaling)")
+                         "configs[4] (one proof over all ranks, strong scaling); step42ns = the quotient program of "
+                         "the reference's zkEVM shape on the 2^(log_n+1) extended domain")
     ap.add_argument("--queries", type=int, default=128)
     ap.add_argument("--cpu-sample-bits", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_BITS", "18")))
     ap.add_argument("--cpu-sample-cols", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_COLS", "4")))
@@ -360,6 +362,59 @@ def lde_measure(args, dev, torch, world, dist):
     return lde, roof
 
 
+def step42ns_setup(args, dev, torch, g):
+    """The step42ns-shaped program (zkgpu/synthetic_bytecode.py, seed 1) on
+    the 2^(log_n+1)-row extended domain: cm1/cm2/cm3/cm4/const 2ns sections of
+    the fork-9 widths in HBM (about 12.5 KB per row), q_2ns written."""
+    import numpy as np
+    import zkgpu
+    import zkgpu.parser as zp
+    import zkgpu.synthetic_bytecode as sb
+    shape = sb.load_shape()
+    ops, a = sb.generate("step42ns", seed=1)
+    secs = sb.sections(shape)
+    prog = zp.convert(zp.STEP42NS, ops, a, secs, shape["n_bits"], shape["n_bits_ext"])
+    log_dom = args.log_n + 1
+    NE = 1 << log_dom
+    dsecs = {}
+    cols = 0
+    for sec, _, w in secs:
+        if sec >= 5:
+            dsecs[sec] = (torch.randint(0, 2**63 - 1, (w, NE), dtype=torch.int64, device=dev, generator=g), NE, w)
+            cols += w
+    dsecs[9] = (torch.randint(0, 2**63 - 1, (shape["n_const"], NE), dtype=torch.int64, device=dev, generator=g), NE,
+                shape["n_const"])
+    cols += shape["n_const"]
+    q = torch.zeros((3, NE), dtype=torch.int64, device=dev)
+    dsecs[10] = (q, NE, 3)
+    rng = np.random.default_rng(42)
+    P = 0xFFFFFFFF00000001
+    chal = rng.integers(0, P, (8, 3), dtype=np.uint64)
+    pub = rng.integers(0, P, 48, dtype=np.uint64)
+    evals = rng.integers(0, P, (4, 3), dtype=np.uint64)
+
+    def step():
+        zkgpu.zxp_eval_dev(prog, dsecs, log_dom, chal, pub, evals, extend_bits=1, x_start=7)
+
+    return step, {"rows": NE, "log_dom": log_dom, "n_ops": int(len(ops)), "cols_read": cols,
+                  "alg_bytes": 8.0 * NE * (cols + 3), "tensors": dsecs}
+
+
+def step42ns_roofline(s42, kernels, steps):
+    """HBM roofline of the compiled quotient kernel: every section column
+    read once + q written (8 B each per row) / its device time per launch."""
+    ks = {k: v for k, v in kernels.items() if k in ("k_zxp_jit", "k_zxp_eval")}
+    if not ks:
+        return None
+    dev_ms = sum(v[1] for v in ks.values()) / steps
+    achieved = s42["alg_bytes"] / (dev_ms * 1e-3) / 1e9
+    return {"kernel": ", ".join(sorted(ks)), "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "alg_bytes_per_launch": s42["alg_bytes"],
+            "alg_bytes_note": "8 B x rows x (%d section columns read + 3 q columns written)" % s42["cols_read"],
+            "avg_launch_ms": round(dev_ms, 4)}
+
+
 def cpu_full_main(args):
     """Time the oracle prover once at the full config-4 size (rank 0, no GPU)."""
     res = cpu_baseline_stark(args.log_n, args.blowup_bits, args.ncols, args.queries)
@@ -424,6 +479,8 @@ def main():
 
             def step():
                 ss.prove()
+        elif args.workload == "step42ns":
+            step, s42 = step42ns_setup(args, dev, torch, g)
         else:  # merkle
             src = torch.randint(0, 2**63 - 1, (C, n), dtype=torch.int64, device=dev, generator=g)
             nodes = torch.empty(zkgpu.merkle_num_elements(n), dtype=torch.int64, device=dev)
@@ -437,6 +494,9 @@ def main():
             value, unit, hib = elapsed / total, "s/proof", False
         elif args.workload == "commit":
             value, unit, hib = ne * C * args.steps / elapsed / 1e9, "Gelem/s", True
+        elif args.workload == "step42ns":
+            value, unit, hib = s42["rows"] * world * args.steps / elapsed / 1e6, "Mrow/s", True
+            roof = step42ns_roofline(s42, kernels, args.steps)
         else:
             value, unit, hib = n * C * world * args.steps / elapsed / 1e9, "Gelem/s", True
         stages = gs.timers() if gs is not None else (ss.timers if ss is not None else None)
@@ -475,6 +535,13 @@ def main():
             workload = ("LDE 2^%d -> 2^%d rows x %d cols per GPU (extendPol, starks.cpp:53), column-major in HBM"
                         % (args.log_n, args.log_n + args.blowup_bits, C))
             parallelism = "column-sharded x%d (no data-path collective)" % world
+        elif args.workload == "step42ns":
+            workload = ("Steps::step42ns_parser_first (constraint quotient, starks.cpp:241) over the 2^%d-row "
+                        "extended domain: a synthetic program with the reference step42ns bytecode's shape (%d ops, "
+                        "opcode histogram, fork-9 memory map, next-row reads; tests/golden/zkevm_bytecode_shape.json) "
+                        "through the product converter and the compiled expression kernel; sections resident in HBM"
+                        % (s42["log_dom"], s42["n_ops"]))
+            parallelism = "replicas x%d" % world
         elif args.workload == "commit":
             workload = ("column-sharded commit of one 2^%d-row x %d-col trace over %d rank(s): LDE, all-to-all "
                         "column->row blocks, per-rank Merkle subtree, sub-root gather + top levels (starks.cpp:53-57)"

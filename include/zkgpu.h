@@ -202,7 +202,10 @@ int zkgpu_zxp_compile(const void *instr, uint32_t n_instr, const void *opnd, uin
 /* Diagnostics for the run-time compiled expression kernels (csrc/zxp_jit.hip):
  * compile a program exactly as zkgpu_zxp_eval_dev does and write the
  * generated straight-line HIP kernel source into buf (truncated to buflen);
- * with rtc_check != 0 also compile it for gfx950 with hiprtc.  No GPU needed.
+ * with rtc_check != 0 also compile it for gfx950 with hiprtc (or find it in
+ * the on-disk code-object cache; rtc_check = 2 also writes the code object to
+ * $ZKGPU_ZXP_JIT_DUMP).  rtc_check = 3 only queries the cache: returns 1 when
+ * the compiled kernel is on disk, 0 when not.  No GPU needed.
  * Returns the source length (>= 0) or an error code. */
 int zkgpu_zxp_jit_source(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd, uint32_t n_tmp1,
                          uint32_t n_tmp3, const uint64_t *challenges, const uint64_t *publics, uint32_t n_publics,

@@ -103,3 +103,48 @@ def test_steps_parser_eval_host_dropin(oracle, zkgpu):
                             x, zh, q=qref)
     assert rc == 0 and qref.any()
     assert np.array_equal(q, qref)
+
+
+def test_step42ns_shaped_jit_gpu_equals_oracle(oracle, zkgpu, monkeypatch):
+    """the compiled expression kernel (csrc/zxp_jit.hip) of the step42ns-shaped
+    program at 2^16 rows == the oracle parser.  The kernel comes from the
+    on-disk cache build() fills (tools/jit_prebuild.py; hiprtc takes minutes
+    at this size), as the reference ships its expression code compiled."""
+    import torch
+    import zkgpu.parser as zp
+    import zkgpu.synthetic_bytecode as sb
+    monkeypatch.setenv("ZKGPU_ZXP_JIT", "2")
+    shape = sb.load_shape()
+    ops, args = sb.generate("step42ns", seed=1)
+    secs = sb.sections(shape)
+    prog = zp.convert(zp.STEP42NS, ops, args, secs, shape["n_bits"], shape["n_bits_ext"])
+    rng = np.random.default_rng(0)
+    assert zkgpu.zxp_jit_cached(prog, _rand(rng, (8, 3)), _rand(rng, 48), _rand(rng, (4, 3))), \
+        "compiled kernel not cached: run build() (tools/jit_prebuild.py)"
+    log_dom = 16
+    dom = 1 << log_dom
+    rng = np.random.default_rng(77)
+    S = {sec: _rand(rng, (dom, w)) for sec, _, w in secs if sec >= 5}
+    const = _rand(rng, (dom, shape["n_const"]))
+    chal, pub, evals = _rand(rng, (8, 3)), _rand(rng, 48), _rand(rng, (4, 3))
+    dsecs = {sec: (zkgpu.to_device(np.ascontiguousarray(a.T)), dom, a.shape[1]) for sec, a in S.items()}
+    dsecs[SEC_CONST_2NS] = (zkgpu.to_device(np.ascontiguousarray(const.T)), dom, const.shape[1])
+    q = torch.zeros((3, dom), dtype=torch.int64, device="cuda:0")
+    dsecs[SEC_Q_2NS] = (q, dom, 3)
+    zkgpu.prof_reset()
+    zkgpu.prof_enable(True)
+    zkgpu.zxp_eval_dev(prog, dsecs, log_dom, chal, pub, evals, extend_bits=1, x_start=7)
+    torch.cuda.synchronize()
+    zkgpu.prof_enable(False)
+    assert "k_zxp_jit" in zkgpu.prof_kernels(), "the compiled kernel did not run"
+    got = zkgpu.from_device(q).T
+    x = np.zeros(dom, np.uint64)
+    oracle.lib().oc_powers(oracle._p(x), 7, oracle.gl_w(log_dom), dom)
+    n = dom >> 1
+    zh = np.array([pow((pow(7, n, P) * pow(P - 1, i, P) - 1) % P, P - 2, P) for i in range(2)], np.uint64)
+    qref = np.zeros((dom, 3), np.uint64)
+    off = {sec: o for sec, o, _ in secs}
+    rc = oracle.parser_eval(3, ops, args, [(off[sec], a.shape[1], a) for sec, a in S.items()], const, dom,
+                            1 << shape["n_bits_ext"], 1196, 175, chal, pub, evals, x, zh, q=qref)
+    assert rc == 0 and qref.any()
+    assert np.array_equal(got, qref)

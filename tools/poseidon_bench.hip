@@ -96,9 +96,28 @@ __global__ void __launch_bounds__(256) k_perm(uint64_t *st_all, uint64_t n, int 
     for (int k = 0; k < 12; k++) st_all[k * n + i] = gl_canon(st[k]);
 }
 
+// K states per thread (perm_fast_k): thread i owns states i + k * n / K
+template <int K, bool SPLIT = false>
+__global__ void __launch_bounds__(256) k_permK(uint64_t *st_all, uint64_t n, int reps)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t m = n / K;
+    if (i >= m) return;
+    uint64_t st[K][12];
+#pragma unroll
+    for (int k = 0; k < K; k++)
+#pragma unroll
+        for (int j = 0; j < 12; j++) st[k][j] = st_all[j * n + i + k * m];
+    for (int r = 0; r < reps; r++) perm_fast_k<K, SPLIT>(st);
+#pragma unroll
+    for (int k = 0; k < K; k++)
+#pragma unroll
+        for (int j = 0; j < 12; j++) st_all[j * n + i + k * m] = gl_canon(st[k][j]);
+}
+
 int main()
 {
-    const uint64_t n = 1 << 21;
+    const uint64_t n = 3 << 20;  // divisible by 2 and 3
     const int reps = 8;
     uint64_t *h = (uint64_t *)malloc(12 * n * 8), *ref = (uint64_t *)malloc(12 * n * 8), *o = (uint64_t *)malloc(12 * n * 8);
     uint64_t x = 0x5EED;
@@ -120,14 +139,19 @@ int main()
         {"fast (FFT MDS + block dots)", k_perm<4>},
         {"fast, multiply-add MDS (mds_fold)", k_perm<5>},
         {"fast, older MDS form", k_perm<6>},
+        {"fast, K=1 generic (perm_fast_k)", k_permK<1>},
+        {"fast, 2 states per thread", k_permK<2>},
+        {"fast, split partial-round dots", k_permK<1, true>},
+        {"fast, 2 states, split dots", k_permK<2, true>},
     };
+    const int nthreads_div[] = {1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 2};
     int bad = 0;
-    for (int v = 0; v < 7; v++) {
+    for (int v = 0; v < 11; v++) {
         float best = 1e30f;
         for (int rep = 0; rep < 3; rep++) {
             (void)hipMemcpy(d, h, 12 * n * 8, hipMemcpyHostToDevice);
             (void)hipEventRecord(e0);
-            hipLaunchKernelGGL(ks[v].f, dim3((uint32_t)(n / 256)), dim3(256), 0, 0, d, n, reps);
+            hipLaunchKernelGGL(ks[v].f, dim3((uint32_t)((n / nthreads_div[v] + 255) / 256)), dim3(256), 0, 0, d, n, reps);
             (void)hipEventRecord(e1);
             (void)hipEventSynchronize(e1);
             float ms;

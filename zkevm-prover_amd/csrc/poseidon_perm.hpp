@@ -430,6 +430,132 @@ __device__ __forceinline__ void perm_fast(uint64_t st[12])
     full_rounds_fold(st, 26);
 }
 
+// ---- K independent permutations per thread, step by step interleaved: the
+// partial rounds are one serial chain per state (S-box of s0 -> dot product
+// -> next S-box), so a second state doubles the independent work the
+// scheduler has to hide that chain's latency
+template <int K>
+__device__ __forceinline__ void full_rounds_fold_k(uint64_t (*st)[12], int r0)
+{
+#pragma unroll 1
+    for (int r = r0; r < r0 + 4; r++) {
+#pragma unroll
+        for (int k = 0; k < K; k++)
+#pragma unroll
+            for (int s = 0; s < 12; s++) st[k][s] = pow7(st[k][s]);
+        const uint64_t *Kc = r == 3 ? ZKGPU_PSP_PRE : (r == 29 ? ZKGPU_PS_ZERO12 : &ZKGPU_POSEIDON_RC[(r + 1) * 12]);
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            if constexpr (ZKGPU_MDS_FFT)
+                mds_fft_fold(st[k], Kc);
+            else
+                mds_fold(st[k], Kc);
+        }
+    }
+}
+
+// SPLIT: each dot product in two halves summed at the end (two independent
+// multiply-add chains per accumulator instead of one; the sum of the halves'
+// carry-free accumulators is the same integer)
+template <int K, bool SPLIT, int t>
+__device__ __forceinline__ void psb_step_k(uint64_t *x, uint64_t (*y)[ZKGPU_PSB_BLOCK], const uint64_t (*L)[11],
+                                           const uint32_t *T)
+{
+    constexpr int o = psb_xoff(t);
+#pragma unroll
+    for (int k = 0; k < K; k++) y[k][t] = pow7(x[k]);
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        Dot3 d(T + o);
+        if constexpr (SPLIT) {
+            Dot3 e;
+            d.term(y[k][t], T + o + 3);
+#pragma unroll
+            for (int j = 0; j < 11; j++) {
+                if (j & 1) d.term(L[k][j], T + o + 9 + 6 * j);
+                else e.term(L[k][j], T + o + 9 + 6 * j);
+            }
+#pragma unroll
+            for (int i = 0; i < t; i++) {
+                if (i & 1) e.term(y[k][i], T + o + 75 + 6 * i);
+                else d.term(y[k][i], T + o + 75 + 6 * i);
+            }
+            d.A0 += e.A0;
+            d.A1 += e.A1;
+            d.A2 += e.A2;
+        } else {
+            d.term(y[k][t], T + o + 3);
+#pragma unroll
+            for (int j = 0; j < 11; j++) d.term(L[k][j], T + o + 9 + 6 * j);
+#pragma unroll
+            for (int i = 0; i < t; i++) d.term(y[k][i], T + o + 75 + 6 * i);
+        }
+        x[k] = d.fin();
+    }
+}
+
+template <int K, bool SPLIT, int... ts>
+__device__ __forceinline__ void psb_steps_k(uint64_t *x, uint64_t (*y)[ZKGPU_PSB_BLOCK], const uint64_t (*L)[11],
+                                            const uint32_t *T, std::integer_sequence<int, ts...>)
+{
+    (psb_step_k<K, SPLIT, ts>(x, y, L, T), ...);
+}
+
+template <int K, bool SPLIT>
+__device__ __forceinline__ void partial_rounds_blocks_k(uint64_t (*st)[12])
+{
+    uint64_t L[K][11];
+#pragma unroll
+    for (int k = 0; k < K; k++)
+#pragma unroll
+        for (int i = 0; i < 11; i++) {
+            Dot3 d(&ZKGPU_PSB_D0[i * 69]);
+#pragma unroll
+            for (int j = 0; j < 11; j++) d.term(st[k][1 + j], &ZKGPU_PSB_D0[i * 69 + 3 + 6 * j]);
+            L[k][i] = d.fin();
+        }
+    uint64_t x[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) x[k] = st[k][0];
+#pragma unroll 1
+    for (int b = 0; b < ZKGPU_PSB_NBLOCKS; b++) {
+        const uint32_t *T = &ZKGPU_PSB_BLOCKS[b * ZKGPU_PSB_BLOCK_WORDS];
+        uint64_t y[K][ZKGPU_PSB_BLOCK];
+        psb_steps_k<K, SPLIT>(x, y, L, T, std::make_integer_sequence<int, ZKGPU_PSB_BLOCK>{});
+        constexpr int base = psb_xoff(ZKGPU_PSB_BLOCK);
+#pragma unroll
+        for (int k = 0; k < K; k++)
+#pragma unroll
+            for (int j = 0; j < 11; j++) {
+                const uint32_t *Tj = T + base + j * (3 + 6 * ZKGPU_PSB_BLOCK);
+                Dot3 d(Tj);
+                d.lane(L[k][j]);
+#pragma unroll
+                for (int i = 0; i < ZKGPU_PSB_BLOCK; i++) d.term(y[k][i], Tj + 3 + 6 * i);
+                L[k][j] = d.fin();
+            }
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        st[k][0] = x[k];
+#pragma unroll
+        for (int j = 0; j < 11; j++) st[k][1 + j] = L[k][j];
+    }
+}
+
+// K permutations, bit-identical to K calls of perm_fast
+template <int K, bool SPLIT = false>
+__device__ __forceinline__ void perm_fast_k(uint64_t (*st)[12])
+{
+#pragma unroll
+    for (int k = 0; k < K; k++)
+#pragma unroll
+        for (int s = 0; s < 12; s++) st[k][s] = gl_add(st[k][s], ZKGPU_POSEIDON_RC[s]);
+    full_rounds_fold_k<K>(st, 0);
+    partial_rounds_blocks_k<K, SPLIT>(st);
+    full_rounds_fold_k<K>(st, 26);
+}
+
 // the permutation the product kernels use
 __device__ __forceinline__ void poseidon_perm(uint64_t st[12]) { perm_fast(st); }
 

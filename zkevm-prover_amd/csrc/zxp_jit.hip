@@ -911,6 +911,10 @@ extern "C" int zkgpu_zxp_jit_source(const void *instr, uint32_t n_instr, const v
         memcpy(buf, src.data(), n);
         buf[n] = 0;
     }
+    if (rtc_check == 3) {  // cache query only: 1 = compiled object on disk
+        std::vector<char> code;
+        return cache_load(src, code) ? 1 : 0;
+    }
     if (rtc_check) {
         // compile (or find in the disk cache); rtc_check == 2 also writes the
         // code object to $ZKGPU_ZXP_JIT_DUMP (register / scratch inspection)

@@ -423,6 +423,26 @@ def zxp_jit_source(prog, challenges, publics, evals=None, rtc_check=False):
     return buf.value.decode()
 
 
+def zxp_jit_cached(prog, challenges, publics, evals=None):
+    """True when the program's compiled kernel is in the on-disk cache
+    (zkgpu_zxp_jit_source with rtc_check = 3; no compile, no GPU)."""
+    ins, opn = prog.arrays()
+    ins = np.ascontiguousarray(ins, np.uint32)
+    opn = np.ascontiguousarray(opn, np.uint32)
+    ch = np.zeros(24, np.uint64)
+    c = _np(challenges).reshape(-1)
+    ch[:c.size] = c
+    pub = _np(publics if publics is not None else np.zeros(1, np.uint64))
+    ev = _np(evals if evals is not None else np.zeros(3, np.uint64)).reshape(-1)
+    rc = lib().zkgpu_zxp_jit_source(ins.ctypes.data, ins.shape[0], opn.ctypes.data, opn.shape[0],
+                                    max(prog.n_tmp1, 1), max(prog.n_tmp3, 1), ch.ctypes.data, pub.ctypes.data,
+                                    pub.size if publics is not None else 0, ev.ctypes.data, ev.size // 3,
+                                    None, 0, 3)
+    if rc < 0:
+        _check(rc, "zkgpu_zxp_jit_source")
+    return rc == 1
+
+
 def zxp_eval_block_dev(prog, sections, log_rows, log_domain, challenges, publics, evals=None, xdiv=None, xdivw=None,
                        extend_bits=0, x_start=7):
     """One row block of a row-sharded domain (zkgpu_zxp_eval_block_dev):
