@@ -107,15 +107,16 @@ def test_steps_parser_eval_host_dropin(oracle, zkgpu):
 
 def test_step42ns_shaped_jit_gpu_equals_oracle(oracle, zkgpu, monkeypatch):
     """the compiled expression kernel (csrc/zxp_jit.hip) of the step42ns-shaped
-    program at 2^16 rows == the oracle parser.  The kernel comes from the
-    on-disk cache build() fills (tools/jit_prebuild.py; hiprtc takes minutes
-    at this size), as the reference ships its expression code compiled."""
+    program (a quarter of step42ns's opcode counts, 5.3 K ops) at 2^16 rows ==
+    the oracle parser.  The kernel comes from the on-disk cache build() fills
+    (tools/jit_prebuild.py; hiprtc takes minutes at this size), as the
+    reference ships its expression code compiled."""
     import torch
     import zkgpu.parser as zp
     import zkgpu.synthetic_bytecode as sb
     monkeypatch.setenv("ZKGPU_ZXP_JIT", "2")
     shape = sb.load_shape()
-    ops, args = sb.generate("step42ns", seed=1)
+    ops, args = sb.generate("step42ns", seed=1, scale=0.25)
     secs = sb.sections(shape)
     prog = zp.convert(zp.STEP42NS, ops, args, secs, shape["n_bits"], shape["n_bits_ext"])
     rng = np.random.default_rng(0)

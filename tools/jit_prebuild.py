@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Fill the on-disk code-object cache (zkevm-prover_amd/jitcache, see
 csrc/zxp_jit.hip cache_dir) for the compiled expression kernels the GPU tests
-and bench.py run on programs of the zkEVM's size: the step42ns-shaped
-synthetic program (zkgpu/synthetic_bytecode.py, seed 1) converted like the
-reference's bytecode.  A program's kernel depends only on its structure, so
+and bench.py run on programs of zkEVM size: the step42ns-shaped synthetic
+program (zkgpu/synthetic_bytecode.py, seed 1) at a quarter of step42ns's
+opcode counts (5.3 K ops, ~2 min of hiprtc; the full 20 K-op program takes
+over an hour), converted like the reference's bytecode.  A program's kernel depends only on its structure, so
 one compile serves every proof (the reference likewise ships its expression
 code compiled, chelpers/*.cpp).  No GPU needed (hiprtc cross-compiles).
 
@@ -19,15 +20,16 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "zkevm-prover_amd")]
 import numpy as np  # noqa: E402
 
 P = 0xFFFFFFFF00000001
+JIT_SCALE = 0.25  # tests/test_gpu_parser.py uses the same program
 
 
 def programs():
     import zkgpu.parser as zp
     import zkgpu.synthetic_bytecode as sb
     shape = sb.load_shape()
-    ops, args = sb.generate("step42ns", seed=1)
+    ops, args = sb.generate("step42ns", seed=1, scale=JIT_SCALE)
     prog = zp.convert(zp.STEP42NS, ops, args, sb.sections(shape), shape["n_bits"], shape["n_bits_ext"])
-    yield "step42ns-shaped (seed 1)", prog
+    yield "step42ns-shaped (seed 1, scale %g)" % JIT_SCALE, prog
 
 
 def main():

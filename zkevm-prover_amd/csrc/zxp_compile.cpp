@@ -29,6 +29,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <unordered_map>
+#include <map>
 #include <vector>
 
 #include "../../include/zkgpu.h"
@@ -694,6 +695,40 @@ struct Out {
 };
 thread_local Out g_out;
 
+// Peak temporary words (1 per base, 3 per extension value) live at once in
+// the source order: every definition of a slot lives to its last read
+// before the slot's next definition.
+uint32_t source_peak_live(const zxp_instr *in, uint32_t n, const zxp_operand *op)
+{
+    std::vector<int64_t> delta((size_t)n + 2, 0);
+    std::map<std::pair<uint32_t, uint32_t>, std::pair<uint32_t, uint32_t>> cur;  // slot -> [def, last read]
+    auto width = [](uint32_t kind) { return kind == ZXP_TMP3 ? 3 : 1; };
+    auto close = [&](const std::pair<uint32_t, uint32_t> &key, const std::pair<uint32_t, uint32_t> &iv) {
+        delta[iv.first] += width(key.first);
+        delta[(size_t)iv.second + 1] -= width(key.first);
+    };
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t srcs[2] = {in[k].a, in[k].b};
+        for (int j = 0; j < (in[k].op == ZXP_COPY ? 1 : 2); j++) {
+            const zxp_operand &o = op[srcs[j]];
+            if (o.kind != ZXP_TMP1 && o.kind != ZXP_TMP3) continue;
+            auto it = cur.find({o.kind, o.a});
+            if (it != cur.end()) it->second.second = k;
+        }
+        const zxp_operand &d = op[in[k].dst];
+        if (d.kind == ZXP_TMP1 || d.kind == ZXP_TMP3) {
+            const std::pair<uint32_t, uint32_t> key{d.kind, d.a};
+            auto it = cur.find(key);
+            if (it != cur.end()) close(key, it->second);
+            cur[key] = {k, k};
+        }
+    }
+    for (const auto &kv : cur) close(kv.first, kv.second);
+    int64_t live = 0, peak = 0;
+    for (size_t k = 0; k < delta.size(); k++) peak = std::max(peak, live += delta[k]);
+    return (uint32_t)peak;
+}
+
 }  // namespace
 
 extern "C" int zkgpu_zxp_compile(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd,
@@ -735,11 +770,17 @@ extern "C" int zkgpu_zxp_compile(const void *instr, uint32_t n_instr, const void
         if (dk != ZXP_TMP1 && dk != ZXP_TMP3 && dk != ZXP_COL && dk != ZXP_COL3)
             return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u writes a read-only operand", k);
     }
-    // reschedule for register pressure (ZKGPU_ZXP_SCHED=0: source order)
-    static const int sched_on = [] {
+    // reschedule for register pressure when the source order keeps more than
+    // 96 temporary words live (the zkEVM's bytecode: ~1,200); otherwise keep
+    // the producer's order, in which each constraint is folded into the
+    // accumulator as soon as it is computed (the 2^23 config-4 quotient: 186
+    // VGPRs in source order, 512 + spills scheduled).
+    // ZKGPU_ZXP_SCHED = 0 never, 1 always, unset: by that estimate.
+    static const int sched_env = [] {
         const char *e = getenv("ZKGPU_ZXP_SCHED");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : -1;
     }();
+    const bool sched_on = sched_env < 0 ? source_peak_live(in, n_instr, op) > 96 : sched_env != 0;
     Scheduled sp;
     if (sched_on) {
         schedule(in, n_instr, op, n_opnd, n_tmp1, n_tmp3, sp);

@@ -222,10 +222,14 @@ int rtc_compile(const std::string &src, std::vector<char> &code)
     // doubled the compile time of the large programs; register pressure is
     // already bounded by the ZXP scheduler (csrc/zxp_compile.cpp), so they
     // are off unless ZKGPU_ZXP_JIT_RESCHED=1.
-    static const bool resched = [] {
+    // Small programs keep them: there they lower register pressure (config-4
+    // quotient 17.2 -> 15.2 ms, FRI polynomial 10.4 -> 9.1 ms at 2^23) and
+    // cost little compile time.
+    static const int resched_env = [] {
         const char *e = getenv("ZKGPU_ZXP_JIT_RESCHED");
-        return e && atoi(e) != 0;
+        return e ? atoi(e) : -1;
     }();
+    const bool resched = resched_env < 0 ? src.find("#define ZKJIT_SPLIT 1") == std::string::npos : resched_env != 0;
     std::vector<const char *> opts = {"--offload-arch=gfx950", olev.c_str(), "-std=c++17"};
     if (!resched) {
         opts.push_back("-mllvm");
@@ -545,10 +549,13 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     // fork-9 step42ns peaked at ~1,300 live words with unbounded streaming
     // against ~110 without.  Only sources defined at most STREAM_SPAN
     // instructions before their DOT are streamed.
-    static const int64_t stream_span = [] {
+    // Small programs (< 1,000 compiled instructions: one or two Horner
+    // accumulators over the whole program) stream without limit.
+    static const int64_t stream_span_env = [] {
         const char *e = getenv("ZKGPU_ZXP_JIT_STREAM_SPAN");
-        return (int64_t)(e ? atol(e) : 24);
+        return (int64_t)(e ? atol(e) : -1);
     }();
+    const int64_t stream_span = stream_span_env >= 0 ? stream_span_env : (in.n_instr < 1000 ? INT64_MAX / 4 : 24);
     {
         uint32_t nt = 0;
         for (uint32_t k = 0; k < in.n_instr; k++)
@@ -629,14 +636,23 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         const long b = e ? atol(e) : 4096;
         return (size_t)(b > 0 ? b : 1L << 40);
     }();
+    // Only programs of ZKGPU_ZXP_JIT_SPLIT_MIN (1000) compiled instructions or
+    // more are split: the opaque branch costs registers (config-4 FRI
+    // polynomial: 74 -> 200 VGPRs, 9 -> 57 ms), and small programs compile in
+    // seconds as one block.
+    static const uint32_t split_min = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_SPLIT_MIN");
+        return (uint32_t)(e ? atol(e) : 1000);
+    }();
+    const bool split = in.n_instr >= split_min;
     size_t block_start = 0;
     auto maybe_split = [&] {
-        if (body.size() - block_start >= block) {
+        if (split && body.size() - block_start >= block) {
             body += "}\nif (zk_one()) { ZK_KREFRESH\n";
             block_start = body.size();
         }
     };
-    body += "if (zk_one()) {\n";
+    body += split ? "if (zk_one()) {\n" : "{\n";
     auto emit_streams = [&](uint32_t at) {
         for (const Stream &st : stream[at]) {
             maybe_split();
@@ -776,6 +792,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     // assemble: prelude, params, declarations, body, deferred stores
     src = k_gl_device_src;
     appendf(src, "#define ZKJIT_KL_LDS %d\n", jit_kl_lds(kl.size()) ? 1 : 0);
+    appendf(src, "#define ZKJIT_SPLIT %d\n", split ? 1 : 0);  // large program: compile-time options (rtc_compile)
     {
         static const int unroll = [] {  // column terms per loop iteration (loads in flight)
             const char *e = getenv("ZKGPU_ZXP_JIT_UNROLL");

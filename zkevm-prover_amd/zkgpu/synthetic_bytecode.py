@@ -96,9 +96,10 @@ class _Gen:
         return self.map[s]["offset"] + c, width
 
 
-def generate(name="step42ns", seed=1, shape=None, isa=None):
+def generate(name="step42ns", seed=1, shape=None, isa=None, scale=1.0):
     """(ops, args) uint64 arrays of a synthetic program shaped like the
-    reference's `name` program (currently step42ns: constraint quotient).
+    reference's `name` program (currently step42ns: constraint quotient);
+    scale < 1 keeps that fraction of every opcode count (same mix, same map).
 
     Values form constraint trees: an opcode's temporary operands are taken
     from the not-yet-used values (most recent first), its result joins them;
@@ -113,7 +114,7 @@ def generate(name="step42ns", seed=1, shape=None, isa=None):
     table = isa[name]
     rng = np.random.default_rng(seed)
     g = _Gen(name, shape, rng)
-    hist = {int(k): v for k, v in g.sh["opcode_hist"].items()}
+    hist = {int(k): max(1, int(round(v * scale))) for k, v in g.sh["opcode_hist"].items()}
     n84, n87 = hist.pop(84, 0), hist.pop(87, 0)
     hist.pop(69, None)
     body = np.repeat(np.array(list(hist), np.int64), list(hist.values()))
