@@ -69,6 +69,9 @@ def parse():
                          "configs[4] (one proof over all ranks, strong scaling); step42ns = the quotient program of "
                          "the reference's zkEVM shape on the 2^(log_n+1) extended domain")
     ap.add_argument("--queries", type=int, default=128)
+    ap.add_argument("--s42-scale", type=float, default=1.0,
+                    help="step42ns workload: fraction of the reference step42ns opcode counts")
+    ap.add_argument("--s42-jit", action="store_true", help="step42ns workload: the compiled kernel (else interpreter)")
     ap.add_argument("--cpu-sample-bits", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_BITS", "18")))
     ap.add_argument("--cpu-sample-cols", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_COLS", "4")))
     ap.add_argument("--cpu-full", action="store_true",
@@ -371,7 +374,7 @@ def step42ns_setup(args, dev, torch, g):
     import zkgpu.parser as zp
     import zkgpu.synthetic_bytecode as sb
     shape = sb.load_shape()
-    ops, a = sb.generate("step42ns", seed=1)
+    ops, a = sb.generate("step42ns", seed=1, scale=args.s42_scale)
     secs = sb.sections(shape)
     prog = zp.convert(zp.STEP42NS, ops, a, secs, shape["n_bits"], shape["n_bits_ext"])
     log_dom = args.log_n + 1
@@ -397,8 +400,9 @@ def step42ns_setup(args, dev, torch, g):
         zkgpu.zxp_eval_dev(prog, dsecs, log_dom, chal, pub, evals, extend_bits=1, x_start=7)
 
     # the full-size program runs on the interpreter: its compiled kernel takes
-    # over an hour of hiprtc
-    os.environ["ZKGPU_ZXP_JIT"] = "0"
+    # over an hour of hiprtc; --s42-jit with a smaller
+    # --s42-scale (0.25: cached by build()) times the compiled kernel
+    os.environ["ZKGPU_ZXP_JIT"] = "2" if args.s42_jit else "0"
     return step, {"rows": NE, "log_dom": log_dom, "n_ops": int(len(ops)), "cols_read": cols,
                   "alg_bytes": 8.0 * NE * (cols + 3), "tensors": dsecs}
 
@@ -540,10 +544,11 @@ def main():
             parallelism = "column-sharded x%d (no data-path collective)" % world
         elif args.workload == "step42ns":
             workload = ("Steps::step42ns_parser_first (constraint quotient, starks.cpp:241) over the 2^%d-row "
-                        "extended domain: a synthetic program with the reference step42ns bytecode's shape (%d ops, "
-                        "opcode histogram, fork-9 memory map, next-row reads; tests/golden/zkevm_bytecode_shape.json) "
-                        "through the product converter and the compiled expression kernel; sections resident in HBM"
-                        % (s42["log_dom"], s42["n_ops"]))
+                        "extended domain: a synthetic program with the reference step42ns bytecode's shape (%d ops = "
+                        "%g x the opcode histogram, fork-9 memory map, next-row reads; tests/golden/"
+                        "zkevm_bytecode_shape.json) through the product converter and the %s; sections resident in HBM"
+                        % (s42["log_dom"], s42["n_ops"], args.s42_scale,
+                           "compiled expression kernel" if args.s42_jit else "expression interpreter"))
             parallelism = "replicas x%d" % world
         elif args.workload == "commit":
             workload = ("column-sharded commit of one 2^%d-row x %d-col trace over %d rank(s): LDE, all-to-all "

@@ -3,7 +3,7 @@
 # stops at the first fault / abort / segfault / timeout (exit >= 124 or
 # signal), but continues past an ordinary test failure (exit 1).
 # Usage: tools/gpu_job.sh <step>...
-#   steps: tests large smoke bench instbench bwbench parser prof pmc starkpmc cpufull merkle commit sharded
+#   steps: tests large smoke bench instbench bwbench parser step42ns prof pmc starkpmc cpufull merkle commit sharded
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOTDIR=$(pwd)
@@ -22,7 +22,7 @@ for step in "$@"; do
     case "$step" in
     tests)
         timeout -k 10 1200 $PYT tests -m gpu --deselect tests/test_gpu_large.py --deselect tests/test_gpu_config4.py \
-            > gpurun_out/pytest_gpu.log 2>&1
+            ${PYTEST_EXTRA:-} > gpurun_out/pytest_gpu.log 2>&1
         ok_or_stop $? "pytest -m gpu"
         tail -5 gpurun_out/pytest_gpu.log
         ;;
@@ -102,6 +102,12 @@ for step in "$@"; do
             cd "$ROOTDIR"
             ok_or_stop $rc "rocprofv3 stark pmc $out"
         done
+        ;;
+    step42ns)
+        timeout -k 10 600 python bench.py --workload step42ns --no-cpu --steps 3 --warmup 1 \
+            > gpurun_out/bench_step42ns.json 2> gpurun_out/bench_step42ns.err
+        ok_or_stop $? "bench step42ns"
+        cat gpurun_out/bench_step42ns.json
         ;;
     merkle)
         timeout -k 10 600 python bench.py --workload merkle --steps 3 --warmup 1 > gpurun_out/bench_merkle.json 2> gpurun_out/bench_merkle.err
