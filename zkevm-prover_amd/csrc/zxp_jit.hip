@@ -627,13 +627,17 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     };
     // Compile time: LLVM's instruction selection and machine scheduler are
     // superlinear in basic-block size (a 600-instruction program took ~60 s
-    // as one block).  Every ZKGPU_ZXP_JIT_BLOCK instructions the body opens a
+    // as one block).  Every ZKGPU_ZXP_JIT_BLOCK source bytes the body opens a
     // new block behind a uniform branch on an opaque 1 (zk_one(): an
     // s_mov_b32 the optimiser cannot see through, so it cannot merge the
-    // blocks back), so each block is compiled on its own.
+    // blocks back), so each block is compiled on its own.  The block size also
+    // bounds how far the scheduler hoists column loads: quarter-size
+    // step42ns-shaped program at 2^24 rows, 256 / 512 / 1024 / 4096 bytes ->
+    // 184 / 246 / 246 / 512+spills VGPRs, 453 / 359 / 303 / 394 ms, hiprtc
+    // 63 / 56 / 80 / 116 s.
     static const size_t block = [] {  // source bytes per block
         const char *e = getenv("ZKGPU_ZXP_JIT_BLOCK");
-        const long b = e ? atol(e) : 4096;
+        const long b = e ? atol(e) : 1024;
         return (size_t)(b > 0 ? b : 1L << 40);
     }();
     // Only programs of ZKGPU_ZXP_JIT_SPLIT_MIN (1000) compiled instructions or
