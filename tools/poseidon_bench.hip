@@ -115,6 +115,21 @@ __global__ void __launch_bounds__(256) k_permK(uint64_t *st_all, uint64_t n, int
         for (int j = 0; j < 12; j++) st_all[j * n + i + k * m] = gl_canon(st[k][j]);
 }
 
+// occupancy targets: the product leaf kernel runs at 89 VGPRs = 5 waves/SIMD
+template <int W>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) k_perm_w(uint64_t *st_all, uint64_t n,
+                                                                                             int reps)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t st[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) st[k] = st_all[k * n + i];
+    for (int r = 0; r < reps; r++) perm_fast(st);
+#pragma unroll
+    for (int k = 0; k < 12; k++) st_all[k * n + i] = gl_canon(st[k]);
+}
+
 int main()
 {
     const uint64_t n = 3 << 20;  // divisible by 2 and 3
@@ -143,10 +158,13 @@ int main()
         {"fast, 2 states per thread", k_permK<2>},
         {"fast, split partial-round dots", k_permK<1, true>},
         {"fast, 2 states, split dots", k_permK<2, true>},
+        {"fast, 6 waves/SIMD target", k_perm_w<6>},
+        {"fast, 7 waves/SIMD target", k_perm_w<7>},
+        {"fast, 8 waves/SIMD target", k_perm_w<8>},
     };
-    const int nthreads_div[] = {1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 2};
+    const int nthreads_div[] = {1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 2, 1, 1, 1};
     int bad = 0;
-    for (int v = 0; v < 11; v++) {
+    for (int v = 0; v < 14; v++) {
         float best = 1e30f;
         for (int rep = 0; rep < 3; rep++) {
             (void)hipMemcpy(d, h, 12 * n * 8, hipMemcpyHostToDevice);
