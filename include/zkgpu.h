@@ -46,6 +46,9 @@ int zkgpu_init(int device);
 void zkgpu_release(void);
 const char *zkgpu_last_error(void);
 int zkgpu_set_stream(void *hip_stream);
+/* the stream every zkgpu call is enqueued on (collectives of a sharded
+ * prover are enqueued on it too, include/zkgpu_stark.h zkgpu_comm) */
+void *zkgpu_get_stream(void);
 int zkgpu_synchronize(void);
 /* number of exported entry points (ABI self-check for tests) */
 int zkgpu_abi_version(void);

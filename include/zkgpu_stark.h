@@ -85,6 +85,48 @@ int zkgpu_stark_timers(void *handle, char *names_buf, uint64_t names_len, double
 void zkgpu_stark_destroy(void *handle);
 const char *zkgpu_stark_last_error(void);
 
+/* ---- one proof sharded over the GPUs of a node (BASELINE
+ * configs[4]: "the same BatchProof trace column-sharded across 8 x MI355X").
+ * The reference proves on one host (Starks::genProof, starks.cpp:9-404); this
+ * is the multi-GPU form of the same proof, bit-identical to it.
+ *
+ * Point-to-point exchange between the ranks of a sharded prover: one grouped
+ * batch of sends and receives of DEVICE buffers.  Operations with the same
+ * peer and direction match in order on both sides; never peer == rank.  The
+ * call returns once work enqueued afterwards on the zkgpu stream
+ * (zkgpu_get_stream) sees the received bytes; the send buffers are not
+ * modified before that either. */
+typedef struct {
+    int32_t peer;
+    int32_t send; /* 1: send buf to peer; 0: receive into buf from peer */
+    void *buf;    /* device pointer */
+    uint64_t bytes;
+} zkgpu_comm_op;
+
+typedef struct {
+    uint32_t rank, world; /* world a power of two */
+    void *ctx;
+    int (*exchange)(void *ctx, const zkgpu_comm_op *ops, uint32_t n_ops);
+} zkgpu_comm;
+
+/* The RCCL implementation (ncclSend / ncclRecv inside ncclGroupStart/End,
+ * enqueued on the zkgpu stream; xGMI between the GPUs of a node).  One rank
+ * makes the id and hands it to the others (any side channel); every rank then
+ * creates its communicator with its own rank.  librccl is opened at run time. */
+int zkgpu_comm_rccl_unique_id(uint8_t id[128]);
+int zkgpu_comm_rccl_create(zkgpu_comm *comm, const uint8_t id[128], uint32_t world, uint32_t rank);
+void zkgpu_comm_rccl_destroy(zkgpu_comm *comm);
+
+/* A prover whose extended (2n) domain is row-sharded over comm->world ranks:
+ * rank r holds rows [r 2n/W, (r+1) 2n/W) of every extended section (plus the
+ * next block's first 2^blowup rows), its share of the commitments' LDE
+ * columns, and the subtrees of its rows; the n-domain sections are whole on
+ * every rank.  Every rank calls the same functions in the same order
+ * (witness / set_cm1 / set_const / set_publics / prove are collective) and
+ * every rank's zkgpu_stark_prove returns the same proof, equal to
+ * zkgpu_stark_create's.  comm is copied; comm->ctx must outlive the handle. */
+int zkgpu_stark_create_sharded(void **handle, const zkgpu_stark_info *info, const zkgpu_comm *comm);
+
 #ifdef __cplusplus
 }
 #endif

@@ -296,6 +296,8 @@ int zkgpu_set_stream(void *s)
     return 0;
 }
 
+void *zkgpu_get_stream(void) { return (void *)g_ctx.stream; }
+
 int zkgpu_synchronize(void) { return check_hip(hipStreamSynchronize(g_ctx.stream), "synchronize"); }
 
 // ---------------------------------------------------------------- NTT

@@ -15,6 +15,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <string>
 #include <vector>
@@ -168,7 +169,7 @@ public:
     std::vector<uint64_t> publics;
     std::vector<std::pair<std::string, double>> timers;
 
-    ~Starks()
+    virtual ~Starks()
     {
         for (void *p : allocs) zkgpu_dev_free(p);
     }
@@ -183,6 +184,13 @@ public:
     }
 
     int create(const zkgpu_stark_info *in)
+    {
+        if (load(in) || alloc()) return -1;
+        return build_const();
+    }
+
+    // validate the description, keep the programs, bind the device
+    int load(const zkgpu_stark_info *in)
     {
         info = *in;
         random_cols.assign(in->random_cols, in->random_cols + in->n_random_cols);
@@ -237,23 +245,27 @@ public:
         NE = 1ULL << in->n_bits_ext;
         eb = in->n_bits_ext - in->n_bits;
         CK(zkgpu_init(-1));
+        return 0;
+    }
+
+    // the n-domain sections (every prover holds them whole)
+    int alloc_n()
+    {
         memset(&S, 0, sizeof S);
+        const zkgpu_stark_info *in = &info;
         const uint32_t widths_n[5] = {in->n_cm1, in->n_cm2, in->n_cm3, in->n_tmp, in->n_const};
         for (int s = 0; s < 5; s++) {
             if (dalloc(&S.sec[s], (uint64_t)(widths_n[s] ? widths_n[s] : 1) * N)) return -1;
             S.ld[s] = N;
             S.ncols[s] = widths_n[s];
         }
-        const uint32_t widths_e[7] = {in->n_cm1, in->n_cm2, in->n_cm3, in->n_cm4, in->n_const, 3, 3};
-        for (int s = 0; s < 7; s++) {
-            if (dalloc(&S.sec[SEC_CM1_2NS + s], (uint64_t)(widths_e[s] ? widths_e[s] : 1) * NE)) return -1;
-            S.ld[SEC_CM1_2NS + s] = NE;
-            S.ncols[SEC_CM1_2NS + s] = widths_e[s];
-        }
-        uint64_t tn = zkgpu_gl_merkle_num_elements(NE);
-        for (int t = 0; t < 4; t++)
-            if (dalloc(&nodes[t], tn)) return -1;
-        if (dalloc(&const_nodes, tn) || dalloc(&qq1, 3 * NE) || dalloc(&qq2, (uint64_t)info.n_cm4 * NE) ||
+        return 0;
+    }
+
+    // stage-4/5 and FRI buffers of the whole extended domain
+    int alloc_fri()
+    {
+        if (dalloc(&qq1, 3 * NE) || dalloc(&qq2, (uint64_t)info.n_cm4 * NE) ||
             dalloc(&cm4_n, (uint64_t)(info.n_cm4 ? info.n_cm4 : 1) * N) || dalloc(&lev, 3 * N) ||
             dalloc(&lpev, 3 * N) || dalloc(&xdiv, 3 * NE) || dalloc(&xdivw, 3 * NE) || dalloc(&fri_pol[0], 3 * NE) ||
             dalloc(&fri_pol[1], 3 * NE))
@@ -265,6 +277,29 @@ public:
             if (dalloc(&fri_aux[si], len) || dalloc(&fri_nodes[si], zkgpu_gl_merkle_num_elements(1ULL << fri_steps[si])))
                 return -1;
         }
+        return 0;
+    }
+
+    virtual int alloc()
+    {
+        if (alloc_n() || alloc_fri()) return -1;
+        const zkgpu_stark_info *in = &info;
+        const uint32_t widths_e[7] = {in->n_cm1, in->n_cm2, in->n_cm3, in->n_cm4, in->n_const, 3, 3};
+        for (int s = 0; s < 7; s++) {
+            if (dalloc(&S.sec[SEC_CM1_2NS + s], (uint64_t)(widths_e[s] ? widths_e[s] : 1) * NE)) return -1;
+            S.ld[SEC_CM1_2NS + s] = NE;
+            S.ncols[SEC_CM1_2NS + s] = widths_e[s];
+        }
+        uint64_t tn = zkgpu_gl_merkle_num_elements(NE);
+        for (int t = 0; t < 4; t++)
+            if (dalloc(&nodes[t], tn)) return -1;
+        if (dalloc(&const_nodes, tn)) return -1;
+        return 0;
+    }
+
+    int build_const()
+    {
+        const zkgpu_stark_info *in = &info;
         // constants (setup): pseudo-random columns, L_first = [1, 0, ...], then step0
         CK(zkgpu_memset_dev(S.sec[SEC_CONST_N], 0, (uint64_t)in->n_const * N * 8));
         if (!random_const.empty())
@@ -276,9 +311,7 @@ public:
             uint64_t ch0[24] = {0}, ev0[3] = {0, 0, 0};
             if (run(step0, false, ch0, ev0, 0)) return -1;
         }
-        CK(zkgpu_gl_extend_pol_dev(S.sec[SEC_CONST_2NS], NE, S.sec[SEC_CONST_N], N, NE, N, in->n_const));
-        CK(zkgpu_gl_merkletree_dev(const_nodes, S.sec[SEC_CONST_2NS], NE, in->n_const, NE));
-        CK(zkgpu_memcpy_d2h(verkey, const_nodes + tn - 4, 32));
+        if (commit_const()) return -1;
         publics.resize(in->n_publics);
         for (uint32_t k = 0; k < in->n_publics; k++) publics[k] = rand_u64(in->seed, 2, k, 0);
         return 0;
@@ -327,6 +360,12 @@ public:
         if (!rc) rc = zkgpu_synchronize();
         zkgpu_dev_free(tmp);
         if (rc) return fail("set_const: %s", zkgpu_last_error());
+        return commit_const();
+    }
+
+    // LDE of the constant polynomials, their tree, verkey = its root
+    virtual int commit_const()
+    {
         CK(zkgpu_gl_extend_pol_dev(S.sec[SEC_CONST_2NS], NE, S.sec[SEC_CONST_N], N, NE, N, info.n_const));
         CK(zkgpu_gl_merkletree_dev(const_nodes, S.sec[SEC_CONST_2NS], NE, info.n_const, NE));
         CK(zkgpu_memcpy_d2h(verkey, const_nodes + zkgpu_gl_merkle_num_elements(NE) - 4, 32));
@@ -376,7 +415,7 @@ public:
         return 0;
     }
 
-    int prove(uint64_t *out)
+    virtual int prove(uint64_t *out)
     {
         timers.clear();
         auto tall = clk::now();
@@ -397,20 +436,7 @@ public:
         if (tstop("STARK_STEP_2_CALCULATE_EXPS")) return -1;
         if (info.n_pu) {
             tstart();
-            for (uint32_t k = 0; k < info.n_pu; k++) {
-                const uint32_t *q = &pu[5 * k];
-                uint64_t miss = 0;
-                const int rc = zkgpu_h1h2_dev(S.sec[SEC_CM2_N] + (uint64_t)q[2] * N, N,
-                                              S.sec[SEC_CM2_N] + (uint64_t)q[3] * N, N,
-                                              S.sec[SEC_TMP_N] + (uint64_t)q[0] * N, N,
-                                              S.sec[SEC_TMP_N] + (uint64_t)q[1] * N, N, N, q[4], &miss);
-                if (rc) {
-                    if (miss != ~0ULL)
-                        return fail("Polinomial::calculateH1H2() Number not included: w=%llu plookup_number=%u",
-                                    (unsigned long long)miss, k);
-                    return fail("calculateH1H2: %s", zkgpu_last_error());
-                }
-            }
+            if (h1h2_all()) return -1;
             if (tstop("STARK_STEP_2_CALCULATEH1H2")) return -1;
         }
         if (commit(1, SEC_CM2_N, SEC_CM2_2NS, info.n_cm2, tr, roots[1], "STARK_STEP_2_LDE", "STARK_STEP_2_MERKLETREE"))
@@ -422,13 +448,7 @@ public:
         if (run(step3prev, false, ch, evals.data(), 0)) return -1;
         if (tstop("STARK_STEP_3_CALCULATE_EXPS")) return -1;
         tstart();
-        for (uint32_t z = 0; z < info.n_zctx; z++) {
-            int closes = 0;
-            CK(zkgpu_calculate_z_dev(S.sec[SEC_CM3_N] + (uint64_t)zctx[3 * z + 2] * N, N,
-                                     S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * z] * N, N,
-                                     S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * z + 1] * N, N, N, &closes));
-            if (!closes) return fail("calculateZ: grand product %u does not close", z);
-        }
+        if (z_all()) return -1;
         if (tstop("STARK_STEP_3_CALCULATE_Z")) return -1;
         // step3: post-Z expressions (starks.cpp:193-208)
         if (!step3.instr.empty()) {
@@ -444,18 +464,7 @@ public:
         if (run(step42ns, true, ch, evals.data(), 0)) return -1;
         if (tstop("STARK_STEP_4_CALCULATE_EXPS_2NS")) return -1;
         tstart();
-        CK(zkgpu_gl_ntt_dev(qq1, NE, S.sec[SEC_Q_2NS], NE, NE, 3, 1));
-        CK(zkgpu_memset_dev(qq2, 0, (uint64_t)info.n_cm4 * NE * 8));
-        uint64_t shift_in = pw(inv(7), N);
-        CK(zkgpu_qsplit_dev(qq2, NE, qq1, NE, N, info.q_deg, shift_in));
-        CK(zkgpu_gl_ntt_dev(S.sec[SEC_CM4_2NS], NE, qq2, NE, NE, info.n_cm4, 0));
-        // the quotient pieces on the n-domain too (for evmap below): qq2 holds
-        // coset-scaled coefficients c_k 7^k (k < N, the rest zero); plain
-        // coefficients c_k = qq2_k 7^-k, then NTT_N -> q_p(w_N^j)
-        for (uint32_t c = 0; c < info.n_cm4; c++)
-            CK(zkgpu_memcpy_d2d(cm4_n + (uint64_t)c * N, qq2 + (uint64_t)c * NE, N * 8));
-        CK(zkgpu_scale_by_powers_dev(cm4_n, N, info.n_cm4, N, inv(7)));
-        CK(zkgpu_gl_ntt_dev(cm4_n, N, cm4_n, N, N, info.n_cm4, 0));
+        if (quotient_pieces(S.sec[SEC_Q_2NS], S.sec[SEC_CM4_2NS])) return -1;
         if (tstop("STARK_STEP_4_CALCULATE_EXPS_2NS_INTT_NTT")) return -1;
         tstart();
         CK(zkgpu_gl_merkletree_dev(nodes[3], S.sec[SEC_CM4_2NS], NE, info.n_cm4, NE));
@@ -473,35 +482,10 @@ public:
         // polynomial of degree < N is the same, the field sums are exact, and
         // contiguous n-domain columns read half the lines of the strided
         // extension rows.
-        uint64_t wN = w_of(info.n_bits);
-        uint64_t xis[3], wxis[3];
-        for (int k = 0; k < 3; k++) {
-            xis[k] = xi[k] % P;
-            wxis[k] = mul(xi[k], wN);
-        }
-        CK(zkgpu_ext_powers_dev(lev, N, xis, N));
-        CK(zkgpu_ext_powers_dev(lpev, N, wxis, N));
-        CK(zkgpu_gl_ntt_dev(lev, N, lev, N, N, 3, 1));
-        CK(zkgpu_gl_ntt_dev(lpev, N, lpev, N, N, 3, 1));
+        if (lagrange_xi(xi)) return -1;
         if (tstop("STARK_STEP_5_LEv_LpEv")) return -1;
         tstart();
-        {
-            std::vector<const uint64_t *> cols(info.n_ev);
-            std::vector<uint64_t> lds(info.n_ev);
-            std::vector<uint32_t> dims(info.n_ev), primes(info.n_ev);
-            for (uint32_t e = 0; e < info.n_ev; e++) {
-                const uint32_t sec = ev[4 * e];
-                const uint64_t *base = sec == SEC_CM4_2NS ? cm4_n
-                                       : sec == SEC_CONST_2NS ? S.sec[SEC_CONST_N]
-                                                              : S.sec[sec - SEC_CM1_2NS + SEC_CM1_N];
-                cols[e] = base + (uint64_t)ev[4 * e + 1] * N;
-                lds[e] = N;
-                dims[e] = ev[4 * e + 2];
-                primes[e] = ev[4 * e + 3];
-            }
-            CK(zkgpu_evmap_dev(evals.data(), cols.data(), lds.data(), dims.data(), primes.data(), info.n_ev, lev, lpev,
-                               N, N, 0));
-        }
+        if (evmap_rows(0, N, evals.data())) return -1;
         if (tstop("STARK_STEP_5_EVMAP")) return -1;
         tr.put(evals.data(), evals.size());
         tr.get_field(ch + 15);
@@ -513,10 +497,108 @@ public:
         if (run(step52ns, true, ch, evals.data(), info.n_ev)) return -1;
         CK(zkgpu_cols3_to_interleaved_dev(fri_pol[0], S.sec[SEC_F_2NS], NE, NE));
         if (tstop("STARK_STEP_5_CALCULATE_EXPS")) return -1;
-        // FRI (friProve.cpp:5-190)
+        return fri_and_queries(tr, &roots[0][0], evals, out, tall);
+    }
+
+    // calculateH1H2 of every plookup (starks.cpp:104-127), n domain
+    int h1h2_all()
+    {
+        for (uint32_t k = 0; k < info.n_pu; k++) {
+            const uint32_t *q = &pu[5 * k];
+            uint64_t miss = 0;
+            const int rc = zkgpu_h1h2_dev(S.sec[SEC_CM2_N] + (uint64_t)q[2] * N, N,
+                                          S.sec[SEC_CM2_N] + (uint64_t)q[3] * N, N,
+                                          S.sec[SEC_TMP_N] + (uint64_t)q[0] * N, N,
+                                          S.sec[SEC_TMP_N] + (uint64_t)q[1] * N, N, N, q[4], &miss);
+            if (rc) {
+                if (miss != ~0ULL)
+                    return fail("Polinomial::calculateH1H2() Number not included: w=%llu plookup_number=%u",
+                                (unsigned long long)miss, k);
+                return fail("calculateH1H2: %s", zkgpu_last_error());
+            }
+        }
+        return 0;
+    }
+
+    // calculateZ of every grand product (starks.cpp:165-189), n domain
+    int z_all()
+    {
+        for (uint32_t z = 0; z < info.n_zctx; z++) {
+            int closes = 0;
+            CK(zkgpu_calculate_z_dev(S.sec[SEC_CM3_N] + (uint64_t)zctx[3 * z + 2] * N, N,
+                                     S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * z] * N, N,
+                                     S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * z + 1] * N, N, N, &closes));
+            if (!closes) return fail("calculateZ: grand product %u does not close", z);
+        }
+        return 0;
+    }
+
+    // LEv / LpEv: the n-domain Lagrange weights of xi and w xi (see prove)
+    int lagrange_xi(const uint64_t xi[3])
+    {
+        uint64_t wN = w_of(info.n_bits);
+        uint64_t xis[3], wxis[3];
+        for (int k = 0; k < 3; k++) {
+            xis[k] = xi[k] % P;
+            wxis[k] = mul(xi[k], wN);
+        }
+        CK(zkgpu_ext_powers_dev(lev, N, xis, N));
+        CK(zkgpu_ext_powers_dev(lpev, N, wxis, N));
+        CK(zkgpu_gl_ntt_dev(lev, N, lev, N, N, 3, 1));
+        CK(zkgpu_gl_ntt_dev(lpev, N, lpev, N, N, 3, 1));
+        return 0;
+    }
+
+    // starks.cpp:255-296: q (NE x 3, column-major, ld NE) -> INTT -> split
+    // into q_deg pieces -> NTT on the coset -> cm4 (n_cm4 x NE); the pieces
+    // on the n domain too (cm4_n, for evmap)
+    int quotient_pieces(const uint64_t *q, uint64_t *cm4)
+    {
+        CK(zkgpu_gl_ntt_dev(qq1, NE, q, NE, NE, 3, 1));
+        CK(zkgpu_memset_dev(qq2, 0, (uint64_t)info.n_cm4 * NE * 8));
+        uint64_t shift_in = pw(inv(7), N);
+        CK(zkgpu_qsplit_dev(qq2, NE, qq1, NE, N, info.q_deg, shift_in));
+        CK(zkgpu_gl_ntt_dev(cm4, NE, qq2, NE, NE, info.n_cm4, 0));
+        // the quotient pieces on the n-domain too (for evmap below): qq2 holds
+        // coset-scaled coefficients c_k 7^k (k < N, the rest zero); plain
+        // coefficients c_k = qq2_k 7^-k, then NTT_N -> q_p(w_N^j)
+        for (uint32_t c = 0; c < info.n_cm4; c++)
+            CK(zkgpu_memcpy_d2d(cm4_n + (uint64_t)c * N, qq2 + (uint64_t)c * NE, N * 8));
+        CK(zkgpu_scale_by_powers_dev(cm4_n, N, info.n_cm4, N, inv(7)));
+        CK(zkgpu_gl_ntt_dev(cm4_n, N, cm4_n, N, N, info.n_cm4, 0));
+        return 0;
+    }
+
+    // Starks::evmap over n-domain rows [k0, k0 + nrows) (starks.cpp:556-669;
+    // the row sum is linear, so row blocks give partial sums)
+    int evmap_rows(uint64_t k0, uint64_t nrows, uint64_t *evals_out)
+    {
+        std::vector<const uint64_t *> cols(info.n_ev);
+        std::vector<uint64_t> lds(info.n_ev);
+        std::vector<uint32_t> dims(info.n_ev), primes(info.n_ev);
+        for (uint32_t e = 0; e < info.n_ev; e++) {
+            const uint32_t sec = ev[4 * e];
+            const uint64_t *base = sec == SEC_CM4_2NS ? cm4_n
+                                   : sec == SEC_CONST_2NS ? S.sec[SEC_CONST_N]
+                                                          : S.sec[sec - SEC_CM1_2NS + SEC_CM1_N];
+            cols[e] = base + (uint64_t)ev[4 * e + 1] * N + k0;
+            lds[e] = N;
+            dims[e] = ev[4 * e + 2];
+            primes[e] = ev[4 * e + 3];
+        }
+        CK(zkgpu_evmap_dev(evals_out, cols.data(), lds.data(), dims.data(), primes.data(), info.n_ev, lev + k0,
+                           lpev + k0, N, nrows, 0));
+        return 0;
+    }
+
+    // FRIProve::prove + queries (friProve.cpp:5-232) once fri_pol[0] holds the
+    // FRI polynomial; s0 openings through open_s0
+    int fri_and_queries(Transcript &tr, const uint64_t *roots, const std::vector<uint64_t> &evals, uint64_t *out,
+                        clk::time_point tall)
+    {
         tstart();
         uint64_t *w = out;
-        memcpy(w, roots, sizeof roots);
+        memcpy(w, roots, 16 * 8);
         w += 16;
         memcpy(w, evals.data(), evals.size() * 8);
         w += evals.size();
@@ -555,7 +637,6 @@ public:
         tr.get_permutations(ys.data(), q(), fri_steps[0]);
         // FRI layers si >= 1: root, vals, siblings
         std::vector<uint64_t> yq = ys;
-        std::vector<std::vector<uint64_t>> fri_open(fri_steps.size());
         for (size_t si = 0; si < fri_steps.size(); si++) {
             if (si > 0) {
                 uint64_t ngroups = 1ULL << fri_steps[si];
@@ -573,7 +654,19 @@ public:
             if (si < fri_steps.size() - 1)
                 for (auto &y : yq) y %= (1ULL << fri_steps[si + 1]);
         }
-        // s0: the 4 stage trees + the constant tree at the original indices
+        if (open_s0(ys, w)) return -1;
+        memcpy(w, final_pol.data(), final_pol.size() * 8);
+        w += final_pol.size();
+        if (tstop("STARK_STEP_FRI_QUERIES")) return -1;
+        if (tr.err) return fail("transcript hashing failed: %s", zkgpu_last_error());
+        if ((uint64_t)(w - out) != proof_len()) return fail("proof length mismatch");
+        timers.emplace_back("STARK_TOTAL", std::chrono::duration<double, std::milli>(clk::now() - tall).count());
+        return 0;
+    }
+
+    // s0: the 4 stage trees + the constant tree at the original indices
+    virtual int open_s0(const std::vector<uint64_t> &ys, uint64_t *&w)
+    {
         const uint32_t secs[5] = {SEC_CM1_2NS, SEC_CM2_2NS, SEC_CM3_2NS, SEC_CM4_2NS, SEC_CONST_2NS};
         const uint32_t widths[5] = {info.n_cm1, info.n_cm2, info.n_cm3, info.n_cm4, info.n_const};
         uint64_t *trees[5] = {nodes[0], nodes[1], nodes[2], nodes[3], const_nodes};
@@ -590,18 +683,17 @@ public:
             memcpy(w, sib_all[t].data(), sib_all[t].size() * 8);
             w += sib_all[t].size();
         }
-        memcpy(w, final_pol.data(), final_pol.size() * 8);
-        w += final_pol.size();
-        if (tstop("STARK_STEP_FRI_QUERIES")) return -1;
-        if (tr.err) return fail("transcript hashing failed: %s", zkgpu_last_error());
-        if ((uint64_t)(w - out) != proof_len()) return fail("proof length mismatch");
-        timers.emplace_back("STARK_TOTAL", std::chrono::duration<double, std::milli>(clk::now() - tall).count());
         return 0;
     }
 };
 
+#include "sharded_starks.hpp"
+
 }  // namespace zkgpu_host
 
+#include "comm_rccl.hpp"
+
+using zkgpu_host::ShardedStarks;
 using zkgpu_host::Starks;
 
 extern "C" {
@@ -655,5 +747,61 @@ int zkgpu_stark_timers(void *h, char *names_buf, uint64_t names_len, double *ms,
     return (int)n;
 }
 void zkgpu_stark_destroy(void *h) { delete (Starks *)h; }
+
+int zkgpu_stark_create_sharded(void **handle, const zkgpu_stark_info *info, const zkgpu_comm *comm)
+{
+    *handle = nullptr;
+    if (!comm) return zkgpu_host::fail("stark_create_sharded: no communicator");
+    ShardedStarks *s = new ShardedStarks();
+    if (s->create_sharded(info, comm)) {
+        delete s;
+        return -1;
+    }
+    *handle = s;
+    return 0;
+}
+
+int zkgpu_comm_rccl_unique_id(uint8_t id[128])
+{
+    using zkgpu_host::g_rccl;
+    if (g_rccl.load()) return -1;
+    ncclUniqueId u;
+    ncclResult_t r = g_rccl.get_unique_id(&u);
+    if (r != ncclSuccess) return zkgpu_host::fail("ncclGetUniqueId: %s", g_rccl.error_string(r));
+    static_assert(sizeof u == 128, "ncclUniqueId size");
+    memcpy(id, &u, 128);
+    return 0;
+}
+
+int zkgpu_comm_rccl_create(zkgpu_comm *comm, const uint8_t id[128], uint32_t world, uint32_t rank)
+{
+    using zkgpu_host::g_rccl;
+    memset(comm, 0, sizeof *comm);
+    if (g_rccl.load()) return -1;
+    if (zkgpu_init(-1)) return zkgpu_host::fail("zkgpu_comm_rccl_create: %s", zkgpu_last_error());
+    ncclUniqueId u;
+    memcpy(&u, id, 128);
+    auto *ctx = new zkgpu_host::RcclCtx();
+    ncclResult_t r = g_rccl.comm_init_rank(&ctx->comm, (int)world, u, (int)rank);
+    if (r != ncclSuccess) {
+        delete ctx;
+        return zkgpu_host::fail("ncclCommInitRank(world %u, rank %u): %s", world, rank, g_rccl.error_string(r));
+    }
+    comm->rank = rank;
+    comm->world = world;
+    comm->ctx = ctx;
+    comm->exchange = zkgpu_host::rccl_exchange;
+    return 0;
+}
+
+void zkgpu_comm_rccl_destroy(zkgpu_comm *comm)
+{
+    if (!comm || !comm->ctx) return;
+    auto *ctx = (zkgpu_host::RcclCtx *)comm->ctx;
+    if (ctx->comm && zkgpu_host::g_rccl.comm_destroy) zkgpu_host::g_rccl.comm_destroy(ctx->comm);
+    delete ctx;
+    comm->ctx = nullptr;
+    comm->exchange = nullptr;
+}
 
 }  // extern "C"

@@ -39,6 +39,7 @@ _SIGS = {
     "zkgpu_last_error": (ctypes.c_char_p, []),
     "zkgpu_set_stream": (ctypes.c_int, [vp]),
     "zkgpu_synchronize": (ctypes.c_int, []),
+    "zkgpu_get_stream": (ctypes.c_void_p, []),
     "zkgpu_abi_version": (ctypes.c_int, []),
     "zkgpu_gl_ntt": (ctypes.c_int, [vp, vp, u64, u64, ctypes.c_int]),
     "zkgpu_gl_extend_pol": (ctypes.c_int, [vp, vp, u64, u64, u64]),

@@ -37,6 +37,21 @@ class _Info(ctypes.Structure):
                 ("n_pu", ctypes.c_uint32), ("pu", ctypes.c_void_p), ("step3", _Prog)]
 
 
+class CommOp(ctypes.Structure):
+    """zkgpu_comm_op (include/zkgpu_stark.h)"""
+    _fields_ = [("peer", ctypes.c_int32), ("send", ctypes.c_int32), ("buf", ctypes.c_void_p),
+                ("bytes", ctypes.c_uint64)]
+
+
+EXCHANGE = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(CommOp), ctypes.c_uint32)
+
+
+class Comm(ctypes.Structure):
+    """zkgpu_comm (include/zkgpu_stark.h)"""
+    _fields_ = [("rank", ctypes.c_uint32), ("world", ctypes.c_uint32), ("ctx", ctypes.c_void_p),
+                ("exchange", EXCHANGE)]
+
+
 _slib = None
 
 
@@ -59,6 +74,11 @@ def slib():
             ("zkgpu_stark_timers", ctypes.c_int, [vp, ctypes.c_char_p, u64, vp, ctypes.c_uint32]),
             ("zkgpu_stark_destroy", None, [vp]),
             ("zkgpu_stark_last_error", ctypes.c_char_p, []),
+            ("zkgpu_stark_create_sharded", ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(_Info),
+                                                          ctypes.POINTER(Comm)]),
+            ("zkgpu_comm_rccl_unique_id", ctypes.c_int, [vp]),
+            ("zkgpu_comm_rccl_create", ctypes.c_int, [ctypes.POINTER(Comm), vp, ctypes.c_uint32, ctypes.c_uint32]),
+            ("zkgpu_comm_rccl_destroy", None, [ctypes.POINTER(Comm)]),
         ]:
             f = getattr(L, name)
             f.restype = res
@@ -72,8 +92,81 @@ def _check(rc, what):
         raise ZkgpuError("%s failed: %s" % (what, slib().zkgpu_stark_last_error().decode(errors="replace")))
 
 
+class RcclComm:
+    """zkgpu_comm over RCCL (host/comm_rccl.hpp): rank 0 makes the id, the
+    process group (any backend) carries it to the others."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        uid = np.zeros(128, np.uint8)
+        if rank == 0:
+            _check(slib().zkgpu_comm_rccl_unique_id(uid.ctypes.data), "zkgpu_comm_rccl_unique_id")
+        if world > 1:
+            t = torch.from_numpy(uid.view(np.int64).copy())
+            dev = t.cuda() if dist.get_backend(group) == "nccl" else t
+            dist.broadcast(dev, 0, group=group)
+            uid = dev.cpu().numpy().view(np.uint8).copy()
+        self.c = Comm()
+        _check(slib().zkgpu_comm_rccl_create(ctypes.byref(self.c), uid.ctypes.data, world, rank),
+               "zkgpu_comm_rccl_create")
+
+    def close(self):
+        slib().zkgpu_comm_rccl_destroy(ctypes.byref(self.c))
+
+
+class HostStagedComm:
+    """zkgpu_comm over a torch.distributed group staged through host memory
+    (gloo): lets two prover processes share one GPU in the tests, where RCCL
+    needs one GPU per rank.  Each exchange waits for the zkgpu stream, copies
+    the send slices to the host, matches the k-th send to a peer with the
+    peer's k-th receive (tag k) and copies the received bytes back."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.group = group
+        self.c = Comm(dist.get_rank(group), dist.get_world_size(group), None, EXCHANGE(self._exchange))
+
+    def _exchange(self, ctx, ops, n_ops):
+        try:
+            import torch
+            import torch.distributed as dist
+            zk = _zk_lib()
+            if zk.zkgpu_synchronize():
+                return -1
+            reqs, recvs, seq, keep = [], [], {}, []
+            for k in range(n_ops):
+                o = ops[k]
+                tag = seq.get((o.peer, o.send), 0)
+                seq[(o.peer, o.send)] = tag + 1
+                t = torch.empty(o.bytes, dtype=torch.uint8)
+                if o.send:
+                    if zk.zkgpu_memcpy_d2h(t.data_ptr(), o.buf, o.bytes):
+                        return -1
+                    reqs.append(dist.isend(t, o.peer, group=self.group, tag=tag))
+                else:
+                    reqs.append(dist.irecv(t, o.peer, group=self.group, tag=tag))
+                    recvs.append((o.buf, t))
+                keep.append(t)
+            for r in reqs:
+                r.wait()
+            for buf, t in recvs:
+                if zk.zkgpu_memcpy_h2d(buf, t.data_ptr(), t.numel()):
+                    return -1
+            return 0
+        except Exception:  # an exception must not cross the C frame
+            import traceback
+            traceback.print_exc()
+            return -1
+
+    def close(self):
+        pass
+
+
 class GpuStark:
-    def __init__(self, inst):
+    def __init__(self, inst, comm=None):
         self.inst = inst
         self._keep = []
         info = _Info()
@@ -106,7 +199,12 @@ class GpuStark:
                                       max(prog.n_tmp1, 1), max(prog.n_tmp3, 1)))
         self._info = info
         self.h = ctypes.c_void_p()
-        _check(slib().zkgpu_stark_create(ctypes.byref(self.h), ctypes.byref(info)), "zkgpu_stark_create")
+        self.comm = comm
+        if comm is None:
+            _check(slib().zkgpu_stark_create(ctypes.byref(self.h), ctypes.byref(info)), "zkgpu_stark_create")
+        else:  # row-sharded over comm's ranks (host/sharded_starks.hpp)
+            _check(slib().zkgpu_stark_create_sharded(ctypes.byref(self.h), ctypes.byref(info), ctypes.byref(comm.c)),
+                   "zkgpu_stark_create_sharded")
 
     def witness(self):
         _check(slib().zkgpu_stark_witness(self.h), "zkgpu_stark_witness")
