@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-lde", action="store_true", help="skip the secondary LDE measurement (stark workload)")
     ap.add_argument("--lde-steps", type=int, default=10)
+    ap.add_argument("--sharded-impl", choices=["cpp", "py"], default="cpp",
+                    help="stark-sharded: the C++ prover over RCCL (default) or the Python orchestration")
     ap.add_argument("--workload", choices=["stark", "lde", "merkle", "commit", "stark-sharded", "step42ns"],
                     default="stark",
                     help="stark = configs[3] (headline: full synthetic STARK proof, 2^23 trace); lde = configs[1] "
@@ -478,7 +480,7 @@ def main():
 
             def step():
                 gs.prove_raw()
-        elif args.workload == "stark-sharded":
+        elif args.workload == "stark-sharded" and args.sharded_impl == "py":
             from zkgpu.sharded_stark import ShardedStark
             inst = stark_instance(args.log_n, args.blowup_bits, C, args.queries)
             ss = ShardedStark(inst, device=dev)
@@ -486,6 +488,16 @@ def main():
 
             def step():
                 ss.prove()
+        elif args.workload == "stark-sharded":
+            # the C++ row-sharded prover (host/sharded_starks.hpp) over RCCL
+            from zkgpu.stark import GpuStark, RcclComm
+            inst = stark_instance(args.log_n, args.blowup_bits, C, args.queries)
+            comm = RcclComm()
+            gs = GpuStark(inst, comm=comm)
+            gs.witness()
+
+            def step():
+                gs.prove_raw()
         elif args.workload == "step42ns":
             step, s42 = step42ns_setup(args, dev, torch, g)
         else:  # merkle
@@ -536,8 +548,10 @@ def main():
         elif args.workload == "stark-sharded":
             workload = ("ONE config-4 STARK proof (2^%d trace, %d cm1 cols, %d queries) row-sharded over %d rank(s)"
                         % (args.log_n, C, args.queries, world))
-            parallelism = ("one proof, extended domain row-sharded x%d: RCCL all-to-all column->row blocks per "
-                           "commit, halo + q/f all-gathers" % world)
+            parallelism = ("one proof, extended domain row-sharded x%d (%s): RCCL exchange column->row blocks + "
+                           "halo rows per commit, q/f row gathers" % (world, "C++ prover, host/sharded_starks.hpp"
+                                                                     if args.sharded_impl == "cpp" else
+                                                                     "Python orchestration, zkgpu/sharded_stark.py"))
         elif args.workload == "lde":
             workload = ("LDE 2^%d -> 2^%d rows x %d cols per GPU (extendPol, starks.cpp:53), column-major in HBM"
                         % (args.log_n, args.log_n + args.blowup_bits, C))
