@@ -117,6 +117,13 @@ int zkgpu_comm_rccl_unique_id(uint8_t id[128]);
 int zkgpu_comm_rccl_create(zkgpu_comm *comm, const uint8_t id[128], uint32_t world, uint32_t rank);
 void zkgpu_comm_rccl_destroy(zkgpu_comm *comm);
 
+/* Host shared-memory implementation for ranks that cannot use RCCL (several
+ * processes sharing one GPU): POSIX shared memory `name` ("/..."), one
+ * outbox of `capacity` bytes per rank and exchange, process-shared barriers.
+ * Every rank calls create with the same name, world and capacity. */
+int zkgpu_comm_host_create(zkgpu_comm *comm, const char *name, uint32_t world, uint32_t rank, uint64_t capacity);
+void zkgpu_comm_host_destroy(zkgpu_comm *comm);
+
 /* A prover whose extended (2n) domain is row-sharded over comm->world ranks:
  * rank r holds rows [r 2n/W, (r+1) 2n/W) of every extended section (plus the
  * next block's first 2^blowup rows), its share of the commitments' LDE

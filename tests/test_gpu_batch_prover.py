@@ -6,6 +6,7 @@ loader and writers on the CPU)."""
 import json
 import os
 import subprocess
+import uuid
 
 import numpy as np
 import pytest
@@ -48,3 +49,40 @@ def test_batch_prover_rejects_wrong_const_tree(oracle, tmp_path):
     r = subprocess.run([DRIVER, cfg], capture_output=True, text=True, timeout=300)
     assert r.returncode == 1 and "zkevmConstantsTree" in r.stderr, r.stderr
     assert not os.path.exists(tmp_path / "out" / "batch_proof.zkin.json")
+
+
+def _sharded_run(cfg, world, comm):
+    procs = [subprocess.Popen([DRIVER, "--shard", "%d/%d" % (r, world), "--comm", comm, cfg], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(world)]
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=120))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for p, (_, err) in zip(procs, outs):
+        assert p.returncode == 0, err
+    return [err for _, err in outs]
+
+
+@pytest.mark.parametrize("world,comm", [(2, "host"), (4, "host"), (1, "rccl")])
+def test_batch_prover_sharded(oracle, tmp_path, world, comm):
+    """--shard r/W: W driver processes prove ONE proof row-sharded
+    (zkgpu_stark_create_sharded); rank 0's zkin equals the oracle's.  host =
+    shared-memory exchange (the W processes share the one GPU here); rccl at
+    world 1 exercises the id file and communicator set-up."""
+    import zkgpu.starkinfo as zs
+    from oracle.stark_prover import OracleStark
+    from zkgpu.synthetic import SyntheticStark
+    inst = SyntheticStark(n_bits=9, blowup_bits=1, t=4, m=2, n_lookups=1, n_queries=12)
+    o = OracleStark(inst)
+    o.witness()
+    proof = o.prove()
+    cfg = zs.write_inputs(str(tmp_path), inst, o.S[4], o.S[9], o.const_nodes, o.S[0], o.publics)
+    spec = "host:/zkgpu_t_%s" % uuid.uuid4().hex[:12] if comm == "host" else "rccl:%s" % (tmp_path / "rccl.id")
+    errs = _sharded_run(cfg, world, spec)
+    assert all("[%d/%d]" % (r, world) in e for r, e in enumerate(errs))
+    assert (tmp_path / "out" / "batch_proof.zkin.json").read_text() == zs.zkin_text(proof, o.publics, inst.n_cm2,
+                                                                                      inst.n_cm3)

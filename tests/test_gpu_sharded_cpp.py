@@ -79,7 +79,7 @@ def test_sharded_rejects_bad_world(zkgpu):
         GpuStark(_inst("lookups"), comm=Three())
 
 
-def _worker(rank, world, port, q, name):
+def _worker(rank, world, port, q, name, shm):
     import sys
     root_dir = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root_dir, os.path.join(root_dir, "zkevm-prover_amd"), os.path.join(root_dir, "tests")]
@@ -88,13 +88,15 @@ def _worker(rank, world, port, q, name):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import zkgpu
-        from zkgpu.stark import GpuStark, HostStagedComm
+        from zkgpu.stark import GpuStark, HostStagedComm, ShmComm
         zkgpu.init(0)
-        g = GpuStark(_inst(name), comm=HostStagedComm())
+        comm = ShmComm(shm, world, rank) if shm else HostStagedComm()
+        g = GpuStark(_inst(name), comm=comm)
         g.witness()
         proof = g.prove()
         q.put((rank, proof, g.timers(), None))
         g.close()
+        comm.close()
     except Exception:  # report instead of hanging the parent
         import traceback
         q.put((rank, None, None, traceback.format_exc()))
@@ -110,13 +112,18 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,name", [(2, "lookups"), (4, "lookups"), (2, "blowup4")])
-def test_sharded_multiprocess_equals_oracle(oracle_proofs, world, name):
+@pytest.mark.parametrize("world,name,comm", [(2, "lookups", "gloo"), (4, "lookups", "gloo"), (2, "blowup4", "gloo"),
+                                             (2, "lookups", "shm"), (4, "blowup4", "shm")])
+def test_sharded_multiprocess_equals_oracle(oracle_proofs, world, name, comm):
+    """gloo = HostStagedComm (Python, torch.distributed); shm = ShmComm
+    (host/comm_host.hpp, shared memory + process-shared barriers)"""
     import multiprocessing as mp
+    import uuid
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, name)) for r in range(world)]
+    shm = "/zkgpu_t_%s" % uuid.uuid4().hex[:12] if comm == "shm" else None
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, name, shm)) for r in range(world)]
     for p in procs:
         p.start()
     try:

@@ -22,7 +22,13 @@
 // step52ns), run as GPU programs (ProverInfo, host/stark_info.cpp); for the
 // zkEVM's parser bytecode, StepsGPU (host/zkgpu_steps.hpp) is the binding.
 //
-// Usage: zkgpu_batch_prover <config.json>
+// Usage: zkgpu_batch_prover [--shard RANK/WORLD --comm rccl:<id file>|host:</shm name> [--device D]] <config.json>
+//        (--shard: one rank of ONE proof row-sharded over WORLD processes,
+//        zkgpu_stark_create_sharded; every rank runs this command with the
+//        same config, rank 0 writes the outputs.  rccl: rank 0 writes the
+//        RCCL id to the file, the others wait for it; host: shared-memory
+//        exchange for ranks sharing a GPU.  --device defaults to RANK for
+//        rccl, 0 for host.)
 //        zkgpu_batch_prover --info <starkinfo.json>                 (derived prover description; no GPU)
 //        zkgpu_batch_prover --zkin <starkinfo.json> <flat proof> <publics.json> <outdir>
 //                                                                   (proof JSON of a flat proof; no GPU)
@@ -31,12 +37,16 @@
 #include <sys/stat.h>
 
 #include <chrono>
+#include <cstdio>
 #include <fstream>
+#include <memory>
+#include <thread>
 #include <sstream>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
+#include "../../include/zkgpu.h"
 #include "../../include/zkgpu_stark.h"
 #include "zkgpu_fri_proof.hpp"
 #include "zkgpu_json.hpp"
@@ -114,7 +124,33 @@ static void check_root(const char *what, const uint64_t got[4], const uint64_t w
             throw std::runtime_error(std::string(what) + ": constant root differs from the tree built from zkevmConstPols");
 }
 
-static int prove(const std::string &config_path)
+struct Shard {
+    uint32_t rank = 0, world = 1;
+    std::string comm;  // "" (single GPU), "rccl:<file>", "host:<name>"
+    int device = -1;
+};
+
+// the RCCL id through a file: rank 0 writes it (atomic rename), the others poll
+static void rccl_id_file(const std::string &path, uint32_t rank, uint8_t id[128])
+{
+    if (rank == 0) {
+        if (zkgpu_comm_rccl_unique_id(id)) throw std::runtime_error(std::string("rccl id: ") + zkgpu_stark_last_error());
+        const std::string tmp = path + ".tmp";
+        std::ofstream f(tmp, std::ios::binary);
+        f.write((const char *)id, 128);
+        f.close();
+        if (!f.good() || std::rename(tmp.c_str(), path.c_str())) throw std::runtime_error("cannot write " + path);
+        return;
+    }
+    for (int t = 0; t < 6000; t++) {
+        std::ifstream f(path, std::ios::binary);
+        if (f.good() && f.read((char *)id, 128) && f.gcount() == 128) return;
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+    throw std::runtime_error("no RCCL id in " + path + " after 60 s");
+}
+
+static int prove(const std::string &config_path, const Shard &sh)
 {
     const Value cfg = zkgpu::json::parse(read_text(config_path));
     auto key = [&](const char *k) { return cfg[k].string(); };
@@ -130,7 +166,41 @@ static int prove(const std::string &config_path)
     if (info.n_publics) publics = read_publics(key("zkgpuPublics"), info.n_publics);
 
     void *h = nullptr;
-    if (zkgpu_stark_create(&h, &info)) throw std::runtime_error(std::string("create: ") + zkgpu_stark_last_error());
+    zkgpu_comm comm{};
+    struct CommGuard {
+        zkgpu_comm *c;
+        bool host;
+        ~CommGuard()
+        {
+            if (host)
+                zkgpu_comm_host_destroy(c);
+            else
+                zkgpu_comm_rccl_destroy(c);
+        }
+    };
+    std::unique_ptr<CommGuard> comm_guard;
+    if (sh.comm.empty()) {
+        if (sh.device >= 0 && zkgpu_init(sh.device)) throw std::runtime_error(std::string("init: ") + zkgpu_last_error());
+        if (zkgpu_stark_create(&h, &info)) throw std::runtime_error(std::string("create: ") + zkgpu_stark_last_error());
+    } else {
+        const bool host = sh.comm.rfind("host:", 0) == 0;
+        const int dev = sh.device >= 0 ? sh.device : (host ? 0 : (int)sh.rank);
+        if (zkgpu_init(dev)) throw std::runtime_error(std::string("init: ") + zkgpu_last_error());
+        int rc;
+        if (host) {
+            rc = zkgpu_comm_host_create(&comm, sh.comm.c_str() + 5, sh.world, sh.rank, 1ULL << 30);
+        } else if (sh.comm.rfind("rccl:", 0) == 0) {
+            uint8_t id[128];
+            rccl_id_file(sh.comm.substr(5), sh.rank, id);
+            rc = zkgpu_comm_rccl_create(&comm, id, sh.world, sh.rank);
+        } else {
+            throw std::runtime_error("--comm must be rccl:<file> or host:</name>");
+        }
+        if (rc) throw std::runtime_error(std::string("comm: ") + zkgpu_stark_last_error());
+        comm_guard.reset(new CommGuard{&comm, host});
+        if (zkgpu_stark_create_sharded(&h, &info, &comm))
+            throw std::runtime_error(std::string("create: ") + zkgpu_stark_last_error());
+    }
     struct Guard {
         void *h;
         ~Guard() { zkgpu_stark_destroy(h); }
@@ -160,11 +230,11 @@ static int prove(const std::string &config_path)
     std::vector<uint64_t> flat(len);
     if (zkgpu_stark_prove(h, flat.data())) throw std::runtime_error(std::string("prove: ") + zkgpu_stark_last_error());
     const auto t2 = clk::now();
-    write_outputs(key("outputPath"), flat.data(), len, info, publics);
+    if (sh.rank == 0) write_outputs(key("outputPath"), flat.data(), len, info, publics);
     const auto t3 = clk::now();
     auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
-    fprintf(stderr, "zkgpu_batch_prover: load %.1f ms, STARK_PROOF_BATCH_PROOF %.1f ms, json %.1f ms\n", ms(t1 - t0),
-            ms(t2 - t1), ms(t3 - t2));
+    fprintf(stderr, "zkgpu_batch_prover[%u/%u]: load %.1f ms, STARK_PROOF_BATCH_PROOF %.1f ms, json %.1f ms\n", sh.rank,
+            sh.world, ms(t1 - t0), ms(t2 - t1), ms(t3 - t2));
     return 0;
 }
 
@@ -184,9 +254,30 @@ int main(int argc, char **argv)
             write_outputs(argv[5], flat.data(), len, pinfo.info(), read_publics(argv[4], si.nPublics));
             return 0;
         }
-        if (argc == 2 && argv[1][0] != '-') return prove(argv[1]);
+        Shard sh;
+        int a = 1;
+        while (a + 1 < argc && argv[a][0] == '-' && argv[a][1] == '-') {
+            const std::string opt = argv[a];
+            if (opt == "--shard") {
+                unsigned r = 0, w = 0;
+                if (sscanf(argv[a + 1], "%u/%u", &r, &w) != 2 || !w || r >= w)
+                    throw std::runtime_error("--shard takes RANK/WORLD");
+                sh.rank = r;
+                sh.world = w;
+            } else if (opt == "--comm") {
+                sh.comm = argv[a + 1];
+            } else if (opt == "--device") {
+                sh.device = atoi(argv[a + 1]);
+            } else {
+                break;
+            }
+            a += 2;
+        }
+        if (sh.world > 1 && sh.comm.empty())
+            throw std::runtime_error("--shard with WORLD > 1 needs --comm");
+        if (argc == a + 1 && argv[a][0] != '-') return prove(argv[a], sh);
         fprintf(stderr,
-                "usage: %s <config.json>\n"
+                "usage: %s [--shard RANK/WORLD --comm rccl:<file>|host:</name> [--device D]] <config.json>\n"
                 "       %s --info <starkinfo.json>\n"
                 "       %s --zkin <starkinfo.json> <flat proof> <publics.json> <outdir>\n",
                 argv[0], argv[0], argv[0]);

@@ -691,6 +691,7 @@ public:
 
 }  // namespace zkgpu_host
 
+#include "comm_host.hpp"
 #include "comm_rccl.hpp"
 
 using zkgpu_host::ShardedStarks;
@@ -792,6 +793,94 @@ int zkgpu_comm_rccl_create(zkgpu_comm *comm, const uint8_t id[128], uint32_t wor
     comm->ctx = ctx;
     comm->exchange = zkgpu_host::rccl_exchange;
     return 0;
+}
+
+int zkgpu_comm_host_create(zkgpu_comm *comm, const char *name, uint32_t world, uint32_t rank, uint64_t capacity)
+{
+    using zkgpu_host::HostCommCtx;
+    using zkgpu_host::HostCommHeader;
+    using zkgpu_host::fail;
+    memset(comm, 0, sizeof *comm);
+    if (!world || rank >= world || !name || name[0] != '/')
+        return fail("zkgpu_comm_host_create: need rank < world and a name starting with '/'");
+    auto *c = new HostCommCtx();
+    c->rank = rank;
+    c->world = world;
+    c->capacity = capacity;
+    c->size = HostCommCtx::header_bytes() + (uint64_t)world * c->box_bytes();
+    int fd = -1;
+    if (rank == 0) {
+        shm_unlink(name);
+        fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd >= 0 && ftruncate(fd, (off_t)c->size)) {
+            close(fd);
+            fd = -1;
+        }
+    } else {
+        // wait (up to 60 s) for rank 0 to create and size the segment
+        for (int t = 0; t < 6000 && fd < 0; t++) {
+            fd = shm_open(name, O_RDWR, 0600);
+            struct stat st;
+            if (fd >= 0 && (fstat(fd, &st) || (uint64_t)st.st_size < c->size)) {
+                close(fd);
+                fd = -1;
+            }
+            if (fd < 0) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+        }
+    }
+    if (fd < 0) {
+        delete c;
+        return fail("zkgpu_comm_host_create: shared memory %s not available", name);
+    }
+    void *m = mmap(nullptr, c->size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) {
+        delete c;
+        return fail("zkgpu_comm_host_create: mmap of %llu bytes failed", (unsigned long long)c->size);
+    }
+    c->base = (uint8_t *)m;
+    HostCommHeader *h = c->hdr();
+    if (rank == 0) {
+        pthread_barrierattr_t a;
+        pthread_barrierattr_init(&a);
+        pthread_barrierattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
+        pthread_barrier_init(&h->barrier, &a, world);
+        pthread_barrierattr_destroy(&a);
+        h->world = world;
+        h->capacity = capacity;
+        h->ready.store(1, std::memory_order_release);
+    } else {
+        int t = 0;
+        while (h->ready.load(std::memory_order_acquire) != 1 && t++ < 6000)
+            std::this_thread::sleep_for(std::chrono::milliseconds(10));
+        if (h->ready.load(std::memory_order_acquire) != 1 || h->world != world || h->capacity != capacity) {
+            munmap(m, c->size);
+            delete c;
+            return fail("zkgpu_comm_host_create: segment %s belongs to another world", name);
+        }
+    }
+    // every rank has mapped the segment: its name is no longer needed
+    if (c->wait()) {
+        munmap(m, c->size);
+        delete c;
+        return -1;
+    }
+    if (rank == 0) shm_unlink(name);
+    comm->rank = rank;
+    comm->world = world;
+    comm->ctx = c;
+    comm->exchange = zkgpu_host::host_exchange;
+    return 0;
+}
+
+void zkgpu_comm_host_destroy(zkgpu_comm *comm)
+{
+    if (!comm || !comm->ctx) return;
+    auto *c = (zkgpu_host::HostCommCtx *)comm->ctx;
+    munmap(c->base, c->size);
+    delete c;
+    comm->ctx = nullptr;
+    comm->exchange = nullptr;
 }
 
 void zkgpu_comm_rccl_destroy(zkgpu_comm *comm)

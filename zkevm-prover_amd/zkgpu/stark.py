@@ -79,6 +79,9 @@ def slib():
             ("zkgpu_comm_rccl_unique_id", ctypes.c_int, [vp]),
             ("zkgpu_comm_rccl_create", ctypes.c_int, [ctypes.POINTER(Comm), vp, ctypes.c_uint32, ctypes.c_uint32]),
             ("zkgpu_comm_rccl_destroy", None, [ctypes.POINTER(Comm)]),
+            ("zkgpu_comm_host_create", ctypes.c_int, [ctypes.POINTER(Comm), ctypes.c_char_p, ctypes.c_uint32,
+                                                      ctypes.c_uint32, u64]),
+            ("zkgpu_comm_host_destroy", None, [ctypes.POINTER(Comm)]),
         ]:
             f = getattr(L, name)
             f.restype = res
@@ -115,6 +118,20 @@ class RcclComm:
 
     def close(self):
         slib().zkgpu_comm_rccl_destroy(ctypes.byref(self.c))
+
+
+class ShmComm:
+    """zkgpu_comm through host shared memory (host/comm_host.hpp): the
+    processes of one machine, e.g. several ranks sharing one GPU; every rank
+    passes the same name ("/...") and capacity (bytes per rank and exchange)."""
+
+    def __init__(self, name, world, rank, capacity=1 << 30):
+        self.c = Comm()
+        _check(slib().zkgpu_comm_host_create(ctypes.byref(self.c), name.encode(), world, rank, capacity),
+               "zkgpu_comm_host_create")
+
+    def close(self):
+        slib().zkgpu_comm_host_destroy(ctypes.byref(self.c))
 
 
 class HostStagedComm:
