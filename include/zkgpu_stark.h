@@ -85,6 +85,20 @@ int zkgpu_stark_timers(void *handle, char *names_buf, uint64_t names_len, double
 void zkgpu_stark_destroy(void *handle);
 const char *zkgpu_stark_last_error(void);
 
+/* ---- the Fiat-Shamir transcript the prover runs on the host, as the
+ * reference's class Transcript (transcript.hpp:14-37, transcript.cpp:4-88):
+ * Poseidon-GL sponge, 8-element rate, 4-element capacity.  Host code only
+ * (no GPU, no zkgpu_init needed).  Inputs are any u64 (reduced mod p, as
+ * Goldilocks::Element); outputs are canonical. */
+typedef struct zkgpu_transcript zkgpu_transcript;
+zkgpu_transcript *zkgpu_transcript_create(void);                              /* Transcript() */
+int zkgpu_transcript_put(zkgpu_transcript *t, const uint64_t *in, uint64_t n); /* put, :4-29 */
+int zkgpu_transcript_get_fields1(zkgpu_transcript *t, uint64_t *out);         /* getFields1, :39-55 */
+int zkgpu_transcript_get_field(zkgpu_transcript *t, uint64_t out[3]);         /* getField, :31-37 */
+/* getPermutations, :57-88: n indices of nbits bits each (nbits <= 63) */
+int zkgpu_transcript_get_permutations(zkgpu_transcript *t, uint64_t *res, uint64_t n, uint64_t nbits);
+void zkgpu_transcript_destroy(zkgpu_transcript *t);
+
 /* ---- one proof sharded over the GPUs of a node (BASELINE
  * configs[4]: "the same BatchProof trace column-sharded across 8 x MI355X").
  * The reference proves on one host (Starks::genProof, starks.cpp:9-404); this

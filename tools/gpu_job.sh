@@ -74,6 +74,16 @@ for step in "$@"; do
         cd "$ROOTDIR"
         ok_or_stop $rc "rocprofv3 kernel-trace"
         ;;
+    trace1)
+        # per-dispatch kernel trace of one timed STARK proof (after one warmup proof)
+        cd /tmp
+        timeout -k 10 400 rocprofv3 --kernel-trace -d "$ROOTDIR/gpurun_out/trace1" -o run \
+            --output-format csv -- python3 "$ROOTDIR/bench.py" --workload stark --no-cpu --no-lde --steps 1 --warmup 1 \
+            > "$ROOTDIR/gpurun_out/trace1_bench.json" 2> "$ROOTDIR/gpurun_out/trace1.err"
+        rc=$?
+        cd "$ROOTDIR"
+        ok_or_stop $rc "rocprofv3 kernel-trace (one proof)"
+        ;;
     pmc)
         # LDE (configs[1]): HBM traffic per pass kernel, separate FETCH / WRITE / SQ passes
         for pass in "FETCH_SIZE:pmc_fetch" "WRITE_SIZE:pmc_write" "SQ_INSTS_VALU SQ_WAVES:pmc_sqb"; do

@@ -749,6 +749,39 @@ int zkgpu_stark_timers(void *h, char *names_buf, uint64_t names_len, double *ms,
 }
 void zkgpu_stark_destroy(void *h) { delete (Starks *)h; }
 
+// the prover's own Transcript class behind the reference's Transcript surface
+struct zkgpu_transcript {
+    zkgpu_host::Transcript t;
+};
+zkgpu_transcript *zkgpu_transcript_create(void) { return new zkgpu_transcript(); }
+void zkgpu_transcript_destroy(zkgpu_transcript *t) { delete t; }
+int zkgpu_transcript_put(zkgpu_transcript *t, const uint64_t *in, uint64_t n)
+{
+    if (!t || (n && !in)) return zkgpu_host::fail("transcript_put: null argument");
+    t->t.put(in, n);
+    return t->t.err ? zkgpu_host::fail("transcript_put: host permutation failed") : 0;
+}
+int zkgpu_transcript_get_fields1(zkgpu_transcript *t, uint64_t *out)
+{
+    if (!t || !out) return zkgpu_host::fail("transcript_get_fields1: null argument");
+    *out = t->t.get_fields1();
+    return t->t.err ? zkgpu_host::fail("transcript_get_fields1: host permutation failed") : 0;
+}
+int zkgpu_transcript_get_field(zkgpu_transcript *t, uint64_t out[3])
+{
+    if (!t || !out) return zkgpu_host::fail("transcript_get_field: null argument");
+    t->t.get_field(out);
+    return t->t.err ? zkgpu_host::fail("transcript_get_field: host permutation failed") : 0;
+}
+int zkgpu_transcript_get_permutations(zkgpu_transcript *t, uint64_t *res, uint64_t n, uint64_t nbits)
+{
+    if (!t || (n && !res)) return zkgpu_host::fail("transcript_get_permutations: null argument");
+    if (nbits == 0 || nbits > 63) return zkgpu_host::fail("transcript_get_permutations: nbits %lu not in [1, 63]", (unsigned long)nbits);
+    if (n == 0) return 0;
+    t->t.get_permutations(res, n, nbits);
+    return t->t.err ? zkgpu_host::fail("transcript_get_permutations: host permutation failed") : 0;
+}
+
 int zkgpu_stark_create_sharded(void **handle, const zkgpu_stark_info *info, const zkgpu_comm *comm)
 {
     *handle = nullptr;

@@ -82,6 +82,12 @@ def slib():
             ("zkgpu_comm_host_create", ctypes.c_int, [ctypes.POINTER(Comm), ctypes.c_char_p, ctypes.c_uint32,
                                                       ctypes.c_uint32, u64]),
             ("zkgpu_comm_host_destroy", None, [ctypes.POINTER(Comm)]),
+            ("zkgpu_transcript_create", vp, []),
+            ("zkgpu_transcript_destroy", None, [vp]),
+            ("zkgpu_transcript_put", ctypes.c_int, [vp, vp, u64]),
+            ("zkgpu_transcript_get_fields1", ctypes.c_int, [vp, vp]),
+            ("zkgpu_transcript_get_field", ctypes.c_int, [vp, vp]),
+            ("zkgpu_transcript_get_permutations", ctypes.c_int, [vp, vp, u64, u64]),
         ]:
             f = getattr(L, name)
             f.restype = res
@@ -93,6 +99,42 @@ def slib():
 def _check(rc, what):
     if rc != 0:
         raise ZkgpuError("%s failed: %s" % (what, slib().zkgpu_stark_last_error().decode(errors="replace")))
+
+
+class Transcript:
+    """The prover's host transcript (zkgpu_transcript_*, host/starks.cpp)
+    with the reference's Transcript surface (transcript.hpp:14-37): put,
+    get_field, get_fields1, get_permutations.  Host code, no GPU."""
+
+    def __init__(self):
+        self._t = slib().zkgpu_transcript_create()
+        if not self._t:
+            raise ZkgpuError("zkgpu_transcript_create failed")
+
+    def __del__(self):
+        if getattr(self, "_t", None) and _slib is not None:
+            _slib.zkgpu_transcript_destroy(self._t)
+            self._t = None
+
+    def put(self, v):
+        a = np.ascontiguousarray(np.asarray(v, dtype=np.uint64).ravel())
+        _check(slib().zkgpu_transcript_put(self._t, a.ctypes.data, a.size), "zkgpu_transcript_put")
+
+    def get_fields1(self):
+        o = np.zeros(1, np.uint64)
+        _check(slib().zkgpu_transcript_get_fields1(self._t, o.ctypes.data), "zkgpu_transcript_get_fields1")
+        return int(o[0])
+
+    def get_field(self):
+        o = np.zeros(3, np.uint64)
+        _check(slib().zkgpu_transcript_get_field(self._t, o.ctypes.data), "zkgpu_transcript_get_field")
+        return o
+
+    def get_permutations(self, n, nbits):
+        o = np.zeros(max(n, 1), np.uint64)
+        _check(slib().zkgpu_transcript_get_permutations(self._t, o.ctypes.data, n, nbits),
+               "zkgpu_transcript_get_permutations")
+        return o[:n]
 
 
 class RcclComm:
