@@ -280,9 +280,20 @@ def stark_valu(kernel, avg_ms):
     frac = rate / peak
     if frac > 1.0:
         raise SystemExit("valu.frac %.3f > 1 for %s: the peak model (%s) is wrong" % (frac, kernel, note))
-    return {"kernel": kernel, "wave_instr_per_launch": k["valu_wave_instr_per_launch"], "avg_launch_ms": round(avg_ms, 4),
-            "achieved": round(rate / 1e9, 1), "peak": round(peak / 1e9, 1), "unit": "G wave-instr/s",
-            "frac": round(frac, 4), "peak_model": note, "source": os.path.basename(f)}
+    res = {"kernel": kernel, "wave_instr_per_launch": k["valu_wave_instr_per_launch"], "avg_launch_ms": round(avg_ms, 4),
+           "achieved": round(rate / 1e9, 1), "peak": round(peak / 1e9, 1), "unit": "G wave-instr/s",
+           "frac": round(frac, 4), "peak_model": note + " at the nominal %.1f GHz" % (CLOCK_HZ / 1e9),
+           "source": os.path.basename(f)}
+    # the clock the kernel actually runs at (power-limited below the nominal
+    # 2.4 GHz; GRBM busy cycles / duration, tools/pmc_clock.sh)
+    fc, clk = _newest("*_clock.json")
+    ghz = (clk or {}).get("labels", {}).get(kernel)
+    if ghz:
+        res["clock_GHz"] = ghz
+        res["peak_at_clock"] = round(peak * ghz * 1e9 / CLOCK_HZ / 1e9, 1)
+        res["frac_at_clock"] = round(frac * CLOCK_HZ / (ghz * 1e9), 4)
+        res["clock_source"] = os.path.basename(fc)
+    return res
 
 
 # ---------------------------------------------------------------- timing helpers
