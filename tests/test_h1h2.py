@@ -110,3 +110,51 @@ def test_gpu_h1h2_non_canonical_and_missing(oracle, zkgpu):
     f2[3000] = np.uint64(987654321)
     if not (t == f2[100]).any() and not (t == f2[3000]).any():
         assert zkgpu.h1h2_dev(h1, n, h2, n, zkgpu.to_device(f2), n, dt, n, n, 1) == 100
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sort_path", [False, True])
+def test_gpu_h1h2_dim3_shared_components(oracle, zkgpu, sort_path, monkeypatch):
+    """dim 3 keys that agree in one or two components (the table must compare
+    all three), non-canonical words in components 1/2, at 2^20 rows; both the
+    hash path (default) and the sort path (ZKGPU_H1H2_SORT=1, read once per
+    process: run in a child) give the oracle's h1/h2."""
+    import subprocess
+    import sys
+    if sort_path:
+        code = ("import sys; sys.path[:0] = %r\n"
+                "import test_h1h2 as T\n"
+                "from oracle import oracle as oc\nimport zkgpu\noc.lib()\nzkgpu.init()\n"
+                "T._shared_components_case(oc, zkgpu)\n") % ([ROOT_DIR, ROOT_DIR + "/zkevm-prover_amd",
+                                                               ROOT_DIR + "/tests"],)
+        env = dict(__import__("os").environ, ZKGPU_H1H2_SORT="1")
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+    else:
+        _shared_components_case(oracle, zkgpu)
+
+
+ROOT_DIR = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+
+
+def _shared_components_case(oracle, zkgpu):
+    import torch
+    n = 1 << 20
+    rng = np.random.default_rng(20)
+    base = rng.integers(0, P, size=(64, 3), dtype=np.uint64)
+    vals = np.repeat(base, 16, axis=0)
+    vals[:, 1] = rng.integers(0, 4, size=len(vals)).astype(np.uint64)          # few distinct second components
+    vals[::2, 2] = vals[1::2, 2]                                               # pairs equal but for component 1
+    vals[::3, 0] = vals[0, 0]                                                  # many share component 0
+    t = vals[rng.integers(0, len(vals), size=n)]
+    small = t[:, 1] < np.uint64(2**32 - 1)
+    t[small, 1] += np.uint64(P)  # same element, non-canonical word
+    f = t[rng.integers(0, n, size=n)] % np.uint64(P)
+    r1, r2 = oracle.h1h2(f, t)
+    cols = (lambda a: np.ascontiguousarray(a.T))
+    df, dt = zkgpu.to_device(cols(f)), zkgpu.to_device(cols(t))
+    h1 = torch.zeros((3, n), dtype=torch.int64, device="cuda:0")
+    h2 = torch.zeros((3, n), dtype=torch.int64, device="cuda:0")
+    assert zkgpu.h1h2_dev(h1, n, h2, n, df, n, dt, n, n, 3) is None
+    assert np.array_equal(zkgpu.from_device(h1).T, r1)
+    assert np.array_equal(zkgpu.from_device(h2).T, r2)

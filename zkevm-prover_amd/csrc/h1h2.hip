@@ -18,6 +18,15 @@
 //   4. one thread per multiset slot s: j = upper_bound(start, s) - 1,
 //      h_{1 + (s & 1)}[s >> 1] = t[j]  (raw copy, like copyElement).
 // Columns are column-major: component c of a dim-3 column at ptr + c * ld.
+//
+// Default path (hash, h1h2_hash below): steps 1-2 as an open-addressing table
+// of table ROWS keyed by the canonical value (linear probing, 2^k >= 2N
+// slots of u32): insertion keeps the largest row per key (atomicMax: the
+// reference's "last row wins"), then every f row probes, and step 4 scatters
+// each table row's 1 + count copies from its start.  The sort path stays
+// selectable with ZKGPU_H1H2_SORT=1 (A/B); both are the same mapping.
+#include <stdlib.h>
+
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
@@ -143,9 +152,171 @@ __global__ void k_h12_deal(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t 
     for (int c = 0; c < DIM; c++) h[c * ld + (s >> 1)] = t[c * t_ld + j];
 }
 
+// ---------------------------------------------------------------- hash path
+constexpr uint32_t H12_EMPTY = 0xFFFFFFFFu;
+
+template <int DIM>
+__device__ __forceinline__ void h12_key(uint64_t key[DIM], const uint64_t *col, uint64_t ld, uint64_t r)
+{
+#pragma unroll
+    for (int c = 0; c < DIM; c++) key[c] = gl_canon(col[c * ld + r]);
+}
+
+template <int DIM>
+__device__ __forceinline__ uint64_t h12_hash(const uint64_t key[DIM])
+{
+    uint64_t h = 0x9E3779B97F4A7C15ULL;
+#pragma unroll
+    for (int c = 0; c < DIM; c++) {
+        uint64_t z = key[c] + h;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        h = z ^ (z >> 31);
+    }
+    return h;
+}
+
+template <int DIM>
+__device__ __forceinline__ bool h12_eq(const uint64_t *t, uint64_t t_ld, uint32_t row, const uint64_t key[DIM])
+{
+#pragma unroll
+    for (int c = 0; c < DIM; c++)
+        if (gl_canon(t[c * t_ld + row]) != key[c]) return false;
+    return true;
+}
+
+// table row i -> its key's slot holds the largest row with that key
+template <int DIM>
+__global__ void __launch_bounds__(256) k_h12_insert(uint32_t *slots, uint64_t mask, const uint64_t *t, uint64_t t_ld,
+                                                    uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t key[DIM];
+    h12_key<DIM>(key, t, t_ld, i);
+    uint64_t h = h12_hash<DIM>(key) & mask;
+    for (uint64_t probe = 0; probe <= mask; probe++, h = (h + 1) & mask) {
+        uint32_t cur = slots[h];
+        if (cur == H12_EMPTY) {
+            cur = atomicCAS(&slots[h], H12_EMPTY, (uint32_t)i);
+            if (cur == H12_EMPTY) return;
+        }
+        if (h12_eq<DIM>(t, t_ld, cur, key)) {
+            atomicMax(&slots[h], (uint32_t)i);
+            return;
+        }
+    }
+}
+
+// f row i -> ++cnt[last table row with f's key]; absent keys record the
+// smallest such row
+template <int DIM>
+__global__ void __launch_bounds__(256) k_h12_probe(const uint32_t *slots, uint64_t mask, const uint64_t *f,
+                                                   uint64_t f_ld, const uint64_t *t, uint64_t t_ld, uint64_t n,
+                                                   uint32_t *cnt, unsigned long long *miss)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t key[DIM];
+    h12_key<DIM>(key, f, f_ld, i);
+    uint64_t h = h12_hash<DIM>(key) & mask;
+    for (uint64_t probe = 0; probe <= mask; probe++, h = (h + 1) & mask) {
+        const uint32_t cur = slots[h];
+        if (cur == H12_EMPTY) break;
+        if (h12_eq<DIM>(t, t_ld, cur, key)) {
+            atomicAdd(&cnt[cur], 1u);
+            return;
+        }
+    }
+    atomicMin(miss, (unsigned long long)i);
+}
+
+// table row j: its 1 + count copies at multiset slots start[j] ..
+template <int DIM>
+__global__ void __launch_bounds__(256) k_h12_scatter(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld,
+                                                     const uint64_t *t, uint64_t t_ld, const uint32_t *start,
+                                                     const uint32_t *cnt, uint64_t n)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    uint64_t v[DIM];
+#pragma unroll
+    for (int c = 0; c < DIM; c++) v[c] = t[c * t_ld + j];  // raw copy (copyElement)
+    const uint64_t s0 = start[j], e = s0 + cnt[j];
+    for (uint64_t sl = s0; sl < e; sl++) {
+        uint64_t *h = (sl & 1) ? h2 : h1;
+        const uint64_t ld = (sl & 1) ? h2_ld : h1_ld;
+#pragma unroll
+        for (int c = 0; c < DIM; c++) h[c * ld + (sl >> 1)] = v[c];
+    }
+}
+
+static int h1h2_hash(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint64_t *f, uint64_t f_ld,
+                     const uint64_t *t, uint64_t t_ld, uint64_t n, uint32_t dim, uint64_t *missing_row, hipStream_t s)
+{
+    uint64_t m = 1;
+    while (m < 2 * n) m <<= 1;
+    const size_t need = m * 4 + 2 * n * 4 + 16;
+    char *w = (char *)workspace(4, need);
+    if (!w) return ZKGPU_ERR_OOM;
+    uint32_t *slots = (uint32_t *)w;
+    uint32_t *cnt = slots + m;
+    uint32_t *start = cnt + n;
+    unsigned long long *miss = (unsigned long long *)(((uintptr_t)(start + n) + 7) & ~(uintptr_t)7);
+    size_t scan_bytes = 0;
+    if (rocprim::exclusive_scan(nullptr, scan_bytes, cnt, start, 0u, (size_t)n, rocprim::plus<uint32_t>(), s) !=
+        hipSuccess)
+        return set_error(ZKGPU_ERR_HIP, "h1h2: rocprim temp-size query failed");
+    void *tmp = workspace(5, scan_bytes);
+    if (!tmp) return ZKGPU_ERR_OOM;
+    const uint32_t B = 256;
+    prof_begin(s);
+    if (check_hip(hipMemsetAsync(slots, 0xFF, m * 4, s), "h1h2 memset") ||
+        check_hip(hipMemsetAsync(miss, 0xFF, 8, s), "h1h2 memset"))
+        return ZKGPU_ERR_HIP;
+    hipLaunchKernelGGL(k_h12_fill1, dim3(nblk2(n, B)), dim3(B), 0, s, cnt, n);
+    if (dim == 1) {
+        hipLaunchKernelGGL(k_h12_insert<1>, dim3(nblk2(n, B)), dim3(B), 0, s, slots, m - 1, t, t_ld, n);
+        hipLaunchKernelGGL(k_h12_probe<1>, dim3(nblk2(n, B)), dim3(B), 0, s, slots, m - 1, f, f_ld, t, t_ld, n, cnt,
+                           miss);
+    } else {
+        hipLaunchKernelGGL(k_h12_insert<3>, dim3(nblk2(n, B)), dim3(B), 0, s, slots, m - 1, t, t_ld, n);
+        hipLaunchKernelGGL(k_h12_probe<3>, dim3(nblk2(n, B)), dim3(B), 0, s, slots, m - 1, f, f_ld, t, t_ld, n, cnt,
+                           miss);
+    }
+    {
+        size_t tb = scan_bytes;
+        if (rocprim::exclusive_scan(tmp, tb, cnt, start, 0u, (size_t)n, rocprim::plus<uint32_t>(), s) != hipSuccess)
+            return set_error(ZKGPU_ERR_HIP, "h1h2: scan failed");
+    }
+    unsigned long long mh = 0;
+    if (check_hip(hipMemcpyAsync(&mh, miss, 8, hipMemcpyDeviceToHost, s), "D2H") ||
+        check_hip(hipStreamSynchronize(s), "h1h2 sync"))
+        return ZKGPU_ERR_HIP;
+    if (mh != ~0ULL) {
+        if (missing_row) *missing_row = mh;
+        return set_error(ZKGPU_ERR_ARG, "calculateH1H2: Number not included: w=%llu", mh);
+    }
+    if (missing_row) *missing_row = ~0ULL;
+    if (dim == 1)
+        hipLaunchKernelGGL(k_h12_scatter<1>, dim3(nblk2(n, B)), dim3(B), 0, s, h1, h1_ld, h2, h2_ld, t, t_ld, start, cnt,
+                           n);
+    else
+        hipLaunchKernelGGL(k_h12_scatter<3>, dim3(nblk2(n, B)), dim3(B), 0, s, h1, h1_ld, h2, h2_ld, t, t_ld, start, cnt,
+                           n);
+    prof_end("k_h1h2", (double)dim * 8.0 * 4.0 * n, s);
+    return check_launch("h1h2");
+}
+
 int h1h2(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint64_t *f, uint64_t f_ld,
          const uint64_t *t, uint64_t t_ld, uint64_t n, uint32_t dim, uint64_t *missing_row, hipStream_t s)
 {
+    static const bool use_sort = [] {
+        const char *e = getenv("ZKGPU_H1H2_SORT");
+        return e && atoi(e) != 0;
+    }();
+    if (!use_sort && n < 0xFFFFFFFFULL)
+        return h1h2_hash(h1, h1_ld, h2, h2_ld, f, f_ld, t, t_ld, n, dim, missing_row, s);
     // scratch: keys_in, keys_out (n u64 each), sk (dim n u64; sk[0] = keys_out
     // of the last pass), perm_in, perm_out, cnt (n u32 each), miss (u64)
     const size_t kb = n * sizeof(uint64_t), pb = n * sizeof(uint32_t);
