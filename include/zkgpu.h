@@ -219,6 +219,13 @@ int zkgpu_zxp_jit_source(const void *instr, uint32_t n_instr, const void *opnd, 
  * (the reference's zkassert). */
 int zkgpu_calculate_z_dev(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,
                           uint64_t den_ld, uint64_t n, int *closes);
+/* One row block of the same grand product (the row-sharded prover: each rank
+ * its block, then a scan of the W block totals): z[i] = z0 * prod_{j<i}
+ * num[j] / den[j] for i < n; total (host, canonical) = z0 * prod_{j<n}
+ * num[j] / den[j].  calculateZ over the whole domain is z0 = 1, closes iff
+ * total == 1. */
+int zkgpu_calculate_z_block_dev(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,
+                                uint64_t den_ld, uint64_t n, const uint64_t z0[3], uint64_t total[3]);
 
 /* Starks::evmap (starks.cpp:556-669): evals[e] = sum_{k<n} L(k) * pol_e[k << extend_bits],
  * L = lev or lpev (device, 3 columns of ld l_ld).  cols = host array of device

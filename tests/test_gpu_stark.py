@@ -136,6 +136,35 @@ def test_calculate_z_dev(oracle, zkgpu):
     assert not zkgpu.calculate_z_dev(dz, n, dnum, n, dden2, n, n)
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_calculate_z_block_dev(oracle, zkgpu, world):
+    """The row-sharded grand product (host/sharded_starks.hpp z_all): W
+    blocks with z0 = 1, the scan of their totals, the blocks redone with
+    z0 = prefix -> the whole-domain z, and the product of the totals closes."""
+    import torch
+    rng = np.random.default_rng(4 + world)
+    n = (1 << 14) + 0
+    num = rand_gl(rng, (n, 3))
+    den = np.roll(num, -1, axis=0)
+    zref = np.zeros((n, 3), np.uint64)
+    assert oracle.lib().oc_calculate_z(oracle._p(zref), 3, oracle._p(num), 3, oracle._p(np.ascontiguousarray(den)),
+                                       3, n)
+    dnum = zkgpu.to_device(np.ascontiguousarray(num.T))
+    dden = zkgpu.to_device(np.ascontiguousarray(den.T))
+    dz = torch.zeros((3, n), dtype=torch.int64, device="cuda:0")
+    nb = n // world
+    tots = []
+    for r in range(world):
+        tots.append(zkgpu.calculate_z_block_dev(dz[:, r * nb:], n, dnum[:, r * nb:], n, dden[:, r * nb:], n, nb))
+    pre = [1, 0, 0]
+    for r in range(world):
+        if r:
+            zkgpu.calculate_z_block_dev(dz[:, r * nb:], n, dnum[:, r * nb:], n, dden[:, r * nb:], n, nb, pre)
+        pre = [int(v) for v in oracle.gl3_mul(np.array(pre, np.uint64), tots[r])]
+    assert pre == [1, 0, 0]
+    assert np.array_equal(zkgpu.from_device(dz).T, zref)
+
+
 def test_xdivxsub_dev(oracle, zkgpu):
     import torch
     rng = np.random.default_rng(4)

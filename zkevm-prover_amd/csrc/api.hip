@@ -1066,21 +1066,34 @@ int zkgpu_zxp_eval_block_dev(const void *instr, uint32_t n_instr, const void *op
                          publics, n_publics, evals, n_evals, xdiv, xdivw, extend_bits, x_start);
 }
 
-int zkgpu_calculate_z_dev(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,
-                          uint64_t den_ld, uint64_t n, int *closes)
+int zkgpu_calculate_z_block_dev(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,
+                                uint64_t den_ld, uint64_t n, const uint64_t z0[3], uint64_t total[3])
 {
     int rc;
     if ((rc = require_init())) return rc;
-    if (!n) return 0;
+    if (!z0 || !total) return set_error(ZKGPU_ERR_ARG, "calculate_z_block: null z0 / total");
+    if (!n) {
+        for (int k = 0; k < 3; k++) total[k] = z0[k] % HP;
+        return 0;
+    }
     const size_t words = calculate_z_scratch_words(n);
     uint64_t *scr = workspace(2, (words + 8) * sizeof(uint64_t));
     if (!scr) return ZKGPU_ERR_OOM;
-    uint32_t *ok = (uint32_t *)(scr + words);
-    if ((rc = calculate_z(z, z_ld, num, num_ld, den, den_ld, n, scr, ok, g_ctx.stream))) return rc;
-    uint32_t okh = 0;
-    if ((rc = check_hip(hipMemcpyAsync(&okh, ok, 4, hipMemcpyDeviceToHost, g_ctx.stream), "D2H"))) return rc;
-    if ((rc = check_hip(hipStreamSynchronize(g_ctx.stream), "calculateZ sync"))) return rc;
-    if (closes) *closes = (int)okh;
+    uint64_t *tot = scr + words;
+    if ((rc = calculate_z(z, z_ld, num, num_ld, den, den_ld, n, z0, scr, tot, g_ctx.stream))) return rc;
+    if ((rc = check_hip(hipMemcpyAsync(total, tot, 24, hipMemcpyDeviceToHost, g_ctx.stream), "D2H"))) return rc;
+    return check_hip(hipStreamSynchronize(g_ctx.stream), "calculateZ sync");
+}
+
+int zkgpu_calculate_z_dev(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,
+                          uint64_t den_ld, uint64_t n, int *closes)
+{
+    const uint64_t one[3] = {1, 0, 0};
+    uint64_t tot[3] = {1, 0, 0};
+    const int rc = zkgpu_calculate_z_block_dev(z, z_ld, num, num_ld, den, den_ld, n, one, tot);
+    if (rc) return rc;
+    // z[n-1] * num[n-1] / den[n-1] == 1: the product of every ratio
+    if (closes) *closes = (tot[0] == 1 && tot[1] == 0 && tot[2] == 0) ? 1 : 0;
     return 0;
 }
 

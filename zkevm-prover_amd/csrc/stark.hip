@@ -349,10 +349,11 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_z_ratio(uint64_t *ratio, uint6
     }
 }
 
-// exclusive prefix of the tile totals: each thread multiplies a contiguous run
-// of ceil(ntiles / 256) totals, one block scan, then the run is re-walked
+// exclusive prefix of the tile totals times z0: each thread multiplies a
+// contiguous run of ceil(ntiles / 256) totals, one block scan, then the run is
+// re-walked; *total = z0 * prod of all ratios (the closing value)
 __global__ void __launch_bounds__(SCAN_THREADS) k_z_totals(uint64_t *tile_pre, const uint64_t *tile_tot,
-                                                           uint64_t ntiles)
+                                                           uint64_t ntiles, gl3 z0, uint64_t *total)
 {
     __shared__ gl3 sh[SCAN_THREADS];
     const uint64_t per = (ntiles + SCAN_THREADS - 1) / SCAN_THREADS;
@@ -362,12 +363,18 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_z_totals(uint64_t *tile_pre, c
     gl3 acc{{1, 0, 0}};
     for (uint64_t b = b0; b < b1; b++) acc = gl3_mul(acc, ld3(tile_tot + 3 * b, 1));
     gl3 tot;
-    gl3 run = block_exclusive_scan3(acc, sh, &tot);
+    gl3 run = gl3_mul(z0, block_exclusive_scan3(acc, sh, &tot));
     for (uint64_t b = b0; b < b1; b++) {
         tile_pre[3 * b] = run.v[0];
         tile_pre[3 * b + 1] = run.v[1];
         tile_pre[3 * b + 2] = run.v[2];
         run = gl3_mul(run, ld3(tile_tot + 3 * b, 1));
+    }
+    if (threadIdx.x == 0) {
+        const gl3 t = gl3_canon(gl3_mul(z0, tot));
+        total[0] = t.v[0];
+        total[1] = t.v[1];
+        total[2] = t.v[2];
     }
 }
 
@@ -400,15 +407,6 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_z_apply(uint64_t *z, uint64_t 
         const uint64_t k = base + e;
         if (k < n) st3(z + k, z_ld, lds_ld3(img, z_slot(e)));
     }
-}
-
-// check value: z[n-1] * ratio[n-1] must be 1 (calculateZ zkassert)
-__global__ void k_z_check(uint32_t *ok, const uint64_t *z, uint64_t z_ld, const uint64_t *ratio, uint64_t n)
-{
-    gl3 zl = ld3(z + (n - 1), z_ld);
-    gl3 r{{ratio[3 * (n - 1)], ratio[3 * (n - 1) + 1], ratio[3 * (n - 1) + 2]}};
-    gl3 c = gl3_canon(gl3_mul(zl, r));
-    *ok = (c.v[0] == 1 && c.v[1] == 0 && c.v[2] == 0) ? 1u : 0u;
 }
 
 // ---------------------------------------------------------------- evmap
@@ -646,11 +644,11 @@ int zxp_eval(const ZxpLaunch &L, hipStream_t s)
 size_t calculate_z_scratch_words(uint64_t n)
 {
     const uint64_t nt = (n + Z_TILE - 1) / Z_TILE;
-    return 3 * n + 3 * nt * SCAN_THREADS + 6 * nt;
+    return 3 * n + 3 * nt * SCAN_THREADS + 6 * nt + 4;
 }
 
 int calculate_z(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,
-                uint64_t den_ld, uint64_t n, uint64_t *scratch, uint32_t *ok_dev, hipStream_t s)
+                uint64_t den_ld, uint64_t n, const uint64_t z0[3], uint64_t *scratch, uint64_t *total_dev, hipStream_t s)
 {
     // scratch: ratio (3n) + per-thread prefixes (3 * 256 per tile) + tile totals + tile prefixes
     const uint64_t nt = (n + Z_TILE - 1) / Z_TILE;
@@ -662,11 +660,11 @@ int calculate_z(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld
     hipLaunchKernelGGL(k_z_ratio, dim3((uint32_t)nt), dim3(SCAN_THREADS), 0, s, ratio, thr, tot, num, num_ld, den,
                        den_ld, n);
     prof_end("k_z_ratio", 8.0 * 9 * n, s);
-    hipLaunchKernelGGL(k_z_totals, dim3(1), dim3(SCAN_THREADS), 0, s, pre, tot, nt);
+    const gl3 z0v{{z0[0], z0[1], z0[2]}};
+    hipLaunchKernelGGL(k_z_totals, dim3(1), dim3(SCAN_THREADS), 0, s, pre, tot, nt, z0v, total_dev);
     prof_begin(s);
     hipLaunchKernelGGL(k_z_apply, dim3((uint32_t)nt), dim3(SCAN_THREADS), 0, s, z, z_ld, ratio, thr, pre, n);
     prof_end("k_z_apply", 8.0 * 6 * n, s);
-    hipLaunchKernelGGL(k_z_check, dim3(1), dim3(1), 0, s, ok_dev, z, z_ld, ratio, n);
     return check_launch("calculateZ");
 }
 

@@ -167,7 +167,7 @@ int rand_cols(uint64_t *base, uint64_t ld, const uint32_t *cols_dev, uint32_t nc
 int zxp_eval(const ZxpLaunch &L, hipStream_t s);
 size_t calculate_z_scratch_words(uint64_t n);
 int calculate_z(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,
-                uint64_t den_ld, uint64_t n, uint64_t *scratch, uint32_t *ok_dev, hipStream_t s);
+                uint64_t den_ld, uint64_t n, const uint64_t z0[3], uint64_t *scratch, uint64_t *total_dev, hipStream_t s);
 size_t evmap_group_size();
 uint32_t evmap_group_width();
 uint64_t evmap_rows_per_block();

@@ -24,8 +24,10 @@
 //   FRI      folds and layer trees on every rank (2n x 3 elements).
 //   queries  each s0 opening by the rank owning its row (subtree siblings +
 //       top levels), all-gathered.
-// The n-domain stage work (step2 / H1H2 / step3prev / calculateZ / step3,
-// starks.cpp:67-211) runs on every rank over whole n-domain sections.  The
+// The n-domain sections are whole on every rank; calculateZ is row-sharded
+// (each rank its N/W-row block, a scan of the W block totals, the blocks
+// all-gathered); the other n-domain stage work (step2 / H1H2 / step3prev /
+// step3, starks.cpp:67-211) runs on every rank.  The
 // transcript runs on every rank on identical inputs; the proof is the
 // single-GPU proof bit for bit.
 //
@@ -233,6 +235,55 @@ public:
     {
         return commit_cols(trees[4], SEC_CONST_2NS, S.sec[SEC_CONST_N], info.n_const, verkey, nullptr, nullptr,
                            nullptr);
+    }
+
+    // F_p^3 product on the host (x^3 = x + 1)
+    static void mul3(uint64_t r[3], const uint64_t a[3], const uint64_t b[3])
+    {
+        const uint64_t c0 = mul(a[0], b[0]), c1 = (uint64_t)(((unsigned __int128)mul(a[0], b[1]) + mul(a[1], b[0])) % P);
+        const uint64_t c2 = (uint64_t)(((unsigned __int128)mul(a[0], b[2]) + mul(a[1], b[1]) + mul(a[2], b[0])) % P);
+        const uint64_t c3 = (uint64_t)(((unsigned __int128)mul(a[1], b[2]) + mul(a[2], b[1])) % P);
+        const uint64_t c4 = mul(a[2], b[2]);
+        // x^3 = x + 1, x^4 = x^2 + x
+        r[0] = (uint64_t)(((unsigned __int128)c0 + c3) % P);
+        r[1] = (uint64_t)(((unsigned __int128)c1 + c3 + c4) % P);
+        r[2] = (uint64_t)(((unsigned __int128)c2 + c4) % P);
+    }
+
+    // calculateZ (starks.cpp:146-224, polinomial.hpp:586-607) over the rank's
+    // N/W-row block: z = prod of the ratios before each row, the block total
+    // all-gathered, the block redone with z0 = the product of the earlier
+    // ranks' totals (rank 0's is already final), then the blocks all-gathered
+    // so every rank holds the whole column (the n-domain sections are whole)
+    int z_all() override
+    {
+        const uint64_t nb = N / W, r0 = (uint64_t)R * nb;
+        for (uint32_t zi = 0; zi < info.n_zctx; zi++) {
+            uint64_t *z = S.sec[SEC_CM3_N] + (uint64_t)zctx[3 * zi + 2] * N;
+            const uint64_t *num = S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * zi] * N;
+            const uint64_t *den = S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * zi + 1] * N;
+            const uint64_t one[3] = {1, 0, 0};
+            uint64_t tot[3];
+            CK(zkgpu_calculate_z_block_dev(z + r0, N, num + r0, N, den + r0, N, nb, one, tot));
+            std::vector<uint64_t> all;
+            if (allgather(tot, 3, all)) return -1;
+            uint64_t pre[3] = {1, 0, 0}, acc[3] = {1, 0, 0};
+            for (uint32_t s = 0; s < W; s++) {
+                if (s == R) memcpy(pre, acc, 24);
+                mul3(acc, acc, &all[3 * s]);
+            }
+            if (acc[0] != 1 || acc[1] || acc[2]) return fail("calculateZ: grand product %u does not close", zi);
+            if (pre[0] != 1 || pre[1] || pre[2])
+                CK(zkgpu_calculate_z_block_dev(z + r0, N, num + r0, N, den + r0, N, nb, pre, tot));
+            for (uint32_t d = 0; d < W; d++)
+                if (d != R)
+                    for (int c = 0; c < 3; c++) op(d, 1, z + (uint64_t)c * N + r0, nb * 8);
+            for (uint32_t s = 0; s < W; s++)
+                if (s != R)
+                    for (int c = 0; c < 3; c++) op(s, 0, z + (uint64_t)c * N + (uint64_t)s * nb, nb * 8);
+            if (exchange()) return -1;
+        }
+        return 0;
     }
 
     // an extended-domain program over the rank's rows

@@ -521,7 +521,7 @@ public:
     }
 
     // calculateZ of every grand product (starks.cpp:165-189), n domain
-    int z_all()
+    virtual int z_all()
     {
         for (uint32_t z = 0; z < info.n_zctx; z++) {
             int closes = 0;

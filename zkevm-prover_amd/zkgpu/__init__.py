@@ -78,6 +78,7 @@ _SIGS = {
     "zkgpu_zxp_jit_source": (ctypes.c_int, [vp, u32, vp, u32, u32, u32, vp, vp, u32, vp, u32, vp, u64,
                                             ctypes.c_int]),
     "zkgpu_calculate_z_dev": (ctypes.c_int, [vp, u64, vp, u64, vp, u64, u64, ctypes.POINTER(ctypes.c_int)]),
+    "zkgpu_calculate_z_block_dev": (ctypes.c_int, [vp, u64, vp, u64, vp, u64, u64, vp, vp]),
     "zkgpu_evmap_dev": (ctypes.c_int, [vp, vp, vp, vp, vp, u32, vp, vp, u64, u64, u32]),
     "zkgpu_xdivxsub_dev": (ctypes.c_int, [vp, vp, vp, u32, u32]),
     "zkgpu_ext_powers_dev": (ctypes.c_int, [vp, u64, vp, u64]),
@@ -321,6 +322,16 @@ def calculate_z_dev(z, z_ld, num, num_ld, den, den_ld, n):
                                        ctypes.byref(closes)), "zkgpu_calculate_z_dev")
     return bool(closes.value)
 
+
+
+def calculate_z_block_dev(z, z_ld, num, num_ld, den, den_ld, n, z0=(1, 0, 0)):
+    """One row block of calculateZ: z = z0 * running product; returns the
+    block's closing total z0 * prod(num / den) (3 canonical u64)."""
+    z0a = np.array([int(v) for v in z0], dtype=np.uint64)
+    tot = np.zeros(3, np.uint64)
+    _check(lib().zkgpu_calculate_z_block_dev(_addr(z), z_ld, _addr(num), num_ld, _addr(den), den_ld, n,
+                                             z0a.ctypes.data, tot.ctypes.data), "zkgpu_calculate_z_block_dev")
+    return tot
 
 def xdivxsub_dev(xdiv, xdivw, xi, n_bits, n_bits_ext):
     x = _np(xi)
