@@ -113,7 +113,7 @@ def _free_port():
 
 
 @pytest.mark.parametrize("world,name,comm", [(2, "lookups", "gloo"), (4, "lookups", "gloo"), (2, "blowup4", "gloo"),
-                                             (2, "lookups", "shm"), (4, "blowup4", "shm")])
+                                             (2, "lookups", "shm"), (4, "blowup4", "shm"), (8, "lookups", "shm")])
 def test_sharded_multiprocess_equals_oracle(oracle_proofs, world, name, comm):
     """gloo = HostStagedComm (Python, torch.distributed); shm = ShmComm
     (host/comm_host.hpp, shared memory + process-shared barriers)"""

@@ -21,7 +21,10 @@
 //       commits its rows of the pieces.
 //   stage 5  evmap on the rank's n-domain rows, partial sums all-gathered and
 //       added mod p; the FRI program on the rank's rows, f gathered.
-//   FRI      folds and layer trees on every rank (2n x 3 elements).
+//   FRI      folds on every rank (2n x 3 elements); a layer tree whose
+//       groups split into W blocks is row-sharded like the commits (each
+//       rank hashes its groups' subtree, sub-roots all-gathered, openings
+//       served by the owning rank); smaller layers on every rank.
 //   queries  each s0 opening by the rank owning its row (subtree siblings +
 //       top levels), all-gathered.
 // The n-domain sections are whole on every rank; calculateZ is row-sharded
@@ -54,6 +57,7 @@ public:
         std::vector<std::vector<uint64_t>> top;  // [0]: W sub-roots ... [last]: root
     };
     Tree trees[5];  // cm1, cm2, cm3, cm4, constants
+    std::vector<Tree> ftrees;  // FRI layers (row-sharded where the groups split)
     std::vector<zkgpu_comm_op> ops;
 
     int create_sharded(const zkgpu_stark_info *in, const zkgpu_comm *c)
@@ -107,6 +111,13 @@ public:
         for (auto &t : trees)
             if (dalloc(&t.nodes, zkgpu_gl_merkle_num_elements(B))) return -1;
         slot = std::max<uint64_t>(4, std::max<uint64_t>(3ULL * info.n_ev, (uint64_t)q() * s0_record()));
+        ftrees.assign(fri_steps.size(), Tree{});
+        for (size_t si = 1; si < fri_steps.size(); si++) {
+            const uint64_t ngroups = 1ULL << fri_steps[si], width = (3ULL << fri_steps[si - 1]) / ngroups;
+            if (!fri_sharded(ngroups)) continue;
+            if (dalloc(&ftrees[si].nodes, zkgpu_gl_merkle_num_elements(ngroups / W))) return -1;
+            slot = std::max<uint64_t>(slot, (uint64_t)q() * (width + 4ULL * fri_steps[si]));
+        }
         return dalloc(&xchg, slot * W);
     }
 
@@ -176,8 +187,14 @@ public:
         t.block = blk;
         t.ld = ld;
         t.ncols = ncols;
+        return top_levels(t, B, root);
+    }
+
+    // the W sub-roots all-gathered, the top log2 W levels hashed on the host
+    int top_levels(Tree &t, uint64_t rows, uint64_t root[4])
+    {
         uint64_t sub[4];
-        CK(zkgpu_memcpy_d2h(sub, t.nodes + zkgpu_gl_merkle_num_elements(B) - 4, 32));
+        CK(zkgpu_memcpy_d2h(sub, t.nodes + zkgpu_gl_merkle_num_elements(rows) - 4, 32));
         t.top.assign(1, {});
         if (allgather(sub, 4, t.top[0])) return -1;
         while (t.top.back().size() > 4) {
@@ -228,6 +245,60 @@ public:
         tstart();
         if (merkelize(t, blk, BH, ncols, root)) return -1;
         if (tree_name && tstop(tree_name)) return -1;
+        return 0;
+    }
+
+    bool fri_sharded(uint64_t ngroups) const { return W > 1 && ngroups % W == 0 && ngroups / W >= 2; }
+
+    // FRI layer tree: each rank hashes its block of groups (friProve.cpp:125-133)
+    int fri_commit(size_t si, uint64_t ngroups, uint64_t width, uint64_t root[4]) override
+    {
+        if (!fri_sharded(ngroups)) return Starks::fri_commit(si, ngroups, width, root);
+        const uint64_t bl = ngroups / W;
+        Tree &t = ftrees[si];
+        t.block = fri_aux[si] + (uint64_t)R * bl * width;
+        t.ld = width;
+        CK(zkgpu_gl_merkletree_rows_dev(t.nodes, t.block, width, bl));
+        return top_levels(t, bl, root);
+    }
+
+    // openings served by the rank owning the group, the records all-gathered
+    int fri_open(size_t si, uint64_t ngroups, uint64_t width, const std::vector<uint64_t> &yq, uint64_t *vals,
+                 uint64_t *sibs) override
+    {
+        if (!fri_sharded(ngroups)) return Starks::fri_open(si, ngroups, width, yq, vals, sibs);
+        const uint64_t bl = ngroups / W, levels = fri_steps[si];
+        uint32_t log_b = 0;
+        while ((1ULL << log_b) < bl) log_b++;
+        const uint64_t rec = width + 4 * levels;
+        const Tree &t = ftrees[si];
+        std::vector<uint64_t> mine((uint64_t)q() * rec, 0), own, local;
+        for (uint32_t qi = 0; qi < q(); qi++)
+            if (yq[qi] / bl == R) {
+                own.push_back(qi);
+                local.push_back(yq[qi] % bl);
+            }
+        if (!own.empty()) {
+            std::vector<uint64_t> v(own.size() * width + 1), sb(own.size() * log_b * 4 + 1);
+            CK(zkgpu_gl_merkle_open_rows_dev(v.data(), sb.data(), t.nodes, t.block, width, bl, local.data(),
+                                             own.size()));
+            for (size_t k = 0; k < own.size(); k++) {
+                uint64_t *r = &mine[own[k] * rec];
+                memcpy(r, &v[k * width], width * 8);
+                memcpy(r + width, &sb[k * log_b * 4], log_b * 32ULL);
+                uint64_t *top = r + width + log_b * 4;
+                uint32_t j = R;
+                for (size_t lv = 0; lv + 1 < t.top.size(); lv++, j >>= 1, top += 4)
+                    memcpy(top, &t.top[lv][4 * (j ^ 1)], 32);
+            }
+        }
+        std::vector<uint64_t> all;
+        if (allgather(mine.data(), mine.size(), all)) return -1;
+        for (uint32_t qi = 0; qi < q(); qi++) {
+            const uint64_t *r = &all[(yq[qi] / bl) * mine.size() + qi * rec];
+            memcpy(vals + (uint64_t)qi * width, r, width * 8);
+            memcpy(sibs + (uint64_t)qi * levels * 4, r + width, levels * 32);
+        }
         return 0;
     }
 

@@ -620,9 +620,7 @@ public:
                 uint64_t ngroups = 1ULL << nb;
                 uint64_t width = (3ULL << fri_steps[si]) / ngroups;
                 CK(zkgpu_fri_transpose_dev(fri_aux[si + 1], fri_pol[cur], 1ULL << fri_steps[si], nb));
-                CK(zkgpu_gl_merkletree_rows_dev(fri_nodes[si + 1], fri_aux[si + 1], width, ngroups));
-                CK(zkgpu_memcpy_d2h(&fri_roots[4 * (si + 1)],
-                                    fri_nodes[si + 1] + zkgpu_gl_merkle_num_elements(ngroups) - 4, 32));
+                if (fri_commit(si + 1, ngroups, width, &fri_roots[4 * (si + 1)])) return -1;
                 tr.put(&fri_roots[4 * (si + 1)], 4);
             } else {
                 CK(zkgpu_memcpy_d2h(final_pol.data(), fri_pol[cur], final_pol.size() * 8));
@@ -642,8 +640,7 @@ public:
                 uint64_t ngroups = 1ULL << fri_steps[si];
                 uint64_t width = (3ULL << fri_steps[si - 1]) / ngroups;
                 std::vector<uint64_t> vals(q() * width), sibs((uint64_t)q() * fri_steps[si] * 4);
-                CK(zkgpu_gl_merkle_open_rows_dev(vals.data(), sibs.data(), fri_nodes[si], fri_aux[si], width, ngroups,
-                                                 yq.data(), q()));
+                if (fri_open(si, ngroups, width, yq, vals.data(), sibs.data())) return -1;
                 memcpy(w, &fri_roots[4 * si], 32);
                 w += 4;
                 memcpy(w, vals.data(), vals.size() * 8);
@@ -661,6 +658,21 @@ public:
         if (tr.err) return fail("transcript hashing failed: %s", zkgpu_last_error());
         if ((uint64_t)(w - out) != proof_len()) return fail("proof length mismatch");
         timers.emplace_back("STARK_TOTAL", std::chrono::duration<double, std::milli>(clk::now() - tall).count());
+        return 0;
+    }
+
+    // FRI layer si's tree over its ngroups x width row-major groups (friProve.cpp:125-133)
+    virtual int fri_commit(size_t si, uint64_t ngroups, uint64_t width, uint64_t root[4])
+    {
+        CK(zkgpu_gl_merkletree_rows_dev(fri_nodes[si], fri_aux[si], width, ngroups));
+        CK(zkgpu_memcpy_d2h(root, fri_nodes[si] + zkgpu_gl_merkle_num_elements(ngroups) - 4, 32));
+        return 0;
+    }
+    // its openings at groups yq (vals q x width, siblings q x log2(ngroups) x 4)
+    virtual int fri_open(size_t si, uint64_t ngroups, uint64_t width, const std::vector<uint64_t> &yq, uint64_t *vals,
+                         uint64_t *sibs)
+    {
+        CK(zkgpu_gl_merkle_open_rows_dev(vals, sibs, fri_nodes[si], fri_aux[si], width, ngroups, yq.data(), q()));
         return 0;
     }
 
