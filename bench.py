@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--blowup-bits", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-lde", action="store_true", help="skip the secondary LDE measurement (stark workload)")
+    ap.add_argument("--no-handoff", action="store_true",
+                    help="skip the host->device trace hand-off timing (stark workload, N=1)")
     ap.add_argument("--lde-steps", type=int, default=10)
     ap.add_argument("--sharded-impl", choices=["cpp", "py"], default="cpp",
                     help="stark-sharded: the C++ prover over RCCL (default) or the Python orchestration")
@@ -435,6 +437,35 @@ def step42ns_roofline(s42, kernels, steps):
             "avg_launch_ms": round(dev_ms, 4)}
 
 
+def handoff_measure(n, C, dev, torch, zkgpu, s_per_proof):
+    """The drop-in boundary hands the committed trace over in HOST memory
+    (zkevmCmPols file / executor buffer, row-major, commit_pols.hpp:18):
+    time its upload into the device column-major section with the streamed
+    loader (zkgpu_load_rows_dev: block H2D on a copy stream overlapped with
+    the transposes), pageable and page-locked.  Reported beside the proof
+    rate, never as `value` (the timed proof starts with the trace in HBM)."""
+    import numpy as np
+    rows = np.empty((n, C), np.uint64)
+    rows.fill(1)  # touch every page before timing
+    cols = torch.empty((C, n), dtype=torch.int64, device=dev)
+    res = {"bytes": int(rows.nbytes), "what": "cm1 %d rows x %d cols, host row-major -> device column-major "
+           "(zkgpu_load_rows_dev)" % (n, C)}
+    for key, reg in (("pageable", False), ("registered", True)):
+        best = None
+        for _ in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            zkgpu.load_rows_dev(cols, n, rows, register_host=reg)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        res[key] = {"ms": round(best * 1e3, 2), "GB/s": round(rows.nbytes / best / 1e9, 1)}
+    up = min(res["pageable"]["ms"], res["registered"]["ms"]) * 1e-3
+    res["s_per_proof_incl_upload"] = round(s_per_proof + up, 4)
+    del rows, cols
+    return res
+
+
 def cpu_full_main(args):
     """Time the oracle prover once at the full config-4 size (rank 0, no GPU)."""
     res = cpu_baseline_stark(args.log_n, args.blowup_bits, args.ncols, args.queries)
@@ -466,7 +497,7 @@ def main():
     C = args.ncols
     res = {"metric": METRIC}
     gs = ss = inst = None
-    lde = roof = None
+    lde = roof = handoff = None
     if args.workload == "lde":
         lde, roof = lde_measure(args, dev, torch, world, dist)
         elapsed = lde["ms_per_lde"] * 1e-3 * args.steps
@@ -532,6 +563,8 @@ def main():
         stages = gs.timers() if gs is not None else (ss.timers if ss is not None else None)
         if args.workload == "stark" and not args.no_lde:
             lde, roof = lde_measure(args, dev, torch, world, dist)
+        if args.workload == "stark" and world == 1 and not args.no_handoff:
+            handoff = handoff_measure(n, C, dev, torch, zkgpu, value)
 
     if rank == 0:
         cpu = None
@@ -606,6 +639,8 @@ def main():
             res["lde"] = lde
         if roof is not None:
             res["roofline"] = roof
+        if handoff is not None:
+            res["handoff"] = handoff
         if kernels is not None:
             res["kernels"] = kernel_table(kernels)
             if args.workload == "stark" and args.log_n == 23 and C == 100:
