@@ -24,7 +24,7 @@ def rand_gl(rng, shape, noncanon=False):
 
 # ------------------------------------------------------------------ NTT
 @pytest.mark.parametrize("logn,ncols", [(0, 1), (1, 2), (4, 3), (8, 1), (10, 5), (12, 2), (13, 1), (14, 3),
-                                        (16, 4), (17, 1), (19, 2)])
+                                        (16, 4), (17, 1), (19, 2), (20, 2)])
 def test_ntt_vs_oracle(oracle, zkgpu, logn, ncols):
     rng = np.random.default_rng(100 + logn)
     x = rand_gl(rng, (1 << logn, ncols))

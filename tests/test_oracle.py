@@ -161,3 +161,26 @@ def test_batch_inverse3(oracle):
     inv = oracle.batch_inverse3(x)
     for i in range(33):
         assert np.array_equal(inv[3 * i:3 * i + 3], oracle.gl3_inv(x[3 * i:3 * i + 3]))
+
+
+def test_config1_ntt_2p20_roundtrip(oracle):
+    """BASELINE configs[0]: the 2^20-point forward + inverse NTT on the CPU is
+    the identity (NTT_Goldilocks::NTT / INTT, starks.cpp:262,285); plus two
+    outputs against the DFT definition (Horner over the 2^20 inputs)."""
+    import time
+    rng = np.random.default_rng(20)
+    n = 1 << 20
+    x = rand_gl(rng, (n, 2))
+    t0 = time.perf_counter()
+    y = oracle.ntt(x)
+    z = oracle.ntt(y, True)
+    dt = time.perf_counter() - t0
+    assert np.array_equal(z, x)
+    w = oracle.gl_w(20)
+    for k in (1, n - 3):
+        wk = pow(w, k, P)
+        acc = 0
+        for v in x[::-1, 1].tolist():  # Horner: sum_j x_j wk^j
+            acc = (acc * wk + v) % P
+        assert int(y[k, 1]) == acc
+    print("config 1: 2^20 x 2 forward + inverse NTT on the CPU oracle in %.3f s" % dt)
