@@ -111,6 +111,11 @@ __device__ __forceinline__ uint64_t gl_pow(uint64_t a, uint64_t e)
 }
 
 // x * 2^E (mod p), compile-time E in [0, 192): 2^96 = -1, 2^192 = 1.
+// With lo = x << k = l0 + 2^32 l1 and hl = x >> (64 - k) (x 2^k = lo + 2^64 hl):
+//   E = 32 + k (0 < k < 32):  x 2^E == (l0 + l1) 2^32 - (l1 + hl)
+//   E = 64 + k (0 <= k < 32): x 2^E == (l0 - hl) 2^32 - (l0 + l1)
+// (2^64 == 2^32 - 1, 2^96 == -1): 10-11 instructions instead of a 128-bit
+// reduction (E < 64) or two chained shift-multiplies (E >= 64, 23-30).
 template <int E>
 __device__ __forceinline__ uint64_t mul2e(uint64_t x)
 {
@@ -122,9 +127,28 @@ __device__ __forceinline__ uint64_t mul2e(uint64_t x)
     } else if constexpr (E <= 32) {
         return gl_reduce96(x << E, (uint32_t)(x >> (64 - E)));
     } else if constexpr (E < 64) {
-        return gl_reduce128(x << E, x >> (64 - E));
+        constexpr int k = E - 32;
+        const uint64_t lo = x << k;
+        const uint32_t hl = (uint32_t)(x >> (64 - k));
+        const uint32_t l0 = (uint32_t)lo, l1 = (uint32_t)(lo >> 32);
+        uint32_t s1;
+        const uint32_t s0 = __builtin_addc(l0, l1, 0u, &s1);
+        // (l0 + l1) 2^32 == s0 2^32 + s1 (2^32 - 1), < 2^64 as one word pair
+        const uint64_t u = ((uint64_t)s0 << 32) | (s1 ? 0xFFFFFFFFu : 0u);
+        uint64_t r;
+        const bool b = __builtin_sub_overflow(u, (uint64_t)l1 + hl, &r);
+        return r - (b ? ZK_EPS : 0ULL);  // b => r >= 2^64 - 2^33: no second borrow
     } else {
-        return mul2e<E - 48>(mul2e<48>(x));
+        constexpr int k = E - 64;
+        const uint64_t lo = x << k;
+        const uint32_t hl = k ? (uint32_t)(x >> (64 - (k ? k : 1))) : 0u;
+        const uint32_t l0 = (uint32_t)lo, l1 = (uint32_t)(lo >> 32);
+        // (l0 - hl) 2^32: when hl > l0, (2^32 + l0 - hl) 2^32 - 2^64 == ... - (2^32 - 1)
+        const uint32_t a = l0 - hl;
+        const uint64_t c = (uint64_t)l0 + l1 + (hl > l0 ? ZK_EPS : 0ULL);  // < 2^34
+        uint64_t r;
+        const bool b = __builtin_sub_overflow((uint64_t)a << 32, c, &r);
+        return r - (b ? ZK_EPS : 0ULL);
     }
 }
 
