@@ -254,7 +254,7 @@ int zkgpu_init(int device)
     if ((rc = check_hip(hipSetDevice(device), "hipSetDevice"))) return rc;
     c.device = device;
     for (int d = 0; d < 2; d++) {
-        if ((rc = alloc_dev(&c.rt_small[d], 2048)) || (rc = alloc_dev(&c.tw_lo[d], TW_LEVEL_SIZE)) ||
+        if ((rc = alloc_dev(&c.rt_small[d], 4096)) || (rc = alloc_dev(&c.tw_lo[d], TW_LEVEL_SIZE)) ||
             (rc = alloc_dev(&c.tw_hi[d], TW_LEVEL_SIZE)))
             return rc;
         uint64_t w12 = h_w(12), w28 = h_w(TW_MAX_LOG);
@@ -262,7 +262,7 @@ int zkgpu_init(int device)
             w12 = h_inv(w12);
             w28 = h_inv(w28);
         }
-        fill_powers(c.rt_small[d], w12, 1, 1, 2048, c.stream);
+        fill_powers(c.rt_small[d], w12, 1, 1, 4096, c.stream);
         fill_powers(c.tw_lo[d], w28, 1, 1, TW_LEVEL_SIZE, c.stream);
         fill_powers(c.tw_hi[d], w28, TW_LEVEL_SIZE, 1, TW_LEVEL_SIZE, c.stream);
     }

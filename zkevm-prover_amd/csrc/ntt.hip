@@ -69,6 +69,7 @@ struct PassArgs {
     uint32_t npass;
     uint32_t rbits[NTT_MAX_PASSES];
     const uint64_t *otw;  // outer twiddles omega_m^(j' k) at [k << logmp | j'] (null: recurrence)
+    const uint64_t *rt4096;  // omega_4096^e, e < 4096, this direction (the pass's omega_R table)
     uint32_t ncols;       // columns in this launch (grid x = unit * ncols + column)
 };
 
@@ -149,8 +150,12 @@ __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
     uint64_t *dst = a.dst + (uint64_t)col * a.dst_ld;
     const int tid = threadIdx.x;
 
-    // omega_R^i = omega_{2^28}^(i << (28 - LOGR))
-    for (int i = tid; i < R; i += T) twR[i] = tw_big(a.tw_lo, a.tw_hi, (uint64_t)i << (TW_MAX_LOG - LOGR));
+    // omega_R^i = omega_4096^(i << (12 - LOGR)) (R <= 256)
+    static_assert(LOGR <= 12, "radix");
+    if (a.rt4096)
+        for (int i = tid; i < R; i += T) twR[i] = a.rt4096[i << (12 - LOGR)];
+    else
+        for (int i = tid; i < R; i += T) twR[i] = tw_big(a.tw_lo, a.tw_hi, (uint64_t)i << (TW_MAX_LOG - LOGR));
 
     uint64_t v[R2 > R1 ? R2 : R1];
     // ------------------------------------------------ step 1 (load + R1-DFT)
@@ -509,6 +514,11 @@ int ntt_columns(Ctx &ctx, uint64_t *dst, uint64_t dst_ld, const uint64_t *src, u
         return check_launch("k_ntt_small");
     }
     PassArgs a;
+    static const bool twr_table = [] {  // A/B switch: omega_R from the table or from the 2-level product
+        const char *e = getenv("ZKGPU_NTT_TWR_TABLE");
+        return !e || atoi(e) != 0;
+    }();
+    a.rt4096 = twr_table ? ctx.rt_small[d] : nullptr;
     a.tw_lo = ctx.tw_lo[d];
     a.tw_hi = ctx.tw_hi[d];
     a.logn = logn;

@@ -24,7 +24,7 @@ struct Ctx {
     bool ready = false;
     hipStream_t stream = nullptr;  // launches go here (zkgpu_set_stream)
     // direction 0 = forward, 1 = inverse
-    uint64_t *rt_small[2] = {nullptr, nullptr};  // omega_4096^k, k < 2048
+    uint64_t *rt_small[2] = {nullptr, nullptr};  // omega_4096^k, k < 4096 (this direction)
     uint64_t *tw_lo[2] = {nullptr, nullptr};     // omega_{2^28}^i, i < 2^14
     uint64_t *tw_hi[2] = {nullptr, nullptr};     // omega_{2^28}^(2^14 i)
     // LDE post-scale tables (1/n * 7^k), cached per log n
