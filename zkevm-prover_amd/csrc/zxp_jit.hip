@@ -842,6 +842,32 @@ int zxp_jit_run(const ZxpJitIn &in, hipStream_t s)
     if (rc) return rc;
     hipFunction_t fn;
     if ((rc = compile(src, &fn))) return rc;
+    // A kernel the compiler leaves at 169-256 VGPRs runs 2 waves per SIMD and
+    // is latency-bound; recompile it with an occupancy target of 3 (<= 168
+    // VGPRs).  Config-4 quotient: 186 VGPRs, 15.3 -> 12.7 ms; kernels that
+    // already fit 3+ waves are left alone (a target there lets the scheduler
+    // spend registers: FRI polynomial 8.9 -> 9.2 ms).  Larger kernels (one
+    // wave) and the block-split large programs (compiled for minutes, their
+    // registers bounded by the blocks) are left as they are.
+    // ZKGPU_ZXP_JIT_AUTOWAVES=0 disables.
+    static const bool auto_waves = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_AUTOWAVES");
+        return !e || atoi(e) != 0;
+    }();
+    if (auto_waves && in.waves_per_eu == 0 && src.find("#define ZKJIT_SPLIT 1") == std::string::npos) {
+        int regs = 0;
+        if (hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, fn) == hipSuccess && regs > 168 && regs <= 256) {
+            ZxpJitIn in3 = in;
+            in3.waves_per_eu = 3;
+            std::string src3;
+            cp.clear();
+            kc.clear();
+            kl.clear();
+            zt.clear();
+            if ((rc = zxp_jit_build_source(in3, src3, cp, kc, kl, zt))) return rc;
+            if ((rc = compile(src3, &fn))) return rc;
+        }
+    }
     // tables: zt | cp | kc | kl
     const size_t off_cp = zt.size() * sizeof(JitTerm), off_kc = off_cp + cp.size() * 8;
     const size_t off_kl = (off_kc + (kc.size() + 1) * 8 + 15) & ~(size_t)15;  // 16-byte limb slots
