@@ -546,23 +546,29 @@ __global__ void __launch_bounds__(256) k_xdivxsub(uint64_t *xdiv, uint64_t *xdiv
 }
 
 // ---------------------------------------------------------------- powers & split
-// out column-major (3 columns, ld): out[k] = base^k, k < n
-__global__ void k_ext_powers(uint64_t *out, uint64_t ld, gl3 base, uint64_t n, uint32_t per_thread)
+// out column-major (3 columns, ld): out[k] = base^k, k < n.  Thread t of T
+// owns rows t + j*T (coalesced stores): r = base^t, stepped by base^T
+__device__ __forceinline__ gl3 gl3_pow(gl3 b, uint64_t e)
 {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t k0 = t * per_thread;
-    if (k0 >= n) return;
-    // base^k0 by square-and-multiply
-    gl3 r{{1, 0, 0}}, b = base;
-    uint64_t e = k0;
+    gl3 r{{1, 0, 0}};
     while (e) {
         if (e & 1) r = gl3_mul(r, b);
         b = gl3_mul(b, b);
         e >>= 1;
     }
-    for (uint32_t j = 0; j < per_thread && k0 + j < n; j++) {
-        st3(out + k0 + j, ld, r);
-        r = gl3_mul(r, base);
+    return r;
+}
+
+__global__ void k_ext_powers(uint64_t *out, uint64_t ld, gl3 base, uint64_t n)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+    if (t >= n) return;
+    gl3 r = gl3_pow(base, t);
+    const gl3 step = gl3_pow(base, T);
+    for (uint64_t k = t; k < n; k += T) {
+        st3(out + k, ld, r);
+        r = gl3_mul(r, step);
     }
 }
 
@@ -716,8 +722,8 @@ int ext_powers(uint64_t *out, uint64_t ld, const uint64_t base[3], uint64_t n, h
 {
     gl3 b{{base[0] % ZK_P, base[1] % ZK_P, base[2] % ZK_P}};
     const uint32_t per = 64;
-    uint64_t threads = (n + per - 1) / per;
-    hipLaunchKernelGGL(k_ext_powers, dim3(nblk(threads, 256)), dim3(256), 0, s, out, ld, b, n, per);
+    const uint64_t threads = (n + per - 1) / per;
+    hipLaunchKernelGGL(k_ext_powers, dim3(nblk(threads, 256)), dim3(256), 0, s, out, ld, b, n);
     return check_launch("k_ext_powers");
 }
 
