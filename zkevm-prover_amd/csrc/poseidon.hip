@@ -13,8 +13,6 @@
 //
 // Leaves: one thread per row; a column-major (SoA) source makes each of the
 // ceil(ncols/8) absorption steps a fully coalesced 8-column read.
-#include <stdlib.h>
-
 #include "poseidon_perm.hpp"
 #include "zkgpu_internal.hpp"
 
@@ -34,22 +32,8 @@ __global__ void k_poseidon_batch(uint64_t *out, const uint64_t *in, uint64_t n, 
 }
 
 // leaf digests from a column-major source (column c at src + c*ld)
-template <int WAVES>
-__device__ __forceinline__ void leaves_cols_body(uint64_t *digests, const uint64_t *__restrict__ src, uint64_t ncols,
-                                                 uint64_t nrows, uint64_t ld);
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) k_leaves_cols_w6(
-    uint64_t *digests, const uint64_t *__restrict__ src, uint64_t ncols, uint64_t nrows, uint64_t ld)
-{
-    leaves_cols_body<6>(digests, src, ncols, nrows, ld);
-}
 __global__ void __launch_bounds__(256) k_leaves_cols(uint64_t *digests, const uint64_t *__restrict__ src,
                                                     uint64_t ncols, uint64_t nrows, uint64_t ld)
-{
-    leaves_cols_body<0>(digests, src, ncols, nrows, ld);
-}
-template <int WAVES>
-__device__ __forceinline__ void leaves_cols_body(uint64_t *digests, const uint64_t *__restrict__ src, uint64_t ncols,
-                                                 uint64_t nrows, uint64_t ld)
 {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nrows) return;
@@ -287,15 +271,7 @@ int merkle_leaves_cols(uint64_t *digests, const uint64_t *src, uint64_t ncols, u
 {
     if (!nrows) return 0;
     prof_begin(s);
-    static const bool w6 = [] {  // A/B: the leaf kernel at a 6-wave occupancy target
-        const char *e = getenv("ZKGPU_LEAVES_W6");
-        return e && atoi(e) != 0;
-    }();
-    if (w6)
-        hipLaunchKernelGGL(k_leaves_cols_w6, dim3(blocks_for(nrows, 256)), dim3(256), 0, s, digests, src, ncols, nrows,
-                           ld);
-    else
-        hipLaunchKernelGGL(k_leaves_cols, dim3(blocks_for(nrows, 256)), dim3(256), 0, s, digests, src, ncols, nrows, ld);
+    hipLaunchKernelGGL(k_leaves_cols, dim3(blocks_for(nrows, 256)), dim3(256), 0, s, digests, src, ncols, nrows, ld);
     prof_end("k_leaves_cols", 8.0 * (double)nrows * (double)ncols + 32.0 * (double)nrows, s);
     return check_launch("k_leaves_cols");
 }
