@@ -54,6 +54,7 @@ struct PassArgs {
     const uint64_t *src;
     uint64_t src_ld;
     uint64_t src_valid;  // rows >= src_valid are zero (LDE padding)
+    uint32_t half_zero;  // first pass of a zero-padded forward transform: inputs j1 >= R1/2 are zero
     uint64_t *dst;
     uint64_t dst_ld;
     const uint64_t *tw_lo;  // big twiddles omega_{2^28}, this direction
@@ -111,6 +112,24 @@ __device__ __forceinline__ void dft_regs(uint64_t *v)
         }(std::make_integer_sequence<int, R / (2 * H)>{});
         dft_regs<LOG, INV, H / 2>(v);
     }
+}
+
+// dft_regs when the upper half of v[] is zero (the zero-padded LDE input):
+// the first stage's butterflies are (a, 0) -> (a, a * 2^e), exactly what
+// gl_add(a, 0) / gl_sub(a, 0) return, without the adds
+template <int LOG, bool INV>
+__device__ __forceinline__ void dft_regs_half(uint64_t *v)
+{
+    constexpr int R = 1 << LOG, H = R / 2;
+    [&]<int... Is>(std::integer_sequence<int, Is...>) {
+        ([&]<int I>() {
+            constexpr int e = (96 * I) / H;
+            static_assert(!INV, "forward only");
+            if constexpr (e == 0) v[I + H] = v[I];
+            else v[I + H] = mul2e<e>(v[I]);
+        }.template operator()<Is>(), ...);
+    }(std::make_integer_sequence<int, H>{});
+    dft_regs<LOG, INV, H / 2>(v);
 }
 
 __host__ __device__ constexpr int brev_c(int x, int bits)
@@ -188,7 +207,14 @@ __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
             v[j1] = pos < a.src_valid ? src[pos] : 0;
         }
     }
-    dft_regs<L1, INV>(v);
+    if constexpr (!INV) {
+        if (a.half_zero)
+            dft_regs_half<L1, INV>(v);
+        else
+            dft_regs<L1, INV>(v);
+    } else {
+        dft_regs<L1, INV>(v);
+    }
     __syncthreads();  // twR ready
 #pragma unroll
     for (int r = 0; r < R1; r++) {
@@ -535,10 +561,19 @@ int ntt_columns(Ctx &ctx, uint64_t *dst, uint64_t dst_ld, const uint64_t *src, u
         const uint32_t rb = a.rbits[p];
         a.post_step = h_pow(post_base, (uint64_t)(1u << (rb / 2)) << (logn - rb));
         a.otw = a.last ? nullptr : otw_table(ctx, d, logm, rb, s);
+        a.half_zero = 0;
         if (p == 0) {
             a.src = src;
             a.src_ld = src_ld;
             a.src_valid = src_valid;
+            // zero-padded forward input: exactly the rows j1 >= R1/2 of every
+            // sub-DFT (positions (R2 j1 + j2) * n / R) are past src_valid
+            const uint32_t l1 = rb / 2;  // launch_pass<L1 = rb/2, L2 = rb - L1>
+            static const bool half_env = [] {  // A/B switch
+                const char *e = getenv("ZKGPU_NTT_HALF");
+                return !e || atoi(e) != 0;
+            }();
+            a.half_zero = (half_env && !inverse && l1 >= 1 && src_valid == (1ULL << (logn - 1))) ? 1u : 0u;
         } else {
             a.src = tmp;
             a.src_ld = tmp_ld;
