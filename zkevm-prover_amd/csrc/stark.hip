@@ -261,7 +261,7 @@ __global__ void __launch_bounds__(ZXP_THREADS) k_zxp_eval(ZxpEnv e)
 //   k_z_apply:  z = tile prefix * thread prefix * running product, through LDS
 constexpr int BI_CHUNK = 16;  // k_xdivxsub / k_ext: rows per thread sharing one inversion
 constexpr int SCAN_THREADS = 256;
-constexpr int Z_PER = 8;
+constexpr int Z_PER = 4;
 constexpr uint64_t Z_TILE = SCAN_THREADS * Z_PER;
 // LDS slot of tile row e: one pad slot per Z_PER rows (run reads: 2-way bank conflicts)
 __device__ __forceinline__ int z_slot(int e) { return e + e / Z_PER; }
