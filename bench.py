@@ -414,9 +414,9 @@ def step42ns_setup(args, dev, torch, g):
     def step():
         zkgpu.zxp_eval_dev(prog, dsecs, log_dom, chal, pub, evals, extend_bits=1, x_start=7)
 
-    # the full-size program runs on the interpreter: its compiled kernel takes
-    # over an hour of hiprtc; --s42-jit with a smaller
-    # --s42-scale (0.25: cached by build()) times the compiled kernel
+    # default: the interpreter.  --s42-jit times the compiled kernel: scale
+    # 0.25 is cached by build(), the full-size kernel (~10 min of hiprtc) by
+    # tools/jit_prebuild.py --full
     os.environ["ZKGPU_ZXP_JIT"] = "2" if args.s42_jit else "0"
     return step, {"rows": NE, "log_dom": log_dom, "n_ops": int(len(ops)), "cols_read": cols,
                   "alg_bytes": 8.0 * NE * (cols + 3), "tensors": dsecs}

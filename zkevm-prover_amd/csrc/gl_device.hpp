@@ -241,11 +241,22 @@ struct Dot3 {
         A1 += (uint64_t)a1 * c[4];
         A2 += (uint64_t)a1 * c[5];
     }
-    // the same from a 16-byte aligned limb slot (one 16-byte + one 8-byte load)
+    // the same from a 16-byte aligned limb slot (one 16-byte + one 8-byte load;
+    // ZK_LIMB_AS: the address space a run-time compiled kernel reads its limb
+    // table through, csrc/zxp_jit.hip)
     __device__ __forceinline__ void term_al(uint64_t a, const uint32_t *c)
     {
+#ifdef ZK_LIMB_AS
+        typedef uint32_t u32x4_ __attribute__((ext_vector_type(4)));
+        typedef uint32_t u32x2_ __attribute__((ext_vector_type(2)));
+        const u32x4_ qv = *(const ZK_LIMB_AS u32x4_ *)c;
+        const u32x2_ rv = *(const ZK_LIMB_AS u32x2_ *)(c + 4);
+        const LimbQ q{qv.x, qv.y, qv.z, qv.w};
+        const LimbP r{rv.x, rv.y};
+#else
         const LimbQ q = *(const LimbQ *)c;
         const LimbP r = *(const LimbP *)(c + 4);
+#endif
         const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);
         A0 += (uint64_t)a0 * q.x;
         A1 += (uint64_t)a0 * q.y;

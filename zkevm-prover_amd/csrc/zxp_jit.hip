@@ -141,7 +141,11 @@ extern "C" __global__ void __launch_bounds__(256) ZKJIT_WAVES zxp_jit(const JitP
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (1ULL << p.logdom)) return;
     const uint64_t m = p.rmask;
+#ifdef ZK_CP_AS
+#define C(j, sh) gload((const uint64_t *)(((const ZK_CP_AS uint64_t *)p.cp)[j]) + ((i + (uint64_t)(sh)) & m))
+#else
 #define C(j, sh) gload(p.cp[j] + ((i + (uint64_t)(sh)) & m))
+#endif
 // a global limb table is re-based in every code block (an opaque copy of K):
 // with thousands of loads off one base register, SIFoldOperands dominated
 // the compile (48 s of 100 for step3prev)
@@ -649,10 +653,19 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         return (uint32_t)(e ? atol(e) : 1000);
     }();
     const bool split = in.n_instr >= split_min;
-    size_t block_start = 0;
+    // ZKGPU_ZXP_JIT_SYNC=n: a workgroup barrier every n blocks keeps the
+    // workgroup's waves in the same stretch of code, so an instruction-cache
+    // line fetched for one wave serves the others (experiment, default off)
+    static const int sync_every = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_SYNC");
+        return e ? atoi(e) : 0;
+    }();
+    size_t block_start = 0, n_blocks = 0;
     auto maybe_split = [&] {
         if (split && body.size() - block_start >= block) {
-            body += "}\nif (zk_one()) { ZK_KREFRESH\n";
+            body += "}\n";
+            if (sync_every > 0 && ++n_blocks % sync_every == 0) body += "__syncthreads();\n";
+            body += "if (zk_one()) { ZK_KREFRESH\n";
             block_start = body.size();
         }
     };
@@ -794,7 +807,33 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         emit_streams(k);
     }
     // assemble: prelude, params, declarations, body, deferred stores
-    src = k_gl_device_src;
+    // Address space of the wave-uniform tables a kernel reads from global
+    // memory (ZKGPU_ZXP_JIT_KAS: the DOT limb table when not in LDS,
+    // ZKGPU_ZXP_JIT_CPAS: the column pointers; 0 generic = FLAT loads,
+    // 1 global = vector loads, 4 constant = scalar loads).  Block-split
+    // programs hide their limb table base behind an asm copy per block (so it
+    // is not provably uniform and was read with FLAT loads, which also count
+    // on LGKM_CNT) and loaded every column pointer with a vector load ahead of
+    // the dependent column load: quarter-size step42ns-shaped program at 2^24
+    // rows, limbs/pointers FLAT/vector 302 ms, global/vector 272, FLAT/scalar
+    // 277, global/scalar 251 (default for split programs), scalar/scalar 293
+    // (scalar limbs: 106 SGPRs, spills).  Small programs keep the compiler's
+    // choice (their limbs already come from scalar loads).
+    static const int kas_env = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_KAS");
+        return e ? atoi(e) : -1;
+    }();
+    static const int cpas_env = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_CPAS");
+        return e ? atoi(e) : -1;
+    }();
+    const int kas = kas_env < 0 ? (split ? 1 : 0) : kas_env;
+    const int cpas = cpas_env < 0 ? (split ? 4 : 0) : cpas_env;
+    src.clear();
+    if ((kas == 1 || kas == 4) && !jit_kl_lds(kl.size()))
+        appendf(src, "#define ZK_LIMB_AS __attribute__((address_space(%d)))\n", kas);
+    if (cpas == 1 || cpas == 4) appendf(src, "#define ZK_CP_AS __attribute__((address_space(%d)))\n", cpas);
+    src += k_gl_device_src;
     appendf(src, "#define ZKJIT_KL_LDS %d\n", jit_kl_lds(kl.size()) ? 1 : 0);
     appendf(src, "#define ZKJIT_SPLIT %d\n", split ? 1 : 0);  // large program: compile-time options (rtc_compile)
     {
