@@ -6,7 +6,4 @@ if grep -q "NOT cached" gpurun_out/s42f_check.txt; then echo "full-size kernel n
 timeout -k 10 300 python bench.py --workload step42ns --s42-scale 1.0 --s42-jit --no-cpu --steps 3 --warmup 1 > gpurun_out/s42f_jit.json 2> gpurun_out/s42f_jit.err || exit $?
 python3 -c "import json; d=json.load(open('gpurun_out/s42f_jit.json')); print('full jit', d['value'], d['unit'], d['ms_per_step'], d.get('roofline'))"
 cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/s42f_prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --workload step42ns --s42-scale 1.0 --s42-jit --no-cpu --steps 3 --warmup 1 > $GRAFT_REPO_ROOT/gpurun_out/s42f_prof.json 2> $GRAFT_REPO_ROOT/gpurun_out/s42f_prof.err || exit $?
-# address-translation and memory-latency counters of the quarter-size kernel
-B="python3 $GRAFT_REPO_ROOT/bench.py --workload step42ns --s42-scale 0.25 --s42-jit --no-cpu --steps 3 --warmup 1"
-timeout -s KILL 200 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum SQ_INSTS_VMEM_RD SQ_WAVES SQ_WAIT_ANY SQ_WAVE_CYCLES --kernel-trace -d $GRAFT_REPO_ROOT/gpurun_out/s42_tlb -o p --output-format csv -- $B > $GRAFT_REPO_ROOT/gpurun_out/s42_tlb.log 2>&1 || exit $?
 echo done
