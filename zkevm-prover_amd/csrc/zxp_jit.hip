@@ -70,6 +70,7 @@ struct JitParams {
 // (scalar loads of every term's limbs hoisted by the scheduler spill SGPRs
 // into VGPR lanes -- thousands of v_readlane/v_writelane per row).
 constexpr size_t JIT_KL_LDS_MAX = 48 * 1024;
+constexpr int JIT_KCHUNK = 1024;  // words per LDS limb chunk (256 threads x 16 bytes)
 
 const char *k_kernel_head = R"(
 using namespace zk;
@@ -119,6 +120,12 @@ __device__ __forceinline__ void dot_cols(Dot3 &d0, Dot3 &d1, Dot3 &d2, const Jit
         }
     }
 }
+// one 16-byte slice of a limb chunk per thread (256 threads: 1024 words)
+__device__ __forceinline__ uint4 kpre(const uint32_t *kl, size_t lo)
+{
+    return *(const __attribute__((address_space(1))) uint4 *)(kl + lo + 4 * threadIdx.x);
+}
+__device__ __forceinline__ void kput(uint32_t *dst, uint4 v) { *(uint4 *)(dst + 4 * threadIdx.x) = v; }
 __device__ __forceinline__ int zk_one()
 {
     int c;
@@ -138,8 +145,19 @@ extern "C" __global__ void __launch_bounds__(256) ZKJIT_WAVES zxp_jit(const JitP
 #if ZKJIT_KL_LDS
     __syncthreads();
 #endif
+#if ZKJIT_KL_CHUNK
+    // limb chunks staged in LDS per code block (workgroup barriers: every
+    // thread stays to the end, rows past the domain only skip the stores)
+    const uint64_t i_ = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool live_ = i_ < (1ULL << p.logdom);
+    const uint64_t i = live_ ? i_ : 0;
+    __shared__ __attribute__((aligned(16))) uint32_t kbuf[2 * ZKJIT_KL_CHUNK];
+    kput(kbuf, kpre(p.kl, 0));
+    __syncthreads();
+#else
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (1ULL << p.logdom)) return;
+#endif
     const uint64_t m = p.rmask;
 #ifdef ZK_CP_AS
 #define C(j, sh) gload((const uint64_t *)(((const ZK_CP_AS uint64_t *)p.cp)[j]) + ((i + (uint64_t)(sh)) & m))
@@ -613,22 +631,6 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     std::vector<std::vector<uint32_t>> declare_at(in.n_instr);
     for (uint32_t k = 0; k < in.n_instr; k++)
         if (first_use[k] != UINT32_MAX) declare_at[first_use[k]].push_back(k);
-    // DOT accumulators are declared at function scope (the body is split into
-    // blocks, below) and initialised where the first term arrives
-    std::string dot_decls;
-    auto emit_declarations = [&](uint32_t at) {
-        for (uint32_t k : declare_at[at]) {
-            const size_t k0 = dot_k0[k];
-            if (in.ins[k].op == ZXP_DOT3) {
-                appendf(dot_decls, "Dot3 D%u_0, D%u_1, D%u_2;\n", k, k, k);
-                appendf(body, "D%u_0 = Dot3(K + %zu); D%u_1 = Dot3(K + %zu); D%u_2 = Dot3(K + %zu);\n", k, k0, k,
-                        k0 + 4, k, k0 + 8);
-            } else {
-                appendf(dot_decls, "Dot3 D%u_0;\n", k);
-                appendf(body, "D%u_0 = Dot3(K + %zu);\n", k, k0);
-            }
-        }
-    };
     // Compile time: LLVM's instruction selection and machine scheduler are
     // superlinear in basic-block size (a 600-instruction program took ~60 s
     // as one block).  Every ZKGPU_ZXP_JIT_BLOCK source bytes the body opens a
@@ -653,6 +655,48 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         return (uint32_t)(e ? atol(e) : 1000);
     }();
     const bool split = in.n_instr >= split_min;
+    // Limb chunks in LDS (ZKGPU_ZXP_JIT_KCHUNK): a split program whose limb
+    // table is too large for LDS reads it from global memory, one wave-uniform
+    // 16 + 8-byte vector load pair per term, each taking the texture
+    // addresser's full 64-lane path.  In this mode the table is rewritten in
+    // emission order (kmap), every code block's limbs form one contiguous
+    // chunk of <= JIT_KCHUNK words, the workgroup copies the next block's
+    // chunk into the other half of an LDS double buffer (one 16-byte load per
+    // thread, issued at the block's start) and a barrier closes each block.
+    // Quarter-size step42ns-shaped program at 2^24 rows: 251 -> 189 ms
+    // (global vector loads of the limbs 25 K -> 6.7 K per wave).  Default on
+    // for split programs; ZKGPU_ZXP_JIT_KCHUNK=0 disables.
+    static const int kchunk_env = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_KCHUNK");
+        return e ? atoi(e) : 1;
+    }();
+    const bool kchunk = split && kchunk_env > 0;
+    std::vector<uint32_t> kl2;
+    size_t blk_lo = 0, blk_no = 0;
+    auto kmap = [&](size_t off, size_t n) -> size_t {  // n words of kl at off, in emission order
+        if (!kchunk) return off;
+        const size_t o = kl2.size();
+        kl2.insert(kl2.end(), kl.begin() + off, kl.begin() + off + n);
+        while (kl2.size() % 4) kl2.push_back(0);
+        return o;
+    };
+    // DOT accumulators are declared at function scope (the body is split into
+    // blocks, below) and initialised where the first term arrives
+    std::string dot_decls;
+    auto emit_declarations = [&](uint32_t at) {
+        for (uint32_t k : declare_at[at]) {
+            const size_t k0 = dot_k0[k];
+            if (in.ins[k].op == ZXP_DOT3) {
+                appendf(dot_decls, "Dot3 D%u_0, D%u_1, D%u_2;\n", k, k, k);
+                const size_t m0 = kmap(k0, 12);
+                appendf(body, "D%u_0 = Dot3(K + %zu); D%u_1 = Dot3(K + %zu); D%u_2 = Dot3(K + %zu);\n", k, m0, k,
+                        m0 + 4, k, m0 + 8);
+            } else {
+                appendf(dot_decls, "Dot3 D%u_0;\n", k);
+                appendf(body, "D%u_0 = Dot3(K + %zu);\n", k, kmap(k0, 4));
+            }
+        }
+    };
     // ZKGPU_ZXP_JIT_SYNC=n: a workgroup barrier every n blocks keeps the
     // workgroup's waves in the same stretch of code, so an instruction-cache
     // line fetched for one wave serves the others (experiment, default off)
@@ -661,25 +705,44 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         return e ? atoi(e) : 0;
     }();
     size_t block_start = 0, n_blocks = 0;
+    auto chunk_head = [&] {  // LDS base of this block's chunk; next block's chunk start patched in at the end
+        appendf(body, "const uint32_t *K = kbuf + %d - %zu; const uint4 pf_ = kpre(p.kl, @KLO%zu@);\n",
+                (int)(blk_no & 1) * JIT_KCHUNK, blk_lo, blk_no + 1);
+    };
+    std::vector<size_t> klo_of;  // chunk start of block b
     auto maybe_split = [&] {
-        if (split && body.size() - block_start >= block) {
-            body += "}\n";
-            if (sync_every > 0 && ++n_blocks % sync_every == 0) body += "__syncthreads();\n";
-            body += "if (zk_one()) { ZK_KREFRESH\n";
+        if (split && (body.size() - block_start >= block || (kchunk && kl2.size() - blk_lo > JIT_KCHUNK - 512))) {
+            if (kchunk) {
+                appendf(body, "kput(kbuf + %d, pf_);\n}\n__syncthreads();\n", (int)((blk_no + 1) & 1) * JIT_KCHUNK);
+                blk_lo = kl2.size();
+                blk_no++;
+                klo_of.push_back(blk_lo);
+                body += "if (zk_one()) {\n";
+                chunk_head();
+            } else {
+                body += "}\n";
+                if (sync_every > 0 && ++n_blocks % sync_every == 0) body += "__syncthreads();\n";
+                body += "if (zk_one()) { ZK_KREFRESH\n";
+            }
             block_start = body.size();
         }
     };
     body += split ? "if (zk_one()) {\n" : "{\n";
+    if (kchunk) {
+        klo_of.push_back(0);
+        chunk_head();
+    }
     auto emit_streams = [&](uint32_t at) {
         for (const Stream &st : stream[at]) {
             maybe_split();
+            const size_t kt = kmap(st.kt, st.three ? 24 : 8);
             if (st.three)
                 appendf(body,
                         "{ const uint64_t v_ = %s; D%u_0.term_al(v_, K + %zu); D%u_1.term_al(v_, K + %zu); "
                         "D%u_2.term_al(v_, K + %zu); }\n",
-                        st.val.c_str(), st.dot, st.kt, st.dot, st.kt + 8, st.dot, st.kt + 16);
+                        st.val.c_str(), st.dot, kt, st.dot, kt + 8, st.dot, kt + 16);
             else
-                appendf(body, "D%u_0.term_al(%s, K + %zu);\n", st.dot, st.val.c_str(), st.kt);
+                appendf(body, "D%u_0.term_al(%s, K + %zu);\n", st.dot, st.val.c_str(), kt);
         }
     };
     for (uint32_t k = 0; k < in.n_instr; k++) {
@@ -730,7 +793,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                     const std::string v = o.kind == ZXP_TMP1
                                               ? "a" + std::to_string(o.a)
                                               : "b" + std::to_string(o.a) + ".v[" + std::to_string(tm.comp) + "]";
-                    const size_t kt = limbs6x3(tm.coef);
+                    const size_t kt = kmap(limbs6x3(tm.coef), three ? 24 : 8);
                     if (three)
                         appendf(body,
                                 "{ const uint64_t v_ = %s; D%u_0.term_al(v_, K + %zu); D%u_1.term_al(v_, K + %zu); "
@@ -744,7 +807,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                 maybe_split();
                 std::string e;
                 if (col_read(o.a, o.b, (int32_t)o.c, e)) return 1;
-                const size_t kt = limbs6x3(tm.coef);
+                const size_t kt = kmap(limbs6x3(tm.coef), three ? 24 : 8);
                 if (three)
                     appendf(body,
                             "{ const uint64_t v_ = %s; D%u_0.term_al(v_, K + %zu); D%u_1.term_al(v_, K + %zu); "
@@ -806,6 +869,29 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         if (assign(I.dst, R)) return 1;
         emit_streams(k);
     }
+    if (kchunk) {  // chunk starts of the blocks' successors; the table in emission order, padded for the last copy
+        klo_of.push_back(kl2.size());
+        for (size_t b = 0; b + 1 < klo_of.size(); b++)
+            if (klo_of[b + 1] - klo_of[b] > (size_t)JIT_KCHUNK)
+                return set_error(ZKGPU_ERR_ARG, "zxp jit: limb chunk of block %zu is %zu words", b,
+                                 klo_of[b + 1] - klo_of[b]);
+        std::string b2;
+        b2.reserve(body.size());
+        size_t pos = 0;
+        for (;;) {
+            const size_t at = body.find("@KLO", pos);
+            if (at == std::string::npos) break;
+            const size_t end = body.find('@', at + 4);
+            b2.append(body, pos, at - pos);
+            const size_t b = strtoull(body.c_str() + at + 4, nullptr, 10);
+            b2 += std::to_string(b < klo_of.size() ? klo_of[b] : kl2.size());
+            pos = end + 1;
+        }
+        b2.append(body, pos, std::string::npos);
+        body.swap(b2);
+        kl2.resize(kl2.size() + JIT_KCHUNK, 0);
+        kl.swap(kl2);
+    }
     // assemble: prelude, params, declarations, body, deferred stores
     // Address space of the wave-uniform tables a kernel reads from global
     // memory (ZKGPU_ZXP_JIT_KAS: the DOT limb table when not in LDS,
@@ -830,12 +916,13 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     const int kas = kas_env < 0 ? (split ? 1 : 0) : kas_env;
     const int cpas = cpas_env < 0 ? (split ? 4 : 0) : cpas_env;
     src.clear();
-    if ((kas == 1 || kas == 4) && !jit_kl_lds(kl.size()))
+    if ((kas == 1 || kas == 4) && !kchunk && !jit_kl_lds(kl.size()))
         appendf(src, "#define ZK_LIMB_AS __attribute__((address_space(%d)))\n", kas);
     if (cpas == 1 || cpas == 4) appendf(src, "#define ZK_CP_AS __attribute__((address_space(%d)))\n", cpas);
     src += k_gl_device_src;
-    appendf(src, "#define ZKJIT_KL_LDS %d\n", jit_kl_lds(kl.size()) ? 1 : 0);
-    appendf(src, "#define ZKJIT_SPLIT %d\n", split ? 1 : 0);  // large program: compile-time options (rtc_compile)
+    appendf(src, "#define ZKJIT_KL_LDS %d\n", !kchunk && jit_kl_lds(kl.size()) ? 1 : 0);
+    appendf(src, "#define ZKJIT_SPLIT %d\n", split ? 1 : 0);
+    appendf(src, "#define ZKJIT_KL_CHUNK %d\n", kchunk ? JIT_KCHUNK : 0);  // large program: compile-time options (rtc_compile)
     {
         static const int unroll = [] {  // column terms per loop iteration (loads in flight)
             const char *e = getenv("ZKGPU_ZXP_JIT_UNROLL");
@@ -859,6 +946,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     src += dot_decls;
     src += body;
     src += "}\n";
+    if (kchunk) src += "if (live_) {\n";
     for (uint32_t r = 0; r < wcell.size(); r++) {
         if (wcell[r].second == 0)
             appendf(src, "gstore(const_cast<uint64_t *>(p.cp[%u]) + i, gl_canon(w%u));\n", wcell[r].first, r);
@@ -866,6 +954,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             appendf(src, "gstore(const_cast<uint64_t *>(p.cp[%u]) + ((i + (uint64_t)(%d)) & m), gl_canon(w%u));\n",
                     wcell[r].first, wcell[r].second, r);
     }
+    if (kchunk) src += "}\n";
     src += "#undef C\n}\n";
     return 0;
 }
@@ -936,7 +1025,7 @@ int zxp_jit_run(const ZxpJitIn &in, hipStream_t s)
     p.logomega = in.log_omega;
     p.rmask = in.wrap ? (1ULL << in.log_dom) - 1 : ~0ULL;
     p.zmask = in.zmask;
-    const bool klds = jit_kl_lds(kl.size());
+    const bool klds = jit_kl_lds(kl.size()) && src.find("#define ZKJIT_KL_CHUNK 0") != std::string::npos;
     p.nkl = klds ? (uint32_t)kl.size() : 0;
     p.one = 1;
     void *args[] = {&p};
