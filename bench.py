@@ -425,7 +425,7 @@ def step42ns_setup(args, dev, torch, g):
 def step42ns_roofline(s42, kernels, steps):
     """HBM roofline of the compiled quotient kernel: every section column
     read once + q written (8 B each per row) / its device time per launch."""
-    ks = {k: v for k, v in kernels.items() if k in ("k_zxp_jit", "k_zxp_eval")}  # compiled kernel / interpreter
+    ks = {k: v for k, v in kernels.items() if k.startswith("k_zxp_jit") or k == "k_zxp_eval"}  # compiled / interpreter
     if not ks:
         return None
     dev_ms = sum(v[1] for v in ks.values()) / steps

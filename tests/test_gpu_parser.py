@@ -105,18 +105,21 @@ def test_steps_parser_eval_host_dropin(oracle, zkgpu):
     assert np.array_equal(q, qref)
 
 
-def test_step42ns_shaped_jit_gpu_equals_oracle(oracle, zkgpu, monkeypatch):
-    """the compiled expression kernel (csrc/zxp_jit.hip) of the step42ns-shaped
-    program (a quarter of step42ns's opcode counts, 5.3 K ops) at 2^16 rows ==
-    the oracle parser.  The kernel comes from the on-disk cache build() fills
-    (tools/jit_prebuild.py; hiprtc takes minutes at this size), as the
-    reference ships its expression code compiled."""
+@pytest.mark.parametrize("scale", [0.25, 1.0])
+def test_step42ns_shaped_jit_gpu_equals_oracle(oracle, zkgpu, monkeypatch, scale):
+    """the compiled expression kernels (csrc/zxp_jit.hip) of the step42ns-shaped
+    program at 2^16 rows == the oracle parser: a quarter of step42ns's opcode
+    counts (5.3 K ops, one kernel) and the full size (20 K ops, the kernel
+    bench.py times at 2^24: segments, csrc/zxp_segment.cpp, their carried
+    values through scratch columns).  The kernels come from the on-disk cache
+    build() fills (tools/jit_prebuild.py; hiprtc takes minutes at this size),
+    as the reference ships its expression code compiled."""
     import torch
     import zkgpu.parser as zp
     import zkgpu.synthetic_bytecode as sb
     monkeypatch.setenv("ZKGPU_ZXP_JIT", "2")
     shape = sb.load_shape()
-    ops, args = sb.generate("step42ns", seed=1, scale=0.25)
+    ops, args = sb.generate("step42ns", seed=1, scale=scale)
     secs = sb.sections(shape)
     prog = zp.convert(zp.STEP42NS, ops, args, secs, shape["n_bits"], shape["n_bits_ext"])
     rng = np.random.default_rng(0)
@@ -137,7 +140,11 @@ def test_step42ns_shaped_jit_gpu_equals_oracle(oracle, zkgpu, monkeypatch):
     zkgpu.zxp_eval_dev(prog, dsecs, log_dom, chal, pub, evals, extend_bits=1, x_start=7)
     torch.cuda.synchronize()
     zkgpu.prof_enable(False)
-    assert "k_zxp_jit" in zkgpu.prof_kernels(), "the compiled kernel did not run"
+    ran = [k for k in zkgpu.prof_kernels() if k.startswith("k_zxp_jit")]
+    if scale == 1.0:
+        assert len(ran) > 1 and "k_zxp_jit_s00" in ran, ("the segmented kernels did not run", ran)
+    else:
+        assert ran == ["k_zxp_jit"], ("the compiled kernel did not run", ran)
     got = zkgpu.from_device(q).T
     x = np.zeros(dom, np.uint64)
     oracle.lib().oc_powers(oracle._p(x), 7, oracle.gl_w(log_dom), dom)

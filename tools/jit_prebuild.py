@@ -3,15 +3,20 @@
 csrc/zxp_jit.hip cache_dir) for the compiled expression kernels the GPU tests
 and bench.py run on programs of zkEVM size: the step42ns-shaped synthetic
 program (zkgpu/synthetic_bytecode.py, seed 1) at a quarter of step42ns's
-opcode counts (5.3 K ops, ~80 s of hiprtc), converted like the reference's
-bytecode; --full also compiles the full-size 20 K-op program (~10 min, not
-part of build()).  A program's kernel depends only on its structure, so
-one compile serves every proof (the reference likewise ships its expression
-code compiled, chelpers/*.cpp).  No GPU needed (hiprtc cross-compiles).
+opcode counts (5.3 K ops, one kernel, ~80 s of hiprtc) and at full size
+(20 K ops), converted like the reference's bytecode.  The full-size program
+runs as segments (csrc/zxp_segment.cpp: ~8 kernels, ~30 s of hiprtc each);
+hiprtc serialises threads, so the segments compile in parallel processes
+(ZKGPU_ZXP_JIT_ONLY=j, one per segment).  A program's kernels depend only on
+its structure, so one compile serves every proof (the reference likewise
+ships its expression code compiled, chelpers/*.cpp).  No GPU needed (hiprtc
+cross-compiles).
 
-Usage: tools/jit_prebuild.py [--check] [--full]   (--check: report cache hits only)
+Usage: tools/jit_prebuild.py [--check] [--quarter-only | --full-only] [-j N]
+       (--check: report cache hits only)
 """
 import os
+import subprocess
 import sys
 import time
 
@@ -21,37 +26,60 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "zkevm-prover_amd")]
 import numpy as np  # noqa: E402
 
 P = 0xFFFFFFFF00000001
-JIT_SCALE = 0.25  # tests/test_gpu_parser.py uses the same program
+SCALES = (0.25, 1.0)  # tests/test_gpu_parser.py and bench.py use the same programs
 
 
-def programs(full=False):
+def program(scale):
     import zkgpu.parser as zp
     import zkgpu.synthetic_bytecode as sb
     shape = sb.load_shape()
-    for scale in (JIT_SCALE, 1.0) if full else (JIT_SCALE,):
-        ops, args = sb.generate("step42ns", seed=1, scale=scale)
-        prog = zp.convert(zp.STEP42NS, ops, args, sb.sections(shape), shape["n_bits"], shape["n_bits_ext"])
-        yield "step42ns-shaped (seed 1, scale %g)" % scale, prog
+    ops, args = sb.generate("step42ns", seed=1, scale=scale)
+    return zp.convert(zp.STEP42NS, ops, args, sb.sections(shape), shape["n_bits"], shape["n_bits_ext"])
+
+
+def consts():
+    rng = np.random.default_rng(0)
+    return (rng.integers(0, P, (8, 3), dtype=np.uint64), rng.integers(0, P, 48, dtype=np.uint64),
+            rng.integers(0, P, (2048, 3), dtype=np.uint64))
+
+
+def one(scale, seg):
+    """child: compile segment `seg` of the program at `scale` (cache hit: no-op)"""
+    import zkgpu
+    os.environ["ZKGPU_ZXP_JIT_ONLY"] = str(seg)
+    zkgpu.zxp_jit_source(program(scale), *consts(), rtc_check=1)
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--one":
+        one(float(sys.argv[2]), int(sys.argv[3]))
+        return
     import zkgpu
     check = "--check" in sys.argv
-    rng = np.random.default_rng(0)
-    ch = rng.integers(0, P, (8, 3), dtype=np.uint64)
-    pub = rng.integers(0, P, 48, dtype=np.uint64)
-    ev = rng.integers(0, P, (2048, 3), dtype=np.uint64)
-    for name, prog in programs("--full" in sys.argv):
-        t = time.time()
-        if check:
-            hit = zkgpu.zxp_jit_cached(prog, ch, pub, ev)
+    jobs = int(sys.argv[sys.argv.index("-j") + 1]) if "-j" in sys.argv else min(16, os.cpu_count() or 1)
+    scales = SCALES[:1] if "--quarter-only" in sys.argv else SCALES[1:] if "--full-only" in sys.argv else SCALES
+    for scale in scales:
+        name = "step42ns-shaped (seed 1, scale %g)" % scale
+        prog = program(scale)
+        hit = zkgpu.zxp_jit_cached(prog, *consts())
+        if check or hit:
             print("%s: %s" % (name, "cached" if hit else "NOT cached"))
             continue
-        if zkgpu.zxp_jit_cached(prog, ch, pub, ev):
-            print("%s: cached" % name)
-            continue
-        zkgpu.zxp_jit_source(prog, ch, pub, ev, rtc_check=1)
-        print("%s: compiled in %.1f s" % (name, time.time() - t), flush=True)
+        nseg = max(1, zkgpu.zxp_jit_source(prog, *consts()).count("// ---- segment "))
+        t = time.time()
+        pending = list(range(nseg))
+        running = []
+        while pending or running:
+            while pending and len(running) < jobs:
+                j = pending.pop(0)
+                running.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "--one", str(scale),
+                                                 str(j)]))
+            running[0].wait()
+            if running[0].returncode:
+                raise SystemExit("%s: segment compile failed (rc %d)" % (name, running[0].returncode))
+            running.pop(0)
+        assert zkgpu.zxp_jit_cached(prog, *consts()), name
+        print("%s: %d kernel(s) compiled in %.1f s" % (name, nseg, time.time() - t), flush=True)
 
 
 if __name__ == "__main__":

@@ -1017,6 +1017,7 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
         J.ins = pin;
         J.n_instr = n_instr;
         J.opnd = opv.data();
+        J.n_opnd = (uint32_t)opv.size();
         J.terms = terms;
         J.csts = csts;
         J.n_tmp1 = n_tmp1;
@@ -1038,6 +1039,9 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
         const char *env_waves = getenv("ZKGPU_ZXP_JIT_WAVES");
         J.dot_loop_min = env_loop ? (uint32_t)atoi(env_loop) : 8u;
         J.waves_per_eu = env_waves ? (uint32_t)atoi(env_waves) : 0u;
+        J.force_split = 0;
+        J.scratch = nullptr;
+        J.scratch_ld = 0;
         rc = zxp_jit_run(J, s);
         if (rc <= 0) return rc;  // launched, or an error
         // 1 = shape unsupported: compile for the interpreter instead

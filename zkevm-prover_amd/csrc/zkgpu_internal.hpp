@@ -32,7 +32,7 @@ struct Ctx {
     uint64_t *post_lo = nullptr;
     uint64_t *post_hi = nullptr;
     // scratch workspaces
-    Workspace ws[6];  // 0-3 NTT / staging, 4 H1H2 scratch, 5 rocPRIM temp
+    Workspace ws[7];  // 0-3 NTT / staging, 4 H1H2 scratch, 5 rocPRIM temp, 6 ZXP segment carries
     // Poseidon constants on device
     uint64_t *poseidon_rc = nullptr;
 };
@@ -133,6 +133,7 @@ struct ZxpJitIn {
     const zxp_instr *ins;  // compiled program (zkgpu_zxp_compile)
     uint32_t n_instr;
     const zxp_operand *opnd;
+    uint32_t n_opnd;
     const zxp_term *terms;
     const uint64_t *csts;
     uint32_t n_tmp1, n_tmp3;
@@ -147,6 +148,9 @@ struct ZxpJitIn {
     double bytes;
     uint32_t dot_loop_min;  // DOTs with at least this many column terms loop over a table
     uint32_t waves_per_eu;  // occupancy hint for the compiler (0: none)
+    uint32_t force_split;   // code blocks / limb chunks even below the size threshold (segments)
+    const uint64_t *scratch;  // columns of section ZXP_SEC_SCRATCH (segments, csrc/zxp_segment.hpp)
+    uint64_t scratch_ld;
 };
 // 0 launched, 1 shape unsupported (run the interpreter), < 0 error
 int zxp_jit_run(const ZxpJitIn &in, hipStream_t s);

@@ -33,6 +33,12 @@
 #include <vector>
 
 #include "zkgpu_internal.hpp"
+#include "zxp_segment.hpp"
+
+#include <algorithm>
+#include <atomic>
+#include <functional>
+#include <thread>
 
 namespace zk {
 
@@ -145,24 +151,35 @@ extern "C" __global__ void __launch_bounds__(256) ZKJIT_WAVES zxp_jit(const JitP
 #if ZKJIT_KL_LDS
     __syncthreads();
 #endif
+    // ZKJIT_ROWS rows per thread: i_r = ib_ + r * S_ (each row set is
+    // contiguous over the lanes, so every column load stays coalesced)
+    const uint64_t S_ = (1ULL << p.logdom) / ZKJIT_ROWS;
 #if ZKJIT_KL_CHUNK
     // limb chunks staged in LDS per code block (workgroup barriers: every
     // thread stays to the end, rows past the domain only skip the stores)
     const uint64_t i_ = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const bool live_ = i_ < (1ULL << p.logdom);
-    const uint64_t i = live_ ? i_ : 0;
+    const bool live_ = i_ < S_;
+    const uint64_t ib_ = live_ ? i_ : 0;
     __shared__ __attribute__((aligned(16))) uint32_t kbuf[2 * ZKJIT_KL_CHUNK];
     kput(kbuf, kpre(p.kl, 0));
     __syncthreads();
 #else
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (1ULL << p.logdom)) return;
+    const uint64_t ib_ = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (ib_ >= S_) return;
 #endif
     const uint64_t m = p.rmask;
 #ifdef ZK_CP_AS
-#define C(j, sh) gload((const uint64_t *)(((const ZK_CP_AS uint64_t *)p.cp)[j]) + ((i + (uint64_t)(sh)) & m))
+#define CPTR(j) ((uint64_t *)(((const ZK_CP_AS uint64_t *)p.cp)[j]))
 #else
-#define C(j, sh) gload(p.cp[j] + ((i + (uint64_t)(sh)) & m))
+#define CPTR(j) (const_cast<uint64_t *>(p.cp[j]))
+#endif
+#define C(j, sh, ii) gload(CPTR(j) + ((ii + (uint64_t)(sh)) & m))
+// scratch columns of a segmented program (csrc/zxp_segment.hpp) are stored
+// where the value is defined, not deferred to the end of the row
+#if ZKJIT_KL_CHUNK
+#define ZK_ST(j, v, ii) do { if (live_) gstore(CPTR(j) + ii, gl_canon(v)); } while (0)
+#else
+#define ZK_ST(j, v, ii) gstore(CPTR(j) + ii, gl_canon(v))
 #endif
 // a global limb table is re-based in every code block (an opaque copy of K):
 // with thousands of loads off one base register, SIFoldOperands dominated
@@ -399,16 +416,65 @@ static bool jit_kl_lds(size_t nkl)
     return mode == 2 || nkl >= JIT_KL_LDS_MIN;
 }
 
+// Rows per thread of a compiled kernel (ZKGPU_ZXP_JIT_ROWS 1 / 2 / 4): large
+// programs evaluate 2 rows per thread, so each wave-uniform limb read from
+// LDS, column pointer and instruction serves 128 rows and two independent
+// chains hide each other's load latency; small programs keep one.
+static uint32_t jit_rows(bool large)
+{
+    static const int env = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_ROWS");
+        return e ? atoi(e) : 0;
+    }();
+    if (env == 1 || env == 2 || env == 4) return (uint32_t)env;
+    return large ? 2 : 1;
+}
+
+// every line holding a ` is written once per row r (` -> _r, ~ -> r)
+static std::string expand_rows(const std::string &text, uint32_t rows)
+{
+    std::string out;
+    out.reserve(text.size() * rows);
+    size_t pos = 0;
+    while (pos < text.size()) {
+        size_t eol = text.find('\n', pos);
+        if (eol == std::string::npos) eol = text.size() - 1;
+        const size_t len = eol + 1 - pos;
+        if (memchr(text.data() + pos, '`', len) == nullptr) {
+            out.append(text, pos, len);
+        } else {
+            for (uint32_t r = 0; r < rows; r++)
+                for (size_t k = pos; k <= eol; k++) {
+                    const char ch = text[k];
+                    if (ch == '`') {
+                        out += '_';
+                        out += (char)('0' + r);
+                    } else if (ch == '~') {
+                        out += (char)('0' + r);
+                    } else {
+                        out += ch;
+                    }
+                }
+        }
+        pos = eol + 1;
+    }
+    return out;
+}
+
 int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const uint64_t *> &cp,
                          std::vector<uint64_t> &kc, std::vector<uint32_t> &kl, std::vector<JitTerm> &zt)
 {
     const zkgpu_sections *S = in.sections;
+    auto col_ptr = [&](uint32_t sec, uint32_t col) -> const uint64_t * {
+        if (sec == ZXP_SEC_SCRATCH) return in.scratch + (uint64_t)col * in.scratch_ld;
+        return S->sec[sec] + (uint64_t)col * S->ld[sec];
+    };
     std::map<std::pair<uint32_t, uint32_t>, uint32_t> slot;  // (section, col) -> cp slot
     auto col_slot = [&](uint32_t sec, uint32_t col) {
         auto key = std::make_pair(sec, col);
         auto it = slot.find(key);
         if (it != slot.end()) return it->second;
-        cp.push_back(S->sec[sec] + (uint64_t)col * S->ld[sec]);
+        cp.push_back(col_ptr(sec, col));
         return slot[key] = (uint32_t)cp.size() - 1;
     };
     // cells written by the program: (column slot, row shift) -> register w<r>;
@@ -418,7 +484,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     std::vector<uint8_t> written_any;                  // per slot, at any shift
     for (uint32_t k = 0; k < in.n_instr; k++) {
         const zxp_operand &d = in.opnd[in.ins[k].dst];
-        if (d.kind == ZXP_COL || d.kind == ZXP_COL3)
+        if ((d.kind == ZXP_COL || d.kind == ZXP_COL3) && d.a != ZXP_SEC_SCRATCH)
             for (uint32_t c = 0; c < (d.kind == ZXP_COL3 ? 3u : 1u); c++) {
                 const uint32_t j = col_slot(d.a, d.b + c);
                 const auto key = std::make_pair(j, (int32_t)d.c);
@@ -437,12 +503,12 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         if (is_written(j)) {
             auto it = wreg.find(std::make_pair(j, sh));
             if (it != wreg.end() && wlive[it->second]) {
-                e = "w" + std::to_string(it->second);
+                e = "w" + std::to_string(it->second) + "`";
                 return 0;
             }
             if (sh != 0) return 1;  // cross-row read of a written column: interpreter
         }
-        e = "C(" + std::to_string(j) + "," + std::to_string(sh) + ")";
+        e = "C(" + std::to_string(j) + "," + std::to_string(sh) + ",i`)";
         return 0;
     };
     auto kconst = [&](const uint64_t *v, int dim) {
@@ -455,8 +521,8 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         const zxp_operand &o = in.opnd[idx];
         char b[160];
         switch (o.kind) {
-        case ZXP_TMP1: x = {"a" + std::to_string(o.a), 1}; return 0;
-        case ZXP_TMP3: x = {"b" + std::to_string(o.a), 3}; return 0;
+        case ZXP_TMP1: x = {"a" + std::to_string(idx) + "`", 1}; return 0;
+        case ZXP_TMP3: x = {"b" + std::to_string(idx) + "`", 3}; return 0;
         case ZXP_COL: x.dim = 1; return col_read(o.a, o.b, (int32_t)o.c, x.e);
         case ZXP_COL3: {
             std::string c0, c1, c2;
@@ -489,10 +555,10 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             x = {b, dim};
             return 0;
         }
-        case ZXP_X: uses_x = true; x = {"xv", 1}; return 0;
-        case ZXP_XDIV: x = {"gl3{{gload(p.xdiv+3*i),gload(p.xdiv+3*i+1),gload(p.xdiv+3*i+2)}}", 3}; return 0;
-        case ZXP_XDIVW: x = {"gl3{{gload(p.xdivw+3*i),gload(p.xdivw+3*i+1),gload(p.xdivw+3*i+2)}}", 3}; return 0;
-        case ZXP_ZI: x = {"gload(p.zh + (i & p.zmask))", 1}; return 0;
+        case ZXP_X: uses_x = true; x = {"xv`", 1}; return 0;
+        case ZXP_XDIV: x = {"gl3{{gload(p.xdiv+3*i`),gload(p.xdiv+3*i`+1),gload(p.xdiv+3*i`+2)}}", 3}; return 0;
+        case ZXP_XDIVW: x = {"gl3{{gload(p.xdivw+3*i`),gload(p.xdivw+3*i`+1),gload(p.xdivw+3*i`+2)}}", 3}; return 0;
+        case ZXP_ZI: x = {"gload(p.zh + (i` & p.zmask))", 1}; return 0;
         default: return 1;
         }
     };
@@ -523,19 +589,31 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     // assignment of a value expression to a destination operand
     auto assign = [&](uint32_t didx, const Expr &r) -> int {
         const zxp_operand &d = in.opnd[didx];
+        if ((d.kind == ZXP_COL || d.kind == ZXP_COL3) && d.a == ZXP_SEC_SCRATCH) {  // carried value: stored at once
+            if (d.c != 0) return 1;
+            if (d.kind == ZXP_COL)
+                appendf(body, "ZK_ST(%u, %s%s, i`);\n", col_slot(d.a, d.b), r.e.c_str(), r.dim == 3 ? ".v[0]" : "");
+            else if (r.dim == 3)
+                appendf(body, "{ const gl3 t_ = %s; ZK_ST(%u, t_.v[0], i`); ZK_ST(%u, t_.v[1], i`); ZK_ST(%u, t_.v[2], i`); }\n",
+                        r.e.c_str(), col_slot(d.a, d.b), col_slot(d.a, d.b + 1), col_slot(d.a, d.b + 2));
+            else
+                appendf(body, "ZK_ST(%u, %s, i`); ZK_ST(%u, 0, i`); ZK_ST(%u, 0, i`);\n", col_slot(d.a, d.b), r.e.c_str(),
+                        col_slot(d.a, d.b + 1), col_slot(d.a, d.b + 2));
+            return 0;
+        }
         switch (d.kind) {
         case ZXP_TMP1:
-            appendf(body, "a%u = %s%s;\n", d.a, r.e.c_str(), r.dim == 3 ? ".v[0]" : "");
+            appendf(body, "a%u` = %s%s;\n", didx, r.e.c_str(), r.dim == 3 ? ".v[0]" : "");
             return 0;
         case ZXP_TMP3:
             if (r.dim == 3)
-                appendf(body, "b%u = %s;\n", d.a, r.e.c_str());
+                appendf(body, "b%u` = %s;\n", didx, r.e.c_str());
             else
-                appendf(body, "b%u = gl3{{%s, 0, 0}};\n", d.a, r.e.c_str());
+                appendf(body, "b%u` = gl3{{%s, 0, 0}};\n", didx, r.e.c_str());
             return 0;
         case ZXP_COL: {
             const uint32_t j = wreg.at(std::make_pair(col_slot(d.a, d.b), (int32_t)d.c));
-            appendf(body, "w%u = %s%s;\n", j, r.e.c_str(), r.dim == 3 ? ".v[0]" : "");
+            appendf(body, "w%u` = %s%s;\n", j, r.e.c_str(), r.dim == 3 ? ".v[0]" : "");
             wlive[j] = 1;
             return 0;
         }
@@ -543,10 +621,10 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             uint32_t j[3];
             for (int c = 0; c < 3; c++) j[c] = wreg.at(std::make_pair(col_slot(d.a, d.b + c), (int32_t)d.c));
             if (r.dim == 3)
-                appendf(body, "{ const gl3 t_ = %s; w%u = t_.v[0]; w%u = t_.v[1]; w%u = t_.v[2]; }\n", r.e.c_str(),
+                appendf(body, "{ const gl3 t_ = %s; w%u` = t_.v[0]; w%u` = t_.v[1]; w%u` = t_.v[2]; }\n", r.e.c_str(),
                         j[0], j[1], j[2]);
             else
-                appendf(body, "w%u = %s; w%u = 0; w%u = 0;\n", j[0], r.e.c_str(), j[1], j[2]);
+                appendf(body, "w%u` = %s; w%u` = 0; w%u` = 0;\n", j[0], r.e.c_str(), j[1], j[2]);
             for (int c = 0; c < 3; c++) wlive[j[c]] = 1;
             return 0;
         }
@@ -584,6 +662,25 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             if (in.ins[k].op == ZXP_DOT1 || in.ins[k].op == ZXP_DOT3) nt = std::max(nt, in.ins[k].a + in.ins[k].b);
         streamed_term.assign(nt, 0);
     }
+    // Large programs (block-split, below) choose per DOT where to open its
+    // accumulators by a register cost (ZKGPU_ZXP_JIT_STREAM=span: the span
+    // rule above for every program)
+    static const int stream_mode_env = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_STREAM");
+        return e ? (strcmp(e, "span") ? 1 : 0) : 1;
+    }();
+    const bool cost_stream = stream_mode_env && (in.n_instr >= 1000 || in.force_split);
+    std::vector<int64_t> last_read(in.n_opnd ? in.n_opnd : 1, -1);  // per SSA operand
+    for (uint32_t k = 0; k < in.n_instr; k++) {
+        const zxp_instr &I = in.ins[k];
+        if (I.op == ZXP_DOT1 || I.op == ZXP_DOT3) {
+            for (uint32_t t = I.a; t < I.a + I.b; t++)
+                if (in.terms[t].src != ZXP_TERM_ONE && in.terms[t].src < last_read.size()) last_read[in.terms[t].src] = k;
+        } else {
+            if (I.a < last_read.size()) last_read[I.a] = k;
+            if (I.op != ZXP_COPY && I.b < last_read.size()) last_read[I.b] = k;
+        }
+    }
     std::vector<size_t> dot_k0(in.n_instr, 0);
     std::vector<uint32_t> first_use(in.n_instr, UINT32_MAX);  // declaration point of DOT k's accumulators
     {
@@ -604,6 +701,38 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                 dot_k0[k] = kl.size();
                 for (int j = 0; j < 3; j++) limbs3(c0[j]);
                 first_use[k] = k;
+                // cost mode: open the accumulators (A VGPRs) at the definition
+                // d_j that minimises A (k - d_j) + sum over the earlier-defined
+                // sources w_i (k - d_i) (those wait in registers); only sources
+                // whose last read is this DOT count (others stay live anyway)
+                int64_t d_open = INT64_MIN;
+                if (cost_stream) {
+                    std::vector<std::pair<int64_t, int64_t>> cand;  // (definition, VGPRs freed)
+                    for (uint32_t t = I.a; t < I.a + I.b; t++) {
+                        const zxp_term &tm = in.terms[t];
+                        if (tm.src == ZXP_TERM_ONE) continue;
+                        const zxp_operand &o = in.opnd[tm.src];
+                        if (o.kind != ZXP_TMP1 && o.kind != ZXP_TMP3) continue;
+                        const int64_t d = o.kind == ZXP_TMP1 ? last1[o.a] : last3[o.a];
+                        if (d < 0 || last_read[tm.src] != (int64_t)k) continue;
+                        cand.push_back({d, 2});  // per term: a base value or one component of an F_p^3 temporary
+                    }
+                    std::sort(cand.begin(), cand.end());
+                    const int64_t A = three ? 18 : 6;
+                    int64_t wait = 0;  // sum w_i (k - d_i) over the sources before j
+                    for (const auto &c : cand) wait += c.second * ((int64_t)k - c.first);
+                    int64_t best = wait;  // no streaming
+                    int64_t acc = 0;
+                    for (size_t j = 0; j < cand.size(); j++) {
+                        const int64_t c = A * ((int64_t)k - cand[j].first) + acc;
+                        if (c < best) {
+                            best = c;
+                            d_open = cand[j].first;
+                        }
+                        acc += cand[j].second * ((int64_t)k - cand[j].first);
+                    }
+                    if (d_open == INT64_MIN) d_open = INT64_MAX;
+                }
                 for (uint32_t t = I.a; t < I.a + I.b; t++) {
                     const zxp_term &tm = in.terms[t];
                     if (tm.src == ZXP_TERM_ONE) continue;
@@ -611,13 +740,14 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                     if (o.kind != ZXP_TMP1 && o.kind != ZXP_TMP3) continue;
                     const int64_t d = o.kind == ZXP_TMP1 ? last1[o.a] : last3[o.a];
                     if (d < 0) continue;  // never written: the value is 0
-                    if ((int64_t)k - d > stream_span) continue;  // read at the DOT instead
+                    if (cost_stream ? (d < d_open || last_read[tm.src] != (int64_t)k) : (int64_t)k - d > stream_span)
+                        continue;  // read at the DOT instead
                     streamed_term[t] = 1;
                     Stream st;
                     st.dot = k;
                     st.three = three;
-                    st.val = o.kind == ZXP_TMP1 ? "a" + std::to_string(o.a)
-                                                : "b" + std::to_string(o.a) + ".v[" + std::to_string(tm.comp) + "]";
+                    st.val = o.kind == ZXP_TMP1 ? "a" + std::to_string(tm.src) + "`"
+                                                : "b" + std::to_string(tm.src) + "`.v[" + std::to_string(tm.comp) + "]";
                     st.kt = limbs6x3(tm.coef);
                     stream[d].push_back(st);
                     first_use[k] = std::min<uint32_t>(first_use[k], (uint32_t)d);
@@ -654,7 +784,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         const char *e = getenv("ZKGPU_ZXP_JIT_SPLIT_MIN");
         return (uint32_t)(e ? atol(e) : 1000);
     }();
-    const bool split = in.n_instr >= split_min;
+    const bool split = in.n_instr >= split_min || in.force_split;
     // Limb chunks in LDS (ZKGPU_ZXP_JIT_KCHUNK): a split program whose limb
     // table is too large for LDS reads it from global memory, one wave-uniform
     // 16 + 8-byte vector load pair per term, each taking the texture
@@ -687,13 +817,13 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         for (uint32_t k : declare_at[at]) {
             const size_t k0 = dot_k0[k];
             if (in.ins[k].op == ZXP_DOT3) {
-                appendf(dot_decls, "Dot3 D%u_0, D%u_1, D%u_2;\n", k, k, k);
+                appendf(dot_decls, "Dot3 D%u_0`, D%u_1`, D%u_2`;\n", k, k, k);
                 const size_t m0 = kmap(k0, 12);
-                appendf(body, "D%u_0 = Dot3(K + %zu); D%u_1 = Dot3(K + %zu); D%u_2 = Dot3(K + %zu);\n", k, m0, k,
+                appendf(body, "D%u_0` = Dot3(K + %zu); D%u_1` = Dot3(K + %zu); D%u_2` = Dot3(K + %zu);\n", k, m0, k,
                         m0 + 4, k, m0 + 8);
             } else {
-                appendf(dot_decls, "Dot3 D%u_0;\n", k);
-                appendf(body, "D%u_0 = Dot3(K + %zu);\n", k, kmap(k0, 4));
+                appendf(dot_decls, "Dot3 D%u_0`;\n", k);
+                appendf(body, "D%u_0` = Dot3(K + %zu);\n", k, kmap(k0, 4));
             }
         }
     };
@@ -738,11 +868,11 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             const size_t kt = kmap(st.kt, st.three ? 24 : 8);
             if (st.three)
                 appendf(body,
-                        "{ const uint64_t v_ = %s; D%u_0.term_al(v_, K + %zu); D%u_1.term_al(v_, K + %zu); "
-                        "D%u_2.term_al(v_, K + %zu); }\n",
+                        "{ const uint64_t v_ = %s; D%u_0`.term_al(v_, K + %zu); D%u_1`.term_al(v_, K + %zu); "
+                        "D%u_2`.term_al(v_, K + %zu); }\n",
                         st.val.c_str(), st.dot, kt, st.dot, kt + 8, st.dot, kt + 16);
             else
-                appendf(body, "D%u_0.term_al(%s, K + %zu);\n", st.dot, st.val.c_str(), kt);
+                appendf(body, "D%u_0`.term_al(%s, K + %zu);\n", st.dot, st.val.c_str(), kt);
         }
     };
     for (uint32_t k = 0; k < in.n_instr; k++) {
@@ -772,15 +902,15 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                     if (is_written(col_slot(o.a, o.b)) && o.c != 0) return 1;
                     JitTerm jt;
                     memset(&jt, 0, sizeof(jt));
-                    jt.ptr = S->sec[o.a] + (uint64_t)o.b * S->ld[o.a];
+                    jt.ptr = col_ptr(o.a, o.b);
                     jt.sh = (int64_t)(int32_t)o.c;
                     for (int j = 0; j < 3; j++) zxp_limbs6(tm.coef[j] % 0xFFFFFFFF00000001ULL, jt.c[j]);
                     zt.push_back(jt);
                 }
                 if (three)
-                    appendf(body, "dot_cols<3>(D%u_0, D%u_1, D%u_2, ZT + %zu, %u, i, m);\n", k, k, k, t0, n_mem);
+                    appendf(body, "dot_cols<3>(D%u_0`, D%u_1`, D%u_2`, ZT + %zu, %u, i`, m);\n", k, k, k, t0, n_mem);
                 else
-                    appendf(body, "dot_cols<1>(D%u_0, D%u_0, D%u_0, ZT + %zu, %u, i, m);\n", k, k, k, t0, n_mem);
+                    appendf(body, "dot_cols<1>(D%u_0`, D%u_0`, D%u_0`, ZT + %zu, %u, i`, m);\n", k, k, k, t0, n_mem);
             }
             for (uint32_t t = I.a; t < I.a + I.b; t++) {
                 const zxp_term &tm = in.terms[t];
@@ -791,16 +921,16 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                     if (streamed_term[t]) continue;  // accumulated at the temporary's definition
                     maybe_split();
                     const std::string v = o.kind == ZXP_TMP1
-                                              ? "a" + std::to_string(o.a)
-                                              : "b" + std::to_string(o.a) + ".v[" + std::to_string(tm.comp) + "]";
+                                              ? "a" + std::to_string(tm.src) + "`"
+                                              : "b" + std::to_string(tm.src) + "`.v[" + std::to_string(tm.comp) + "]";
                     const size_t kt = kmap(limbs6x3(tm.coef), three ? 24 : 8);
                     if (three)
                         appendf(body,
-                                "{ const uint64_t v_ = %s; D%u_0.term_al(v_, K + %zu); D%u_1.term_al(v_, K + %zu); "
-                                "D%u_2.term_al(v_, K + %zu); }\n",
+                                "{ const uint64_t v_ = %s; D%u_0`.term_al(v_, K + %zu); D%u_1`.term_al(v_, K + %zu); "
+                                "D%u_2`.term_al(v_, K + %zu); }\n",
                                 v.c_str(), k, kt, k, kt + 8, k, kt + 16);
                     else
-                        appendf(body, "D%u_0.term_al(%s, K + %zu);\n", k, v.c_str(), kt);
+                        appendf(body, "D%u_0`.term_al(%s, K + %zu);\n", k, v.c_str(), kt);
                     continue;
                 }
                 if (loop && memcol(tm)) continue;
@@ -810,17 +940,17 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                 const size_t kt = kmap(limbs6x3(tm.coef), three ? 24 : 8);
                 if (three)
                     appendf(body,
-                            "{ const uint64_t v_ = %s; D%u_0.term_al(v_, K + %zu); D%u_1.term_al(v_, K + %zu); "
-                            "D%u_2.term_al(v_, K + %zu); }\n",
+                            "{ const uint64_t v_ = %s; D%u_0`.term_al(v_, K + %zu); D%u_1`.term_al(v_, K + %zu); "
+                            "D%u_2`.term_al(v_, K + %zu); }\n",
                             e.c_str(), k, kt, k, kt + 8, k, kt + 16);
                 else
-                    appendf(body, "D%u_0.term_al(%s, K + %zu);\n", k, e.c_str(), kt);
+                    appendf(body, "D%u_0`.term_al(%s, K + %zu);\n", k, e.c_str(), kt);
             }
             char fin[128];
             if (three)
-                snprintf(fin, sizeof(fin), "gl3{{D%u_0.fin(), D%u_1.fin(), D%u_2.fin()}}", k, k, k);
+                snprintf(fin, sizeof(fin), "gl3{{D%u_0`.fin(), D%u_1`.fin(), D%u_2`.fin()}}", k, k, k);
             else
-                snprintf(fin, sizeof(fin), "D%u_0.fin()", k);
+                snprintf(fin, sizeof(fin), "D%u_0`.fin()", k);
             if (assign(I.dst, Expr{fin, three ? 3 : 1})) return 1;
             emit_streams(k);
             continue;
@@ -935,41 +1065,284 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         appendf(src, "#define ZKJIT_WAVES __attribute__((amdgpu_waves_per_eu(%u)))\n", in.waves_per_eu);
     else
         src += "#define ZKJIT_WAVES\n";
+    const uint32_t rows = jit_rows(split);
+    appendf(src, "#define ZKJIT_ROWS %u\n", rows);
     src += k_kernel_head;
-    for (uint32_t s = 0; s < in.n_tmp1; s++) appendf(src, "uint64_t a%u = 0;\n", s);
-    for (uint32_t s = 0; s < in.n_tmp3; s++) appendf(src, "gl3 b%u = gl3{{0, 0, 0}};\n", s);
-    for (uint32_t r = 0; r < wcell.size(); r++) appendf(src, "uint64_t w%u = 0;\n", r);
+    // per-row text carries a ` (-> _r) and ~ (-> r) on its line; expand()
+    // writes such a line once per row
+    std::string decl = "const uint64_t i` = ib_ + ~ * S_;\n", tail;
+    // Temporaries are named by SSA value (operand index), not by slot: the
+    // code blocks sit behind branches the compiler cannot resolve, so a slot
+    // variable reused through the program would keep every dead value it
+    // held alive up to the slot's last read (the not-taken paths), i.e. all
+    // slots live everywhere (~250 VGPRs on the zkEVM-sized quotient)
+    {
+        std::vector<uint8_t> seen(in.n_opnd, 0);
+        for (uint32_t k = 0; k < in.n_instr; k++) {
+            const uint32_t d = in.ins[k].dst;
+            if (d >= in.n_opnd || seen[d]) continue;
+            seen[d] = 1;
+            if (in.opnd[d].kind == ZXP_TMP1) appendf(decl, "uint64_t a%u`;\n", d);
+            if (in.opnd[d].kind == ZXP_TMP3) appendf(decl, "gl3 b%u`;\n", d);
+        }
+    }
+    for (uint32_t r = 0; r < wcell.size(); r++) appendf(decl, "uint64_t w%u` = 0;\n", r);
     if (uses_x)
-        appendf(src, "const uint64_t ex_ = i << (%u - p.logomega);\n"
-                     "const uint64_t xv = gl_mul(p.x_start, gl_mul(gload(p.tw_lo + (ex_ & %lluULL)), gload(p.tw_hi + (ex_ >> %u))));\n",
+        appendf(decl, "const uint64_t ex_` = i` << (%u - p.logomega);\n"
+                     "const uint64_t xv` = gl_mul(p.x_start, gl_mul(gload(p.tw_lo + (ex_` & %lluULL)), gload(p.tw_hi + (ex_` >> %u))));\n",
                 TW_MAX_LOG, (unsigned long long)(TW_LEVEL_SIZE - 1), TW_LEVEL_BITS);
-    src += dot_decls;
-    src += body;
-    src += "}\n";
-    if (kchunk) src += "if (live_) {\n";
     for (uint32_t r = 0; r < wcell.size(); r++) {
         if (wcell[r].second == 0)
-            appendf(src, "gstore(const_cast<uint64_t *>(p.cp[%u]) + i, gl_canon(w%u));\n", wcell[r].first, r);
+            appendf(tail, "gstore(const_cast<uint64_t *>(p.cp[%u]) + i`, gl_canon(w%u`));\n", wcell[r].first, r);
         else
-            appendf(src, "gstore(const_cast<uint64_t *>(p.cp[%u]) + ((i + (uint64_t)(%d)) & m), gl_canon(w%u));\n",
+            appendf(tail, "gstore(const_cast<uint64_t *>(p.cp[%u]) + ((i` + (uint64_t)(%d)) & m), gl_canon(w%u`));\n",
                     wcell[r].first, wcell[r].second, r);
     }
+    src += expand_rows(decl, rows);
+    src += expand_rows(dot_decls, rows);
+    src += expand_rows(body, rows);
+    src += "}\n";
+    if (kchunk) src += "if (live_) {\n";
+    src += expand_rows(tail, rows);
     if (kchunk) src += "}\n";
     src += "#undef C\n}\n";
     return 0;
 }
 
-int zxp_jit_run(const ZxpJitIn &in, hipStream_t s)
-{
+namespace {
+
+// one kernel ready to launch: source, tables, compiled function
+struct JitKernel {
     std::string src;
     std::vector<const uint64_t *> cp;
     std::vector<uint64_t> kc;
     std::vector<uint32_t> kl;
     std::vector<JitTerm> zt;
-    int rc = zxp_jit_build_source(in, src, cp, kc, kl, zt);
+    hipFunction_t fn = nullptr;
+    size_t off = 0, off_cp = 0, off_kc = 0, off_kl = 0, end = 0;  // table layout in the launch buffer
+    bool klds = false;
+    uint32_t rows = 1;  // rows per thread (ZKJIT_ROWS)
+    double bytes = 0;
+};
+
+int prepare(const ZxpJitIn &in, JitKernel &K)
+{
+    K.cp.clear();
+    K.kc.clear();
+    K.kl.clear();
+    K.zt.clear();
+    const int rc = zxp_jit_build_source(in, K.src, K.cp, K.kc, K.kl, K.zt);
+    const size_t at = K.src.find("#define ZKJIT_ROWS ");
+    K.rows = at == std::string::npos ? 1 : (uint32_t)atoi(K.src.c_str() + at + 19);
+    return rc;
+}
+
+// code objects of several sources (disk cache or hiprtc), compiled in
+// parallel threads: the segments of a large program are independent
+void objects_parallel(const std::vector<const std::string *> &srcs, std::vector<std::vector<char>> &code,
+                      std::vector<int> &rcs)
+{
+    code.assign(srcs.size(), {});
+    rcs.assign(srcs.size(), 0);
+    static const unsigned nthr = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_THREADS");
+        const unsigned hc = std::max(1u, std::thread::hardware_concurrency());
+        return e && atoi(e) > 0 ? (unsigned)atoi(e) : std::min(16u, hc);
+    }();
+    std::vector<std::thread> th;
+    std::atomic<size_t> next{0};
+    auto work = [&] {
+        for (size_t j; (j = next++) < srcs.size();) rcs[j] = code_object(*srcs[j], code[j]);
+    };
+    const unsigned n = std::min<unsigned>(nthr, (unsigned)srcs.size());
+    for (unsigned t = 1; t < n; t++) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+}
+
+// code objects of several kernels: the ones not in this process's cache are
+// found on disk or compiled by hiprtc, in parallel (the segments of a large
+// program compile independently), then loaded
+int compile_all(std::vector<JitKernel *> ks)
+{
+    Cache &c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    std::vector<JitKernel *> todo;
+    for (JitKernel *k : ks) {
+        auto it = c.fn.find(k->src);
+        if (it != c.fn.end())
+            k->fn = it->second;
+        else if (std::find_if(todo.begin(), todo.end(), [&](JitKernel *t) { return t->src == k->src; }) == todo.end())
+            todo.push_back(k);
+    }
+    std::vector<const std::string *> srcs;
+    for (JitKernel *k : todo) srcs.push_back(&k->src);
+    std::vector<std::vector<char>> code;
+    std::vector<int> rcs;
+    objects_parallel(srcs, code, rcs);
+    for (size_t j = 0; j < todo.size(); j++) {
+        int rc;
+        if (rcs[j]) return rcs[j];
+        hipModule_t mod;
+        if ((rc = check_hip(hipModuleLoadData(&mod, code[j].data()), "zxp jit: hipModuleLoadData"))) return rc;
+        hipFunction_t f;
+        if ((rc = check_hip(hipModuleGetFunction(&f, mod, "zxp_jit"), "zxp jit: hipModuleGetFunction"))) return rc;
+        c.fn.emplace(todo[j]->src, f);
+    }
+    for (JitKernel *k : ks) k->fn = c.fn.at(k->src);
+    return 0;
+}
+
+// tables of every kernel in one buffer (zt | cp | kc | kl per kernel), one
+// upload, then the launches in order on stream s
+int launch_all(std::vector<JitKernel> &ks, const ZxpJitIn &in, hipStream_t s)
+{
+    size_t total = 0;
+    for (JitKernel &K : ks) {
+        K.off = total;
+        K.off_cp = K.off + K.zt.size() * sizeof(JitTerm);
+        K.off_kc = K.off_cp + K.cp.size() * 8;
+        K.off_kl = (K.off_kc + (K.kc.size() + 1) * 8 + 15) & ~(size_t)15;  // 16-byte limb slots
+        K.end = K.off_kl + (K.kl.size() + 1) * 4;
+        total = (K.end + 15) & ~(size_t)15;
+        K.klds = jit_kl_lds(K.kl.size()) && K.src.find("#define ZKJIT_KL_CHUNK 0") != std::string::npos;
+    }
+    char *buf = jit_buf(total);
+    if (!buf) return set_error(ZKGPU_ERR_OOM, "zxp jit: table buffer");
+    std::vector<char> h(total, 0);
+    for (JitKernel &K : ks) {
+        memcpy(h.data() + K.off, K.zt.data(), K.zt.size() * sizeof(JitTerm));
+        memcpy(h.data() + K.off_cp, K.cp.data(), K.cp.size() * 8);
+        memcpy(h.data() + K.off_kc, K.kc.data(), K.kc.size() * 8);
+        memcpy(h.data() + K.off_kl, K.kl.data(), K.kl.size() * 4);
+    }
+    int rc;
+    if ((rc = check_hip(hipMemcpyAsync(buf, h.data(), total, hipMemcpyHostToDevice, s), "zxp jit: H2D"))) return rc;
+    if ((rc = check_hip(hipStreamSynchronize(s), "zxp jit: table upload"))) return rc;  // pageable source
+    Ctx &c = ctx();
+    const uint64_t dom = 1ULL << in.log_dom;
+    for (JitKernel &K : ks)
+        if (dom < K.rows) return set_error(ZKGPU_ERR_ARG, "zxp jit: 2^%u rows < %u rows per thread", in.log_dom, K.rows);
+    for (size_t j = 0; j < ks.size(); j++) {
+        JitKernel &K = ks[j];
+        JitParams p;
+        p.zt = (const JitTerm *)(buf + K.off);
+        p.cp = (const uint64_t *const *)(buf + K.off_cp);
+        p.kc = (const uint64_t *)(buf + K.off_kc);
+        p.kl = (const uint32_t *)(buf + K.off_kl);
+        p.xdiv = in.xdiv;
+        p.xdivw = in.xdivw;
+        p.zh = in.zh_dev;
+        p.tw_lo = c.tw_lo[0];
+        p.tw_hi = c.tw_hi[0];
+        p.x_start = in.x_start;
+        p.logdom = in.log_dom;
+        p.logomega = in.log_omega;
+        p.rmask = in.wrap ? dom - 1 : ~0ULL;
+        p.zmask = in.zmask;
+        p.nkl = K.klds ? (uint32_t)K.kl.size() : 0;
+        p.one = 1;
+        void *args[] = {&p};
+        prof_begin(s);
+        rc = check_hip(hipModuleLaunchKernel(K.fn, (uint32_t)((dom / K.rows + JIT_THREADS - 1) / JIT_THREADS), 1, 1,
+                                             JIT_THREADS, 1, 1, K.klds ? (uint32_t)(K.kl.size() * 4) : 0, s, args,
+                                             nullptr),
+                       "zxp jit: launch");
+        char name[32];
+        if (ks.size() > 1)
+            snprintf(name, sizeof(name), "k_zxp_jit_s%02zu", j);  // one segment of a large program
+        else
+            snprintf(name, sizeof(name), "k_zxp_jit");
+        prof_end(name, K.bytes, s);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+// Segments of a large program (csrc/zxp_segment.hpp).  ZKGPU_ZXP_SEGMENTS:
+// 0 never, n > 0 exactly n (programs of >= 2 * n instructions), unset: one
+// segment per ZKGPU_ZXP_SEG_COST of estimated VALU work for programs of
+// >= ZKGPU_ZXP_SEG_MIN (2,000) compiled instructions.
+uint32_t segments_for(const zxp_compiled &cp)
+{
+    static const int env_n = [] {
+        const char *e = getenv("ZKGPU_ZXP_SEGMENTS");
+        return e ? atoi(e) : -1;
+    }();
+    static const uint64_t seg_cost = [] {
+        const char *e = getenv("ZKGPU_ZXP_SEG_COST");
+        return (uint64_t)(e && atoll(e) > 0 ? atoll(e) : 50000);
+    }();
+    static const uint32_t seg_min = [] {
+        const char *e = getenv("ZKGPU_ZXP_SEG_MIN");
+        return (uint32_t)(e ? atoi(e) : 2000);
+    }();
+    if (env_n == 0) return 1;
+    if (env_n > 0) return cp.n_instr >= 2u * (uint32_t)env_n ? (uint32_t)env_n : 1;
+    if (cp.n_instr < seg_min) return 1;
+    uint64_t cost = 0;
+    for (uint32_t k = 0; k < cp.n_instr; k++) cost += zxp_instr_cost(cp, k);
+    return (uint32_t)std::max<uint64_t>(1, (cost + seg_cost / 2) / seg_cost);
+}
+
+// the kernels of a program: one, or one per segment (scratch(n) returns the
+// carry columns' base for n columns of ld 2^log_dom)
+int build_kernels(const ZxpJitIn &in, std::vector<JitKernel> &ks, const std::function<uint64_t *(uint32_t)> &scratch)
+{
+    zxp_compiled view;
+    memset(&view, 0, sizeof(view));
+    view.instr = in.ins;
+    view.n_instr = in.n_instr;
+    view.opnd = in.opnd;
+    view.n_opnd = in.n_opnd;
+    view.term = in.terms;
+    view.n_tmp1 = in.n_tmp1;
+    view.n_tmp3 = in.n_tmp3;
+    const uint32_t nseg = in.n_opnd ? segments_for(view) : 1;
+    int rc;
+    ks.clear();
+    if (nseg <= 1) {
+        ks.resize(1);
+        ks[0].bytes = in.bytes;
+        return prepare(in, ks[0]);
+    }
+    std::vector<ZxpSegment> seg;
+    uint32_t n_scratch = 0;
+    if ((rc = zxp_segment(view, nseg, seg, n_scratch))) return rc;
+    uint64_t *scr = scratch(std::max<uint32_t>(1, n_scratch));
+    if (!scr) return ZKGPU_ERR_OOM;
+    const uint64_t dom = 1ULL << in.log_dom;
+    ks.resize(seg.size());
+    for (size_t j = 0; j < seg.size(); j++) {
+        ZxpJitIn J = in;
+        J.ins = seg[j].instr.data();
+        J.n_instr = (uint32_t)seg[j].instr.size();
+        J.opnd = seg[j].opnd.data();
+        J.n_opnd = (uint32_t)seg[j].opnd.size();
+        J.terms = seg[j].term.data();
+        J.force_split = 1;
+        J.scratch = scr;
+        J.scratch_ld = dom;
+        if ((rc = prepare(J, ks[j]))) return rc;  // 1: unsupported shape -> interpreter for the whole program
+        ks[j].bytes = in.bytes / seg.size() + 8.0 * (seg[j].carry_in + seg[j].carry_out) * (double)dom;
+    }
+    return 0;
+}
+
+}  // namespace
+
+int zxp_jit_run(const ZxpJitIn &in, hipStream_t s)
+{
+    std::vector<JitKernel> ks;
+    int rc = build_kernels(in, ks, [&](uint32_t n) { return workspace(6, (size_t)n << in.log_dom << 3); });
     if (rc) return rc;
-    hipFunction_t fn;
-    if ((rc = compile(src, &fn))) return rc;
+    if (ks.size() > 1) {
+        std::vector<JitKernel *> pk;
+        for (JitKernel &K : ks) pk.push_back(&K);
+        if ((rc = compile_all(pk))) return rc;
+        return launch_all(ks, in, s);
+    }
+    if ((rc = compile_all({&ks[0]}))) return rc;
     // A kernel the compiler leaves at 169-256 VGPRs runs 2 waves per SIMD and
     // is latency-bound; recompile it with an occupancy target of 3 (<= 168
     // VGPRs).  Config-4 quotient: 186 VGPRs, 15.3 -> 12.7 ms; kernels that
@@ -982,60 +1355,17 @@ int zxp_jit_run(const ZxpJitIn &in, hipStream_t s)
         const char *e = getenv("ZKGPU_ZXP_JIT_AUTOWAVES");
         return !e || atoi(e) != 0;
     }();
-    if (auto_waves && in.waves_per_eu == 0 && src.find("#define ZKJIT_SPLIT 1") == std::string::npos) {
+    if (auto_waves && in.waves_per_eu == 0 && ks[0].src.find("#define ZKJIT_SPLIT 1") == std::string::npos) {
         int regs = 0;
-        if (hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, fn) == hipSuccess && regs > 168 && regs <= 256) {
+        if (hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, ks[0].fn) == hipSuccess && regs > 168 &&
+            regs <= 256) {
             ZxpJitIn in3 = in;
             in3.waves_per_eu = 3;
-            std::string src3;
-            cp.clear();
-            kc.clear();
-            kl.clear();
-            zt.clear();
-            if ((rc = zxp_jit_build_source(in3, src3, cp, kc, kl, zt))) return rc;
-            if ((rc = compile(src3, &fn))) return rc;
+            if ((rc = prepare(in3, ks[0]))) return rc;
+            if ((rc = compile_all({&ks[0]}))) return rc;
         }
     }
-    // tables: zt | cp | kc | kl
-    const size_t off_cp = zt.size() * sizeof(JitTerm), off_kc = off_cp + cp.size() * 8;
-    const size_t off_kl = (off_kc + (kc.size() + 1) * 8 + 15) & ~(size_t)15;  // 16-byte limb slots
-    const size_t total = off_kl + (kl.size() + 1) * 4;
-    char *buf = jit_buf(total);
-    if (!buf) return set_error(ZKGPU_ERR_OOM, "zxp jit: table buffer");
-    std::vector<char> h(total, 0);
-    memcpy(h.data(), zt.data(), zt.size() * sizeof(JitTerm));
-    memcpy(h.data() + off_cp, cp.data(), cp.size() * 8);
-    memcpy(h.data() + off_kc, kc.data(), kc.size() * 8);
-    memcpy(h.data() + off_kl, kl.data(), kl.size() * 4);
-    if ((rc = check_hip(hipMemcpyAsync(buf, h.data(), total, hipMemcpyHostToDevice, s), "zxp jit: H2D"))) return rc;
-    if ((rc = check_hip(hipStreamSynchronize(s), "zxp jit: table upload"))) return rc;  // pageable source
-    Ctx &c = ctx();
-    JitParams p;
-    p.zt = (const JitTerm *)buf;
-    p.cp = (const uint64_t *const *)(buf + off_cp);
-    p.kc = (const uint64_t *)(buf + off_kc);
-    p.kl = (const uint32_t *)(buf + off_kl);
-    p.xdiv = in.xdiv;
-    p.xdivw = in.xdivw;
-    p.zh = in.zh_dev;
-    p.tw_lo = c.tw_lo[0];
-    p.tw_hi = c.tw_hi[0];
-    p.x_start = in.x_start;
-    p.logdom = in.log_dom;
-    p.logomega = in.log_omega;
-    p.rmask = in.wrap ? (1ULL << in.log_dom) - 1 : ~0ULL;
-    p.zmask = in.zmask;
-    const bool klds = jit_kl_lds(kl.size()) && src.find("#define ZKJIT_KL_CHUNK 0") != std::string::npos;
-    p.nkl = klds ? (uint32_t)kl.size() : 0;
-    p.one = 1;
-    void *args[] = {&p};
-    const uint64_t dom = 1ULL << in.log_dom;
-    prof_begin(s);
-    rc = check_hip(hipModuleLaunchKernel(fn, (uint32_t)((dom + JIT_THREADS - 1) / JIT_THREADS), 1, 1, JIT_THREADS, 1,
-                                         1, klds ? (uint32_t)(kl.size() * 4) : 0, s, args, nullptr),
-                   "zxp jit: launch");
-    prof_end("k_zxp_jit", in.bytes, s);
-    return rc;
+    return launch_all(ks, in, s);
 }
 
 }  // namespace zk
@@ -1074,35 +1404,60 @@ extern "C" int zkgpu_zxp_jit_source(const void *instr, uint32_t n_instr, const v
     J.challenges = challenges;
     J.publics = publics;
     J.evals = evals;
-    std::string src;
-    std::vector<const uint64_t *> colp;
-    std::vector<uint64_t> kc;
-    std::vector<uint32_t> kl;
-    std::vector<JitTerm> zt;
+    J.n_opnd = cp.n_opnd;
+    // the same environment overrides as zkgpu_zxp_eval_dev (api.hip), so the
+    // sources (and cache keys) match
     J.dot_loop_min = getenv("ZKGPU_ZXP_JIT_DOTLOOP") ? (uint32_t)atoi(getenv("ZKGPU_ZXP_JIT_DOTLOOP")) : 8;
-    if ((rc = zxp_jit_build_source(J, src, colp, kc, kl, zt))) return rc < 0 ? rc : set_error(ZKGPU_ERR_ARG, "zxp jit: unsupported program shape");
+    J.waves_per_eu = getenv("ZKGPU_ZXP_JIT_WAVES") ? (uint32_t)atoi(getenv("ZKGPU_ZXP_JIT_WAVES")) : 0;
+    std::vector<JitKernel> ks;
+    static uint64_t dummy_scratch;
+    if ((rc = build_kernels(J, ks, [](uint32_t) { return &dummy_scratch; })))
+        return rc < 0 ? rc : set_error(ZKGPU_ERR_ARG, "zxp jit: unsupported program shape");
+    std::string src;  // the kernels' sources (one per segment)
+    for (size_t j = 0; j < ks.size(); j++) {
+        if (ks.size() > 1) appendf(src, "// ---- segment %zu of %zu\n", j, ks.size());
+        src += ks[j].src;
+    }
     if (buf && buflen) {
         const size_t n = std::min<size_t>(src.size(), buflen - 1);
         memcpy(buf, src.data(), n);
         buf[n] = 0;
     }
-    if (rtc_check == 3) {  // cache query only: 1 = compiled object on disk
+    if (rtc_check == 3) {  // cache query only: 1 = every compiled object on disk
         std::vector<char> code;
-        return cache_load(src, code) ? 1 : 0;
+        for (const JitKernel &K : ks)
+            if (!cache_load(K.src, code)) return 0;
+        return 1;
     }
     if (rtc_check) {
         // compile (or find in the disk cache); rtc_check == 2 also writes the
-        // code object to $ZKGPU_ZXP_JIT_DUMP (register / scratch inspection)
-        std::vector<char> code;
-        if ((rc = code_object(src, code))) return rc;
-        const char *dump = getenv("ZKGPU_ZXP_JIT_DUMP");
-        if (rtc_check == 2 && dump) {
-            FILE *f = fopen(dump, "wb");
-            if (f) {
-                fwrite(code.data(), 1, code.size(), f);
-                fclose(f);
+        // code objects to $ZKGPU_ZXP_JIT_DUMP (.<segment> appended when there
+        // are several; register / scratch inspection)
+        // ZKGPU_ZXP_JIT_ONLY=j: only segment j (tools/jit_prebuild.py runs the
+        // segments in parallel processes: hiprtc serialises threads)
+        std::vector<const std::string *> srcs;
+        std::vector<size_t> idx;
+        const char *only = getenv("ZKGPU_ZXP_JIT_ONLY");
+        for (size_t j = 0; j < ks.size(); j++)
+            if (!only || (size_t)atoi(only) == j) {
+                srcs.push_back(&ks[j].src);
+                idx.push_back(j);
             }
-        }
+        std::vector<std::vector<char>> code;
+        std::vector<int> rcs;
+        objects_parallel(srcs, code, rcs);
+        for (int r : rcs)
+            if (r) return r;
+        const char *dump = getenv("ZKGPU_ZXP_JIT_DUMP");
+        if (rtc_check == 2 && dump)
+            for (size_t j = 0; j < code.size(); j++) {
+                const std::string path = ks.size() > 1 ? std::string(dump) + "." + std::to_string(idx[j]) : dump;
+                FILE *f = fopen(path.c_str(), "wb");
+                if (f) {
+                    fwrite(code[j].data(), 1, code[j].size(), f);
+                    fclose(f);
+                }
+            }
     }
     return (int)std::min<size_t>(src.size(), 0x7FFFFFFF);
 }

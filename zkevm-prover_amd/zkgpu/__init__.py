@@ -425,14 +425,19 @@ def zxp_jit_source(prog, challenges, publics, evals=None, rtc_check=False):
     ch[:c.size] = c
     pub = _np(publics if publics is not None else np.zeros(1, np.uint64))
     ev = _np(evals if evals is not None else np.zeros(3, np.uint64)).reshape(-1)
-    buf = ctypes.create_string_buffer(1 << 22)
-    rc = lib().zkgpu_zxp_jit_source(ins.ctypes.data, ins.shape[0], opn.ctypes.data, opn.shape[0],
-                                    max(prog.n_tmp1, 1), max(prog.n_tmp3, 1), ch.ctypes.data, pub.ctypes.data,
-                                    pub.size if publics is not None else 0, ev.ctypes.data, ev.size // 3,
-                                    buf, len(buf), int(rtc_check))
-    if rc < 0:
-        _check(rc, "zkgpu_zxp_jit_source")
-    return buf.value.decode()
+    size = 1 << 22
+    while True:  # the return value is the source length: grow the buffer until it fits
+        buf = ctypes.create_string_buffer(size)
+        rc = lib().zkgpu_zxp_jit_source(ins.ctypes.data, ins.shape[0], opn.ctypes.data, opn.shape[0],
+                                        max(prog.n_tmp1, 1), max(prog.n_tmp3, 1), ch.ctypes.data, pub.ctypes.data,
+                                        pub.size if publics is not None else 0, ev.ctypes.data, ev.size // 3,
+                                        buf, len(buf), int(rtc_check))
+        if rc < 0:
+            _check(rc, "zkgpu_zxp_jit_source")
+        if rc < size:
+            return buf.value.decode()
+        size = rc + 1
+        rtc_check = False  # compiled (or cached) already
 
 
 def zxp_jit_cached(prog, challenges, publics, evals=None):
