@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--s42-scale", type=float, default=1.0,
                     help="step42ns workload: fraction of the reference step42ns opcode counts")
     ap.add_argument("--s42-jit", action="store_true", help="step42ns workload: the compiled kernel (else interpreter)")
+    ap.add_argument("--no-s42", action="store_true",
+                    help="stark workload: skip the zkEVM-shaped quotient block (quotient_zkevm_shaped)")
+    ap.add_argument("--s42-steps", type=int, default=3)
     ap.add_argument("--cpu-sample-bits", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_BITS", "18")))
     ap.add_argument("--cpu-sample-cols", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_COLS", "4")))
     ap.add_argument("--cpu-full", action="store_true",
@@ -212,8 +215,10 @@ def _profile_order(path):
     return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
 
 
-def _newest(pattern):
+def _newest(pattern, load=True):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=_profile_order)
+    if not load:
+        return (files[-1], None) if files else (None, None)
     for f in reversed(files):
         try:
             return f, json.load(open(f))
@@ -418,8 +423,16 @@ def step42ns_setup(args, dev, torch, g):
     # 0.25 is cached by build(), the full-size kernel (~10 min of hiprtc) by
     # tools/jit_prebuild.py --full
     os.environ["ZKGPU_ZXP_JIT"] = "2" if args.s42_jit else "0"
-    return step, {"rows": NE, "log_dom": log_dom, "n_ops": int(len(ops)), "cols_read": cols,
-                  "alg_bytes": 8.0 * NE * (cols + 3), "tensors": dsecs}
+    # the distinct element reads per row -- every (section,
+    # column, row shift) the program reads once -- plus the 3 q columns written
+    ins, opn = prog.arrays()
+    reads = set()
+    for kind, a_, b_, c_ in opn.tolist():
+        if kind in (2, 3):  # ZXP_COL / ZXP_COL3
+            for j in range(3 if kind == 3 else 1):
+                reads.add((a_, b_ + j, c_))
+    return step, {"rows": NE, "log_dom": log_dom, "n_ops": int(len(ops)), "cols_read": len(reads),
+                  "cols_alloc": cols, "alg_bytes": 8.0 * NE * (len(reads) + 3), "tensors": dsecs}
 
 
 def step42ns_roofline(s42, kernels, steps):
@@ -433,8 +446,89 @@ def step42ns_roofline(s42, kernels, steps):
     return {"kernel": ", ".join(sorted(ks)), "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
             "alg_bytes_per_launch": s42["alg_bytes"],
-            "alg_bytes_note": "8 B x rows x (%d section columns read + 3 q columns written)" % s42["cols_read"],
+            "alg_bytes_note": "SURVEY.md 8(d): 8 B x rows x (%d distinct (section, column, row shift) reads + 3 q "
+                              "columns written)" % s42["cols_read"],
             "avg_launch_ms": round(dev_ms, 4)}
+
+
+def leaves_line(inst, args, v):
+    """The dominant kernel of the proof, k_leaves_cols (the Merkle leaf hash
+    of each commit, linear_hash per row, merkleTreeGL.cpp:37-44), on both of
+    its bounds: HBM (8 B x rows x cols + 32 B digest per row)
+    and permutations per second against the isolated permutation benchmark
+    (tools/poseidon_bench.hip, profiles/*_poseidon_bench.txt)."""
+    ne = 1 << (args.log_n + args.blowup_bits)
+    widths = [inst.n_cm1, inst.n_cm2, inst.n_cm3, inst.n_cm4]
+    launches, ms = v[0] / args.steps, v[1] / args.steps  # per proof
+    alg = sum(8.0 * ne * w + 32.0 * ne for w in widths)
+    perms = sum(ne * ((w + 7) // 8) for w in widths)
+    res = {"kernel": "k_leaves_cols", "launches_per_proof": launches, "ms_per_proof": round(ms, 3),
+           "avg_launch_ms": round(ms / launches, 4), "widths": widths, "rows": ne,
+           "alg_bytes_per_proof": alg, "achieved_GBs": round(alg / (ms * 1e-3) / 1e9, 1),
+           "hbm_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "perms_per_proof": perms, "Gperm_s": round(perms / (ms * 1e-3) / 1e9, 3),
+           "bound": "VALU (~20 K VALU per 64 B absorbed; the valu block prices it against the issue peak)"}
+    f, _ = _newest("*_poseidon_bench.txt", load=False)
+    if f:
+        import re
+        m = re.search(r"^fast \(FFT MDS \+ block dots\)\s+[\d.]+ ms\s+([\d.]+) Gperm/s", open(f).read(), re.M)
+        if m:
+            iso = float(m.group(1))
+            res["isolated_Gperm_s"] = iso
+            res["ratio_to_isolated"] = round(res["Gperm_s"] / iso, 3)
+            res["isolated_source"] = os.path.basename(f) + " (the shipped permutation, 8 waves/SIMD at 2.02 GHz; " \
+                "the leaf kernel runs at 2.33 GHz, profiles/r02_clock.json)"
+    return res
+
+
+def quotient_measure(args, dev, torch, world, dist):
+    """The zkEVM-shaped constraint quotient (step42ns, starks.cpp:241) at its
+    real domain, 2^24 rows: the full-size step42ns-shaped program (20 K ops,
+    fork-9 memory map, 1,567 section columns in HBM) through the compiled
+    segment kernels (csrc/zxp_segment.cpp).  Reported beside the config-4
+    proof, whose own quotient is a small synthetic program."""
+    import argparse as _ap
+    import zkgpu
+    a = _ap.Namespace(**vars(args))
+    a.s42_scale, a.s42_jit, a.log_n = 1.0, True, 23
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED)
+    step, s42 = step42ns_setup(a, dev, torch, g)
+    elapsed, kernels = timed(step, args.s42_steps, 1, world, dist, torch)
+    segs = {k: v for k, v in kernels.items() if k.startswith("k_zxp_jit")}
+    dev_ms = sum(v[1] for v in segs.values()) / args.s42_steps
+    roof = step42ns_roofline(s42, kernels, args.s42_steps)
+    res = {"value": round(s42["rows"] * args.s42_steps / elapsed / 1e6, 3), "unit": "Mrow/s",
+           "s_per_pass": round(elapsed / args.s42_steps, 4), "device_ms_per_pass": round(dev_ms, 3),
+           "rows": s42["rows"], "n_ops": s42["n_ops"], "segments": len(segs),
+           "segment_ms": [round(segs[k][1] / segs[k][0], 3) for k in sorted(segs)],
+           "what": "step42ns-shaped synthetic program (zkgpu/synthetic_bytecode.py seed 1, the reference step42ns's "
+                   "opcode histogram / temporaries / fork-9 map, tests/golden/zkevm_bytecode_shape.json) -> product "
+                   "converter -> ZXP compile -> segment kernels; 2^24-row extended domain, sections resident in HBM; "
+                   "parity: tests/test_gpu_parser.py (full size, 2^16 rows, vs the oracle parser)"}
+    f, d = _newest("*_s42_pmc.json")
+    if roof is not None and d and d.get("hbm_bytes_per_step"):
+        roof["traffic"] = d["hbm_bytes_per_step"]
+        roof["traffic_ratio"] = round(d["hbm_bytes_per_step"] / roof["alg_bytes_per_launch"], 2)
+        roof["traffic_source"] = os.path.basename(f)
+        roof["traffic_note"] = ("PMC HBM bytes per pass (2 x FETCH_SIZE + WRITE_SIZE): the program reads %.0f column "
+                                "values per row against %d distinct -- re-reads the registers cannot hold"
+                                % (d["per_step"].get("SQ_INSTS_VMEM_RD", 0) * 64 / s42["rows"], s42["cols_read"]))
+        roof["hbm_frac_measured_traffic"] = round(d["hbm_bytes_per_step"] / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        valu = d["per_step"].get("SQ_INSTS_VALU")
+        if valu:
+            rate = valu / (dev_ms * 1e-3)
+            res["valu"] = {"wave_instr_per_pass": valu, "achieved": round(rate / 1e9, 1), "peak": 978.0,
+                           "unit": "G wave-instr/s", "frac": round(rate / 978e9, 4),
+                           "peak_model": "mix-weighted issue peak of the field-arithmetic kernels (DESIGN.md 3)",
+                           "source": os.path.basename(f)}
+    res["roofline"] = roof
+    for t in s42["tensors"].values():
+        del t
+    s42.clear()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
 
 
 def handoff_measure(n, C, dev, torch, zkgpu, s_per_proof):
@@ -497,7 +591,7 @@ def main():
     C = args.ncols
     res = {"metric": METRIC}
     gs = ss = inst = None
-    lde = roof = handoff = None
+    lde = roof = handoff = quotient = None
     if args.workload == "lde":
         lde, roof = lde_measure(args, dev, torch, world, dist)
         elapsed = lde["ms_per_lde"] * 1e-3 * args.steps
@@ -565,6 +659,11 @@ def main():
             lde, roof = lde_measure(args, dev, torch, world, dist)
         if args.workload == "stark" and world == 1 and not args.no_handoff:
             handoff = handoff_measure(n, C, dev, torch, zkgpu, value)
+        if args.workload == "stark" and world == 1 and args.log_n == 23 and not args.no_s42:
+            gs = None  # the config-4 instance's HBM back before the 200 GB of fork-9-width sections
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            quotient = quotient_measure(args, dev, torch, world, dist)
 
     if rank == 0:
         cpu = None
@@ -641,6 +740,8 @@ def main():
             res["roofline"] = roof
         if handoff is not None:
             res["handoff"] = handoff
+        if quotient is not None:
+            res["quotient_zkevm_shaped"] = quotient
         if kernels is not None:
             res["kernels"] = kernel_table(kernels)
             if args.workload == "stark" and args.log_n == 23 and C == 100:
@@ -650,6 +751,7 @@ def main():
                 if "k_leaves_cols" in kernels:
                     v = kernels["k_leaves_cols"]
                     res["valu"] = stark_valu("k_leaves_cols", v[1] / v[0])
+                    res["leaves"] = leaves_line(inst, args, v)
             if args.workload in ("stark", "stark-sharded") and stages:
                 res["stages_ms"] = {k: round(v, 3) for k, v in stages.items()}
         res["cpu_baseline"] = cpu

@@ -81,8 +81,14 @@ def test_batch_prover_sharded(oracle, tmp_path, world, comm):
     o.witness()
     proof = o.prove()
     cfg = zs.write_inputs(str(tmp_path), inst, o.S[4], o.S[9], o.const_nodes, o.S[0], o.publics)
-    spec = "host:/zkgpu_t_%s" % uuid.uuid4().hex[:12] if comm == "host" else "rccl:%s" % (tmp_path / "rccl.id")
-    errs = _sharded_run(cfg, world, spec)
-    assert all("[%d/%d]" % (r, world) in e for r, e in enumerate(errs))
-    assert (tmp_path / "out" / "batch_proof.zkin.json").read_text() == zs.zkin_text(proof, o.publics, inst.n_cm2,
-                                                                                      inst.n_cm3)
+    idf = tmp_path / "rccl.id"
+    spec = "host:/zkgpu_t_%s" % uuid.uuid4().hex[:12] if comm == "host" else "rccl:%s" % idf
+    if comm == "rccl":  # an id file left at the same path by an earlier run (other tag): overwritten, not used
+        idf.write_bytes(b"ZKGPUID1" + (9).to_bytes(4, "little") + b"stale-run" + bytes(128))
+    for run in range(2 if comm == "rccl" else 1):  # twice against the same id path
+        errs = _sharded_run(cfg, world, spec)
+        assert all("[%d/%d]" % (r, world) in e for r, e in enumerate(errs))
+        assert (tmp_path / "out" / "batch_proof.zkin.json").read_text() == zs.zkin_text(proof, o.publics, inst.n_cm2,
+                                                                                          inst.n_cm3)
+        if comm == "rccl":
+            assert not idf.exists(), "rank 0 removes the id file once the communicator exists"

@@ -328,8 +328,8 @@ static std::string cache_key(const std::string &src)
         }
     };
     mix(src.data(), src.size());
-    char opt[96];
-    snprintf(opt, sizeof(opt), "hiprtc%d.%d opt%s resched%s", major, minor,
+    char opt[160];
+    snprintf(opt, sizeof(opt), "hiprtc%d.%d hip%d gfx950 opt%s resched%s", major, minor, (int)HIP_VERSION,
              getenv("ZKGPU_ZXP_JIT_OPT") ? getenv("ZKGPU_ZXP_JIT_OPT") : "-",
              getenv("ZKGPU_ZXP_JIT_RESCHED") ? getenv("ZKGPU_ZXP_JIT_RESCHED") : "-");
     mix(opt, strlen(opt));
@@ -338,17 +338,31 @@ static std::string cache_key(const std::string &src)
     return key;
 }
 
+// On-disk entry: "ZKJITCO2", u32 key length, key (cache_key: hash of source,
+// options, hiprtc / HIP versions, target), u64 object length, object.  A file
+// that does not carry this exact key and a complete ELF object is a miss.
+static const char JIT_CO_MAGIC[8] = {'Z', 'K', 'J', 'I', 'T', 'C', 'O', '2'};
+
 static bool cache_load(const std::string &src, std::vector<char> &code)
 {
     const std::string dir = cache_dir();
     if (dir.empty()) return false;
-    FILE *f = fopen((dir + "/" + cache_key(src)).c_str(), "rb");
+    const std::string key = cache_key(src);
+    FILE *f = fopen((dir + "/" + key).c_str(), "rb");
     if (!f) return false;
-    fseek(f, 0, SEEK_END);
-    const long n = ftell(f);
-    fseek(f, 0, SEEK_SET);
-    code.resize(n > 0 ? (size_t)n : 0);
-    const bool ok = n > 0 && fread(code.data(), 1, (size_t)n, f) == (size_t)n;
+    char magic[8];
+    uint32_t kn = 0;
+    uint64_t n = 0;
+    bool ok = fread(magic, 1, 8, f) == 8 && !memcmp(magic, JIT_CO_MAGIC, 8) && fread(&kn, 4, 1, f) == 1 &&
+              kn == key.size();
+    if (ok) {
+        std::string k2(kn, '\0');
+        ok = fread(&k2[0], 1, kn, f) == kn && k2 == key && fread(&n, 8, 1, f) == 1 && n > 4 && n < (1ULL << 32);
+    }
+    if (ok) {
+        code.resize(n);
+        ok = fread(code.data(), 1, n, f) == n && fgetc(f) == EOF && !memcmp(code.data(), "\x7f" "ELF", 4);
+    }
     fclose(f);
     return ok;
 }
@@ -358,43 +372,31 @@ static void cache_store(const std::string &src, const std::vector<char> &code)
     const std::string dir = cache_dir();
     if (dir.empty()) return;
     mkdir(dir.c_str(), 0775);
-    const std::string path = dir + "/" + cache_key(src), tmp = path + ".tmp" + std::to_string(getpid());
+    const std::string key = cache_key(src);
+    const std::string path = dir + "/" + key, tmp = path + ".tmp" + std::to_string(getpid());
     FILE *f = fopen(tmp.c_str(), "wb");
     if (!f) return;
-    const bool ok = fwrite(code.data(), 1, code.size(), f) == code.size();
+    const uint32_t kn = (uint32_t)key.size();
+    const uint64_t n = code.size();
+    const bool ok = fwrite(JIT_CO_MAGIC, 1, 8, f) == 8 && fwrite(&kn, 4, 1, f) == 1 && fwrite(key.data(), 1, kn, f) == kn &&
+                    fwrite(&n, 8, 1, f) == 1 && fwrite(code.data(), 1, n, f) == n;
     fclose(f);
     if (ok) rename(tmp.c_str(), path.c_str());
     else unlink(tmp.c_str());
 }
 
-// source -> code object: the disk cache, else hiprtc (and fill the cache)
-int code_object(const std::string &src, std::vector<char> &code)
+// source -> code object: the disk cache, else hiprtc (and fill the cache);
+// *cached tells which
+int code_object(const std::string &src, std::vector<char> &code, bool *cached = nullptr)
 {
-    if (cache_load(src, code)) return 0;
+    if (cached) *cached = false;
+    if (cache_load(src, code)) {
+        if (cached) *cached = true;
+        return 0;
+    }
     int rc;
     if ((rc = rtc_compile(src, code))) return rc;
     cache_store(src, code);
-    return 0;
-}
-
-int compile(const std::string &src, hipFunction_t *out)
-{
-    Cache &c = cache();
-    std::lock_guard<std::mutex> lk(c.mu);
-    auto it = c.fn.find(src);
-    if (it != c.fn.end()) {
-        *out = it->second;
-        return 0;
-    }
-    std::vector<char> code;
-    int rc;
-    if ((rc = code_object(src, code))) return rc;
-    hipModule_t mod;
-    if ((rc = check_hip(hipModuleLoadData(&mod, code.data()), "zxp jit: hipModuleLoadData"))) return rc;
-    hipFunction_t f;
-    if ((rc = check_hip(hipModuleGetFunction(&f, mod, "zxp_jit"), "zxp jit: hipModuleGetFunction"))) return rc;
-    c.fn.emplace(src, f);
-    *out = f;
     return 0;
 }
 
@@ -416,10 +418,11 @@ static bool jit_kl_lds(size_t nkl)
     return mode == 2 || nkl >= JIT_KL_LDS_MIN;
 }
 
-// Rows per thread of a compiled kernel (ZKGPU_ZXP_JIT_ROWS 1 / 2 / 4): large
-// programs evaluate 2 rows per thread, so each wave-uniform limb read from
-// LDS, column pointer and instruction serves 128 rows and two independent
-// chains hide each other's load latency; small programs keep one.
+// Rows per thread of a compiled kernel (ZKGPU_ZXP_JIT_ROWS 1 / 2 / 4, default
+// 1): with 2 rows each wave-uniform limb read from LDS, column pointer and
+// instruction serves 128 rows and two independent chains hide each other's
+// load latency -- measured equal to 1 row at twice the occupancy on the
+// zkEVM-sized quotient (0.557 vs 0.547 s at 2^24 rows), so it stays an option.
 static uint32_t jit_rows(bool large)
 {
     static const int env = [] {
@@ -427,7 +430,8 @@ static uint32_t jit_rows(bool large)
         return e ? atoi(e) : 0;
     }();
     if (env == 1 || env == 2 || env == 4) return (uint32_t)env;
-    return large ? 2 : 1;
+    (void)large;  // measured: 2 rows x 2 waves == 1 row x 4 waves on the zkEVM-sized quotient
+    return 1;
 }
 
 // every line holding a ` is written once per row r (` -> _r, ~ -> r)
@@ -892,7 +896,11 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             };
             uint32_t n_mem = 0;
             for (uint32_t t = I.a; t < I.a + I.b; t++) n_mem += memcol(in.terms[t]);
-            const bool loop = n_mem >= in.dot_loop_min;
+            // (large programs unroll every term: a looped DOT reads its
+            // term records through vector loads, one wait each, and holds its
+            // accumulators and in-flight loads across the loop -- the
+            // zkEVM-sized quotient 1.27 s with loops, 0.57 s without)
+            const bool loop = !split && n_mem >= in.dot_loop_min;
             if (loop) {
                 const size_t t0 = zt.size();
                 for (uint32_t t = I.a; t < I.a + I.b; t++) {
@@ -1003,8 +1011,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         klo_of.push_back(kl2.size());
         for (size_t b = 0; b + 1 < klo_of.size(); b++)
             if (klo_of[b + 1] - klo_of[b] > (size_t)JIT_KCHUNK)
-                return set_error(ZKGPU_ERR_ARG, "zxp jit: limb chunk of block %zu is %zu words", b,
-                                 klo_of[b + 1] - klo_of[b]);
+                return 1;  // a block's limbs overflow the LDS chunk: unsupported shape, the interpreter runs it
         std::string b2;
         b2.reserve(body.size());
         size_t pos = 0;
@@ -1140,10 +1147,11 @@ int prepare(const ZxpJitIn &in, JitKernel &K)
 // code objects of several sources (disk cache or hiprtc), compiled in
 // parallel threads: the segments of a large program are independent
 void objects_parallel(const std::vector<const std::string *> &srcs, std::vector<std::vector<char>> &code,
-                      std::vector<int> &rcs)
+                      std::vector<int> &rcs, std::vector<uint8_t> *from_cache = nullptr)
 {
     code.assign(srcs.size(), {});
     rcs.assign(srcs.size(), 0);
+    if (from_cache) from_cache->assign(srcs.size(), 0);
     static const unsigned nthr = [] {
         const char *e = getenv("ZKGPU_ZXP_JIT_THREADS");
         const unsigned hc = std::max(1u, std::thread::hardware_concurrency());
@@ -1152,7 +1160,11 @@ void objects_parallel(const std::vector<const std::string *> &srcs, std::vector<
     std::vector<std::thread> th;
     std::atomic<size_t> next{0};
     auto work = [&] {
-        for (size_t j; (j = next++) < srcs.size();) rcs[j] = code_object(*srcs[j], code[j]);
+        for (size_t j; (j = next++) < srcs.size();) {
+            bool hit = false;
+            rcs[j] = code_object(*srcs[j], code[j], &hit);
+            if (from_cache) (*from_cache)[j] = hit;
+        }
     };
     const unsigned n = std::min<unsigned>(nthr, (unsigned)srcs.size());
     for (unsigned t = 1; t < n; t++) th.emplace_back(work);
@@ -1179,12 +1191,21 @@ int compile_all(std::vector<JitKernel *> ks)
     for (JitKernel *k : todo) srcs.push_back(&k->src);
     std::vector<std::vector<char>> code;
     std::vector<int> rcs;
-    objects_parallel(srcs, code, rcs);
+    std::vector<uint8_t> hit;
+    objects_parallel(srcs, code, rcs, &hit);
     for (size_t j = 0; j < todo.size(); j++) {
         int rc;
         if (rcs[j]) return rcs[j];
         hipModule_t mod;
-        if ((rc = check_hip(hipModuleLoadData(&mod, code[j].data()), "zxp jit: hipModuleLoadData"))) return rc;
+        if (hit[j] && hipModuleLoadData(&mod, code[j].data()) != hipSuccess) {
+            // a cached object the runtime refuses: a miss -- compile and replace it
+            (void)hipGetLastError();
+            if ((rc = rtc_compile(todo[j]->src, code[j]))) return rc;
+            cache_store(todo[j]->src, code[j]);
+            hit[j] = 0;
+        }
+        if (!hit[j] && (rc = check_hip(hipModuleLoadData(&mod, code[j].data()), "zxp jit: hipModuleLoadData")))
+            return rc;
         hipFunction_t f;
         if ((rc = check_hip(hipModuleGetFunction(&f, mod, "zxp_jit"), "zxp jit: hipModuleGetFunction"))) return rc;
         c.fn.emplace(todo[j]->src, f);
@@ -1321,6 +1342,14 @@ int build_kernels(const ZxpJitIn &in, std::vector<JitKernel> &ks, const std::fun
         J.n_opnd = (uint32_t)seg[j].opnd.size();
         J.terms = seg[j].term.data();
         J.force_split = 1;
+        // occupancy target of a segment (ZKGPU_ZXP_SEG_WAVES, default 4 waves
+        // per SIMD = 128 VGPRs): zkEVM-sized quotient at 2^24 rows 0.57 s
+        // with the compiler's choice (~250 VGPRs), 0.55 s at 4 waves
+        static const uint32_t seg_waves = [] {
+            const char *e = getenv("ZKGPU_ZXP_SEG_WAVES");
+            return (uint32_t)(e ? atoi(e) : 4);
+        }();
+        if (!J.waves_per_eu) J.waves_per_eu = seg_waves;
         J.scratch = scr;
         J.scratch_ld = dom;
         if ((rc = prepare(J, ks[j]))) return rc;  // 1: unsupported shape -> interpreter for the whole program

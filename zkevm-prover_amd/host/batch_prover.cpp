@@ -35,6 +35,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <chrono>
 #include <cstdio>
@@ -130,13 +131,31 @@ struct Shard {
     int device = -1;
 };
 
-// the RCCL id through a file: rank 0 writes it (atomic rename), the others poll
+// The RCCL id through a file: rank 0 writes it (atomic rename), the others
+// poll.  Every file carries this run's tag -- ZKGPU_RUN_ID if set, else the
+// launcher's pid (ranks started by one launcher share their parent) -- and a
+// reader takes only a file with its own tag, so a file left by an earlier run
+// at the same path is never mistaken for this run's id.  Rank 0 removes the
+// file once the communicator exists (every rank has read it by then).
+static std::string run_tag()
+{
+    const char *e = getenv("ZKGPU_RUN_ID");
+    return e && *e ? std::string(e) : "ppid" + std::to_string((long)getppid());
+}
+
+static const char RCCL_ID_MAGIC[8] = {'Z', 'K', 'G', 'P', 'U', 'I', 'D', '1'};
+
 static void rccl_id_file(const std::string &path, uint32_t rank, uint8_t id[128])
 {
+    const std::string tag = run_tag();
     if (rank == 0) {
         if (zkgpu_comm_rccl_unique_id(id)) throw std::runtime_error(std::string("rccl id: ") + zkgpu_stark_last_error());
-        const std::string tmp = path + ".tmp";
+        const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
         std::ofstream f(tmp, std::ios::binary);
+        const uint32_t n = (uint32_t)tag.size();
+        f.write(RCCL_ID_MAGIC, 8);
+        f.write((const char *)&n, 4);
+        f.write(tag.data(), n);
         f.write((const char *)id, 128);
         f.close();
         if (!f.good() || std::rename(tmp.c_str(), path.c_str())) throw std::runtime_error("cannot write " + path);
@@ -144,10 +163,15 @@ static void rccl_id_file(const std::string &path, uint32_t rank, uint8_t id[128]
     }
     for (int t = 0; t < 6000; t++) {
         std::ifstream f(path, std::ios::binary);
-        if (f.good() && f.read((char *)id, 128) && f.gcount() == 128) return;
+        char magic[8];
+        uint32_t n = 0;
+        if (f.good() && f.read(magic, 8) && !memcmp(magic, RCCL_ID_MAGIC, 8) && f.read((char *)&n, 4) && n < 4096) {
+            std::string got(n, '\0');
+            if (f.read(&got[0], n) && got == tag && f.read((char *)id, 128) && f.gcount() == 128) return;
+        }
         std::this_thread::sleep_for(std::chrono::milliseconds(10));
     }
-    throw std::runtime_error("no RCCL id in " + path + " after 60 s");
+    throw std::runtime_error("no RCCL id for run " + tag + " in " + path + " after 60 s");
 }
 
 static int prove(const std::string &config_path, const Shard &sh)
@@ -193,6 +217,7 @@ static int prove(const std::string &config_path, const Shard &sh)
             uint8_t id[128];
             rccl_id_file(sh.comm.substr(5), sh.rank, id);
             rc = zkgpu_comm_rccl_create(&comm, id, sh.world, sh.rank);
+            if (!rc && sh.rank == 0) std::remove(sh.comm.substr(5).c_str());  // every rank has joined
         } else {
             throw std::runtime_error("--comm must be rccl:<file> or host:</name>");
         }

@@ -15,6 +15,8 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cstdlib>
+#include <string>
 #include <thread>
 
 namespace zkgpu_host {
@@ -23,8 +25,21 @@ struct HostCommHeader {
     std::atomic<uint32_t> ready;
     uint32_t world;
     uint64_t capacity;
+    uint64_t run;                 // this run's tag (run_tag_hash): a stale segment never matches
+    std::atomic<uint32_t> error;  // sticky: a rank failed inside an exchange
     pthread_barrier_t barrier;
 };
+
+// 64-bit tag of this run: ZKGPU_RUN_ID if set, else the launcher's pid
+// (ranks started by one launcher share their parent)
+static uint64_t run_tag_hash()
+{
+    const char *e = getenv("ZKGPU_RUN_ID");
+    const std::string t = e && *e ? std::string(e) : "ppid" + std::to_string((long)getppid());
+    uint64_t h = 1469598103934665603ULL;
+    for (char ch : t) h = (h ^ (uint8_t)ch) * 1099511628211ULL;
+    return h | 1;  // never 0 (a fresh segment)
+}
 
 struct HostCommEntry {
     int32_t peer;
@@ -54,26 +69,43 @@ struct HostCommCtx {
     }
 };
 
+// Every rank reaches both barriers whatever happens: a rank that fails
+// raises the shared (sticky) error flag and still waits, so one rank's error
+// is every rank's non-zero return instead of a hang in the barrier.
 static int host_exchange(void *vctx, const zkgpu_comm_op *ops, uint32_t n_ops)
 {
     HostCommCtx &c = *(HostCommCtx *)vctx;
+    HostCommHeader *h = c.hdr();
+    int rc = 0;
     uint64_t off = 0, n = 0;
     HostCommEntry *tab = c.entries(c.rank);
-    for (uint32_t k = 0; k < n_ops; k++) {
+    for (uint32_t k = 0; k < n_ops && !rc; k++) {
         const zkgpu_comm_op &o = ops[k];
-        if (o.peer < 0 || (uint32_t)o.peer >= c.world || (uint32_t)o.peer == c.rank)
-            return fail("host comm: bad peer %d", o.peer);
+        if (o.peer < 0 || (uint32_t)o.peer >= c.world || (uint32_t)o.peer == c.rank) {
+            rc = fail("host comm: bad peer %d", o.peer);
+            break;
+        }
         if (!o.send) continue;
-        if (n == HOST_COMM_MAX_OPS || off + o.bytes > c.capacity)
-            return fail("host comm: exchange exceeds the %llu-byte outbox", (unsigned long long)c.capacity);
-        CK(zkgpu_memcpy_d2h(c.data(c.rank) + off, o.buf, o.bytes));
+        if (n == HOST_COMM_MAX_OPS || off + o.bytes > c.capacity) {
+            rc = fail("host comm: exchange exceeds the %llu-byte outbox", (unsigned long long)c.capacity);
+            break;
+        }
+        if (zkgpu_memcpy_d2h(c.data(c.rank) + off, o.buf, o.bytes)) {
+            rc = fail("host comm: device -> outbox copy failed: %s", zkgpu_last_error());
+            break;
+        }
         tab[n++] = HostCommEntry{o.peer, 0, o.bytes, off};
         off += o.bytes;
     }
     c.n_entries(c.rank) = n;
+    if (rc) h->error.store(1);
     if (c.wait()) return -1;
+    if (h->error.load()) {
+        (void)c.wait();
+        return rc ? rc : fail("host comm: another rank failed in this exchange");
+    }
     std::vector<uint64_t> cursor(c.world, 0);
-    for (uint32_t k = 0; k < n_ops; k++) {
+    for (uint32_t k = 0; k < n_ops && !rc; k++) {
         const zkgpu_comm_op &o = ops[k];
         if (o.send) continue;
         const uint32_t s = (uint32_t)o.peer;
@@ -81,14 +113,20 @@ static int host_exchange(void *vctx, const zkgpu_comm_op *ops, uint32_t n_ops)
         const uint64_t ns = c.n_entries(s);
         uint64_t &i = cursor[s];
         while (i < ns && st[i].peer != (int32_t)c.rank) i++;
-        if (i == ns) return fail("host comm: rank %u sent rank %u fewer slices than it receives", s, c.rank);
-        if (st[i].bytes != o.bytes)
-            return fail("host comm: slice of %llu bytes from rank %u, receive of %llu", (unsigned long long)st[i].bytes,
-                        s, (unsigned long long)o.bytes);
-        CK(zkgpu_memcpy_h2d(o.buf, c.data(s) + st[i].off, o.bytes));
+        if (i == ns) {
+            rc = fail("host comm: rank %u sent rank %u fewer slices than it receives", s, c.rank);
+        } else if (st[i].bytes != o.bytes) {
+            rc = fail("host comm: slice of %llu bytes from rank %u, receive of %llu", (unsigned long long)st[i].bytes, s,
+                      (unsigned long long)o.bytes);
+        } else if (zkgpu_memcpy_h2d(o.buf, c.data(s) + st[i].off, o.bytes)) {
+            rc = fail("host comm: outbox -> device copy failed: %s", zkgpu_last_error());
+        }
         i++;
     }
-    return c.wait();
+    if (rc) h->error.store(1);
+    if (c.wait()) return -1;
+    if (h->error.load()) return rc ? rc : fail("host comm: another rank failed in this exchange");
+    return 0;
 }
 
 }  // namespace zkgpu_host

@@ -853,39 +853,26 @@ int zkgpu_comm_host_create(zkgpu_comm *comm, const char *name, uint32_t world, u
     c->world = world;
     c->capacity = capacity;
     c->size = HostCommCtx::header_bytes() + (uint64_t)world * c->box_bytes();
-    int fd = -1;
+    const uint64_t run = zkgpu_host::run_tag_hash();
+    void *m = MAP_FAILED;
     if (rank == 0) {
         shm_unlink(name);
-        fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
         if (fd >= 0 && ftruncate(fd, (off_t)c->size)) {
             close(fd);
             fd = -1;
         }
-    } else {
-        // wait (up to 60 s) for rank 0 to create and size the segment
-        for (int t = 0; t < 6000 && fd < 0; t++) {
-            fd = shm_open(name, O_RDWR, 0600);
-            struct stat st;
-            if (fd >= 0 && (fstat(fd, &st) || (uint64_t)st.st_size < c->size)) {
-                close(fd);
-                fd = -1;
-            }
-            if (fd < 0) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+        if (fd >= 0) {
+            m = mmap(nullptr, c->size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            close(fd);
         }
-    }
-    if (fd < 0) {
-        delete c;
-        return fail("zkgpu_comm_host_create: shared memory %s not available", name);
-    }
-    void *m = mmap(nullptr, c->size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-    close(fd);
-    if (m == MAP_FAILED) {
-        delete c;
-        return fail("zkgpu_comm_host_create: mmap of %llu bytes failed", (unsigned long long)c->size);
-    }
-    c->base = (uint8_t *)m;
-    HostCommHeader *h = c->hdr();
-    if (rank == 0) {
+        if (m == MAP_FAILED) {
+            delete c;
+            return fail("zkgpu_comm_host_create: shared memory %s of %llu bytes not available", name,
+                        (unsigned long long)c->size);
+        }
+        c->base = (uint8_t *)m;
+        HostCommHeader *h = c->hdr();
         pthread_barrierattr_t a;
         pthread_barrierattr_init(&a);
         pthread_barrierattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
@@ -893,16 +880,37 @@ int zkgpu_comm_host_create(zkgpu_comm *comm, const char *name, uint32_t world, u
         pthread_barrierattr_destroy(&a);
         h->world = world;
         h->capacity = capacity;
+        h->run = run;
+        h->error.store(0);
         h->ready.store(1, std::memory_order_release);
     } else {
-        int t = 0;
-        while (h->ready.load(std::memory_order_acquire) != 1 && t++ < 6000)
-            std::this_thread::sleep_for(std::chrono::milliseconds(10));
-        if (h->ready.load(std::memory_order_acquire) != 1 || h->world != world || h->capacity != capacity) {
-            munmap(m, c->size);
-            delete c;
-            return fail("zkgpu_comm_host_create: segment %s belongs to another world", name);
+        // wait (up to 60 s) for rank 0's segment of THIS run: a segment left
+        // under the name by an earlier run (other tag, or not yet unlinked by
+        // rank 0) is unmapped and looked up again
+        for (int t = 0; t < 6000 && m == MAP_FAILED; t++) {
+            const int fd = shm_open(name, O_RDWR, 0600);
+            struct stat st;
+            if (fd >= 0 && !fstat(fd, &st) && (uint64_t)st.st_size >= c->size)
+                m = mmap(nullptr, c->size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            if (fd >= 0) close(fd);
+            if (m != MAP_FAILED) {
+                const HostCommHeader *h = (const HostCommHeader *)m;
+                if (h->ready.load(std::memory_order_acquire) != 1 || h->run != run) {
+                    munmap(m, c->size);
+                    m = MAP_FAILED;
+                } else if (h->world != world || h->capacity != capacity) {
+                    munmap(m, c->size);
+                    delete c;
+                    return fail("zkgpu_comm_host_create: segment %s belongs to another world", name);
+                }
+            }
+            if (m == MAP_FAILED) std::this_thread::sleep_for(std::chrono::milliseconds(10));
         }
+        if (m == MAP_FAILED) {
+            delete c;
+            return fail("zkgpu_comm_host_create: shared memory %s of this run not available", name);
+        }
+        c->base = (uint8_t *)m;
     }
     // every rank has mapped the segment: its name is no longer needed
     if (c->wait()) {
