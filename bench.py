@@ -511,8 +511,10 @@ def quotient_measure(args, dev, torch, world, dist):
         roof["traffic"] = d["hbm_bytes_per_step"]
         roof["traffic_ratio"] = round(d["hbm_bytes_per_step"] / roof["alg_bytes_per_launch"], 2)
         roof["traffic_source"] = os.path.basename(f)
-        roof["traffic_note"] = ("PMC HBM bytes per pass (2 x FETCH_SIZE + WRITE_SIZE): the program reads %.0f column "
-                                "values per row against %d distinct -- re-reads the registers cannot hold"
+        roof["traffic_note"] = ("PMC HBM bytes per pass (2 x FETCH_SIZE + WRITE_SIZE): %.0f vector-memory reads per "
+                                "row (column values, carries, limb-chunk prefetch; SQ_INSTS_VMEM_RD x 64 / rows) "
+                                "against %d distinct column reads -- the program re-reads columns the registers "
+                                "cannot hold (DESIGN.md 3.4)"
                                 % (d["per_step"].get("SQ_INSTS_VMEM_RD", 0) * 64 / s42["rows"], s42["cols_read"]))
         roof["hbm_frac_measured_traffic"] = round(d["hbm_bytes_per_step"] / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         valu = d["per_step"].get("SQ_INSTS_VALU")

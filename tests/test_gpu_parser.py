@@ -156,3 +156,76 @@ def test_step42ns_shaped_jit_gpu_equals_oracle(oracle, zkgpu, monkeypatch, scale
                             1 << shape["n_bits_ext"], 1196, 175, chal, pub, evals, x, zh, q=qref)
     assert rc == 0 and qref.any()
     assert np.array_equal(got, qref)
+
+
+# fork-9 map sections of the n-domain programs
+STAGE = ["step2prev", "step3prev", "step3"]
+
+
+@pytest.mark.parametrize("name", STAGE + ["step52ns"])
+@pytest.mark.parametrize("log_dom,jit", [(12, "1"), (16, "2")])
+def test_zkevm_shaped_programs_gpu_equal_oracle(oracle, zkgpu, monkeypatch, name, log_dom, jit):
+    """The stage-2/3 column programs (step2prev / step3prev / step3: the
+    reference's opcode mix, ~300 written cm3/tmpExp columns, shifted stores
+    101-119 landing on row i+1 mod N) and the FRI polynomial (step52ns, 2,000
+    evals, xDivXSub) of zkgpu/synthetic_bytecode.py on the GPU == the oracle's
+    case-table interpreter, every section bit for bit: 2^12 rows through the
+    interpreter, 2^16 through the run-time compiled kernels (segments for the
+    large ones)."""
+    import torch
+    import zkgpu.parser as zp
+    import zkgpu.synthetic_bytecode as sb
+    monkeypatch.setenv("ZKGPU_ZXP_JIT", jit)
+    shape = sb.load_shape()
+    pid = sb.PARSERS.index(name)
+    ext = pid >= 3
+    ops, args = sb.generate(name, seed=1)
+    secs = sb.sections(shape)
+    prog = zp.convert(pid, ops, args, secs, shape["n_bits"], shape["n_bits_ext"])
+    dom = 1 << log_dom
+    rng = np.random.default_rng(1000 * pid + log_dom)
+    S = {sec: _rand(rng, (dom, w)) for sec, _, w in secs if (sec >= 5) == ext}
+    const = _rand(rng, (dom, shape["n_const"]))
+    chal, pub, evals = _rand(rng, (8, 3)), _rand(rng, 48), _rand(rng, (2048, 3))
+    xdiv, xdivw = (_rand(rng, (dom, 3)), _rand(rng, (dom, 3))) if ext else (None, None)
+    csec = SEC_CONST_2NS if ext else 4
+    dsecs = {sec: (zkgpu.to_device(np.ascontiguousarray(a.T)), dom, a.shape[1]) for sec, a in S.items()}
+    dsecs[csec] = (zkgpu.to_device(np.ascontiguousarray(const.T)), dom, const.shape[1])
+    f = torch.zeros((3, dom), dtype=torch.int64, device="cuda:0")
+    if ext:
+        dsecs[11] = (f, dom, 3)
+    dx = zkgpu.to_device(xdiv) if ext else None
+    dxw = zkgpu.to_device(xdivw) if ext else None
+    zkgpu.prof_reset()
+    zkgpu.prof_enable(True)
+    zkgpu.zxp_eval_dev(prog, dsecs, log_dom, chal, pub, evals, xdiv=dx, xdivw=dxw, extend_bits=1 if ext else 0,
+                       x_start=7 if ext else 1)
+    torch.cuda.synchronize()
+    zkgpu.prof_enable(False)
+    ran = zkgpu.prof_kernels()
+    if jit == "2":
+        assert any(k.startswith("k_zxp_jit") for k in ran), ("the compiled kernels did not run", ran)
+    # oracle on the same inputs (x_i = 7 w^i on the 2n coset, w^i on the n domain)
+    x = np.zeros(dom, np.uint64)
+    oracle.lib().oc_powers(oracle._p(x), 7 if ext else 1, oracle.gl_w(log_dom), dom)
+    zh = np.array([pow((pow(7, dom >> 1, P) * pow(P - 1, i, P) - 1) % P, P - 2, P) for i in range(2)], np.uint64)
+    off = {sec: o for sec, o, _ in secs}
+    R = {sec: a.copy() for sec, a in S.items()}
+    fref = np.zeros((dom, 3), np.uint64)
+    sh = shape["programs"][name]
+    rc = oracle.parser_eval(pid, ops, args, [(off[sec], a.shape[1], a) for sec, a in R.items()], const, dom,
+                            1 << (shape["n_bits_ext"] if ext else shape["n_bits"]), max(sh["ntemp1"], 8),
+                            max(sh["ntemp3"], 4), chal, pub, evals, x, zh,
+                            xdiv if ext else np.zeros((dom, 3), np.uint64),
+                            xdivw if ext else np.zeros((dom, 3), np.uint64), f=fref)
+    assert rc == 0
+    if ext:
+        assert fref.any()
+        assert np.array_equal(zkgpu.from_device(f).T, fref)
+    else:
+        changed = 0
+        for sec, a in R.items():
+            got = zkgpu.from_device(dsecs[sec][0]).T
+            assert np.array_equal(got, a), "%s: section %d differs" % (name, sec)
+            changed += int(not np.array_equal(a, S[sec]))
+        assert changed >= 1

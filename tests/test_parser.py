@@ -245,3 +245,37 @@ def test_synthetic_step42ns_converter_equals_oracle_parser(oracle, zp):
     finally:
         LOG_DOM = saved
     assert np.array_equal(B[SEC_Q_2NS], qref)
+
+
+@pytest.mark.parametrize("name", ["step2prev", "step3prev", "step3", "step42ns", "step52ns"])
+def test_synthetic_programs_converter_equals_oracle_parser(oracle, zp, name):
+    """Every synthetic program of zkgpu/synthetic_bytecode.py (the shapes of
+    the reference's five fork-9 programs: stage-2/3 column programs with
+    shifted stores, the quotient, the FRI polynomial) through the converter
+    and the ZXP compiler == the oracle's case-table interpreter on the fork-9
+    map at 2^10 rows; and the compiled program is one the run-time compiled
+    kernels take (no interpreter fallback on the GPU)."""
+    import zkgpu
+    import zkgpu.synthetic_bytecode as sb
+    pid = parser_isa.PARSERS.index(name)
+    ops, args = sb.generate(name, seed=1)
+    prog = zp.convert(pid, ops, args, ZKEVM_MAP, N_BITS, N_BITS_EXT)
+    written = _written(prog)
+    assert written, name
+    rng = np.random.default_rng(0x5E + pid)
+    S0, sc = _data(rng, name, pid >= 3)
+    A = _copy(S0)
+    sh = sb.load_shape()["programs"][name]
+    _run_oracle_parser(oracle, pid, ops, args, A, sc, (max(sh["ntemp1"], 8), max(sh["ntemp3"], 4)))
+    B = _copy(S0)
+    _run_zxp(oracle, prog, B, sc)
+    comp = zkgpu.zxp_compile(prog, sc["challenges"], sc["publics"], sc["evals"])
+    C = _copy(S0)
+    _run_zxp(oracle, prog, C, sc, compiled=comp)
+    changed = 0
+    for k in S0:
+        assert np.array_equal(A[k], B[k]), "%s: section %d, converted program != oracle parser" % (name, k)
+        assert np.array_equal(A[k], C[k]), "%s: section %d, compiled program != oracle parser" % (name, k)
+        changed += int(not np.array_equal(A[k], S0[k]))
+    assert changed == len(written), (name, written)
+    assert zkgpu.zxp_jit_source(prog, sc["challenges"], sc["publics"], sc["evals"])

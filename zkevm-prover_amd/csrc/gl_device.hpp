@@ -39,6 +39,12 @@ namespace zk {
 typedef __attribute__((address_space(1))) uint64_t gu64_t;
 __device__ __forceinline__ uint64_t gload(const uint64_t *p) { return *(const gu64_t *)p; }
 __device__ __forceinline__ void gstore(uint64_t *p, uint64_t v) { *(gu64_t *)p = v; }
+// A store to a column the same kernel never loads (the expression kernels'
+// output / carry columns, csrc/zxp_jit.hip): written as a double, a type no
+// load of the kernel uses, so type-based alias analysis lets the scheduler
+// move column loads across it.  The bits are the u64's.
+typedef __attribute__((address_space(1))) double gf64_t;
+__device__ __forceinline__ void gstore_out(uint64_t *p, uint64_t v) { *(gf64_t *)p = __builtin_bit_cast(double, v); }
 
 // any u64 -> [0, p)   (x < 2^64 < 2p, so one conditional subtraction)
 __device__ __forceinline__ uint64_t gl_canon(uint64_t a) { return a >= ZK_P ? a - ZK_P : a; }

@@ -22,11 +22,13 @@
 #include <dlfcn.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <utime.h>
 
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <set>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -177,9 +179,11 @@ extern "C" __global__ void __launch_bounds__(256) ZKJIT_WAVES zxp_jit(const JitP
 // scratch columns of a segmented program (csrc/zxp_segment.hpp) are stored
 // where the value is defined, not deferred to the end of the row
 #if ZKJIT_KL_CHUNK
-#define ZK_ST(j, v, ii) do { if (live_) gstore(CPTR(j) + ii, gl_canon(v)); } while (0)
+#define ZK_ST(j, v, ii) do { if (live_) gstore_out(CPTR(j) + ii, gl_canon(v)); } while (0)
+#define ZK_STS(j, v, ii, sh) do { if (live_) gstore_out(CPTR(j) + ((ii + (uint64_t)(int64_t)(sh)) & m), gl_canon(v)); } while (0)
 #else
-#define ZK_ST(j, v, ii) gstore(CPTR(j) + ii, gl_canon(v))
+#define ZK_ST(j, v, ii) gstore_out(CPTR(j) + ii, gl_canon(v))
+#define ZK_STS(j, v, ii, sh) gstore_out(CPTR(j) + ((ii + (uint64_t)(int64_t)(sh)) & m), gl_canon(v))
 #endif
 // a global limb table is re-based in every code block (an opaque copy of K):
 // with thousands of loads off one base register, SIFoldOperands dominated
@@ -364,6 +368,7 @@ static bool cache_load(const std::string &src, std::vector<char> &code)
         ok = fread(code.data(), 1, n, f) == n && fgetc(f) == EOF && !memcmp(code.data(), "\x7f" "ELF", 4);
     }
     fclose(f);
+    if (ok) utime((dir + "/" + key).c_str(), nullptr);  // in use: tools/jit_prebuild.py --prune keeps it
     return ok;
 }
 
@@ -481,14 +486,45 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         cp.push_back(col_ptr(sec, col));
         return slot[key] = (uint32_t)cp.size() - 1;
     };
-    // cells written by the program: (column slot, row shift) -> register w<r>;
-    // stores are deferred to the end of the row and land on row (i + shift) & m
+    // Columns the program reads (any shift): a written column it never reads
+    // is stored where the value is assigned (the compiled program forwards
+    // every read of a cell the row wrote, zxp_compile.cpp); a written column
+    // it also reads keeps its value in a register w<r> stored at the end of
+    // the row, landing on row (i + shift) & m (reads before the write see the
+    // old value).  Immediate stores keep the stage-3 programs' ~300 written
+    // cells out of the registers.
+    std::set<std::pair<uint32_t, uint32_t>> read_cols;
+    {
+        auto note = [&](uint32_t o) {
+            if (o >= in.n_opnd) return;
+            const zxp_operand &x = in.opnd[o];
+            if (x.kind == ZXP_COL || x.kind == ZXP_COL3)
+                for (uint32_t c = 0; c < (x.kind == ZXP_COL3 ? 3u : 1u); c++) read_cols.insert({x.a, x.b + c});
+        };
+        for (uint32_t k = 0; k < in.n_instr; k++) {
+            const zxp_instr &I = in.ins[k];
+            if (I.op == ZXP_DOT1 || I.op == ZXP_DOT3) {
+                for (uint32_t t = I.a; t < I.a + I.b; t++)
+                    if (in.terms[t].src != ZXP_TERM_ONE) note(in.terms[t].src);
+            } else {
+                note(I.a);
+                if (I.op != ZXP_COPY) note(I.b);
+            }
+        }
+    }
+    static const bool imm_stores = [] {  // ZKGPU_ZXP_JIT_IMMST=0: every store deferred (the round-2 form)
+        const char *e = getenv("ZKGPU_ZXP_JIT_IMMST");
+        return !e || atoi(e) != 0;
+    }();
+    auto store_now = [&](uint32_t sec, uint32_t col) {
+        return imm_stores && sec != ZXP_SEC_SCRATCH && !read_cols.count({sec, col});
+    };
     std::map<std::pair<uint32_t, int32_t>, uint32_t> wreg;
     std::vector<std::pair<uint32_t, int32_t>> wcell;  // register -> (slot, shift)
     std::vector<uint8_t> written_any;                  // per slot, at any shift
     for (uint32_t k = 0; k < in.n_instr; k++) {
         const zxp_operand &d = in.opnd[in.ins[k].dst];
-        if ((d.kind == ZXP_COL || d.kind == ZXP_COL3) && d.a != ZXP_SEC_SCRATCH)
+        if ((d.kind == ZXP_COL || d.kind == ZXP_COL3) && d.a != ZXP_SEC_SCRATCH && !store_now(d.a, d.b))
             for (uint32_t c = 0; c < (d.kind == ZXP_COL3 ? 3u : 1u); c++) {
                 const uint32_t j = col_slot(d.a, d.b + c);
                 const auto key = std::make_pair(j, (int32_t)d.c);
@@ -593,6 +629,24 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     // assignment of a value expression to a destination operand
     auto assign = [&](uint32_t didx, const Expr &r) -> int {
         const zxp_operand &d = in.opnd[didx];
+        if ((d.kind == ZXP_COL || d.kind == ZXP_COL3) && d.a != ZXP_SEC_SCRATCH && store_now(d.a, d.b)) {
+            // a column the program never reads: stored here, on row (i + shift) & m
+            const uint32_t nc = d.kind == ZXP_COL3 ? 3 : 1;
+            for (uint32_t c = 1; c < nc; c++)
+                if (!store_now(d.a, d.b + c)) return 1;  // mixed triple: keep the deferred form simple
+            const int32_t sh = (int32_t)d.c;
+            if (d.kind == ZXP_COL)
+                appendf(body, "ZK_STS(%u, %s%s, i`, %d);\n", col_slot(d.a, d.b), r.e.c_str(), r.dim == 3 ? ".v[0]" : "",
+                        sh);
+            else if (r.dim == 3)
+                appendf(body, "{ const gl3 t_ = %s; ZK_STS(%u, t_.v[0], i`, %d); ZK_STS(%u, t_.v[1], i`, %d); "
+                              "ZK_STS(%u, t_.v[2], i`, %d); }\n",
+                        r.e.c_str(), col_slot(d.a, d.b), sh, col_slot(d.a, d.b + 1), sh, col_slot(d.a, d.b + 2), sh);
+            else
+                appendf(body, "ZK_STS(%u, %s, i`, %d); ZK_STS(%u, 0, i`, %d); ZK_STS(%u, 0, i`, %d);\n",
+                        col_slot(d.a, d.b), r.e.c_str(), sh, col_slot(d.a, d.b + 1), sh, col_slot(d.a, d.b + 2), sh);
+            return 0;
+        }
         if ((d.kind == ZXP_COL || d.kind == ZXP_COL3) && d.a == ZXP_SEC_SCRATCH) {  // carried value: stored at once
             if (d.c != 0) return 1;
             if (d.kind == ZXP_COL)

@@ -98,16 +98,28 @@ class _Gen:
 
 def generate(name="step42ns", seed=1, shape=None, isa=None, scale=1.0):
     """(ops, args) uint64 arrays of a synthetic program shaped like the
-    reference's `name` program (currently step42ns: constraint quotient);
-    scale < 1 keeps that fraction of every opcode count (same mix, same map).
+    reference's `name` program: step42ns (constraint quotient), step2prev /
+    step3prev / step3 (stage-2/3 column programs with shifted stores) or
+    step52ns (FRI polynomial); scale < 1 keeps that fraction of every opcode
+    count (same mix, same map)."""
+    if name == "step42ns":
+        return _generate_step42ns(seed, shape, isa, scale)
+    if name in ("step2prev", "step3prev", "step3"):
+        return _generate_stage(name, seed, shape, isa, scale)
+    if name == "step52ns":
+        return _generate_step52ns(seed, shape, isa, scale)
+    raise ValueError("unknown program %r" % name)
+
+
+def _generate_step42ns(seed=1, shape=None, isa=None, scale=1.0):
+    """step42ns (the constraint quotient).
 
     Values form constraint trees: an opcode's temporary operands are taken
     from the not-yet-used values (most recent first), its result joins them;
     the oldest unused values become constraint results once more than
     FRONTIER are waiting, and results are folded into the accumulator by the
     Horner opcodes.  No value is dead, as in the reference."""
-    if name != "step42ns":
-        raise NotImplementedError("synthetic shapes: step42ns")
+    name = "step42ns"
     FRONTIER = 24
     shape = shape or load_shape()
     isa = isa or load_isa()
@@ -264,6 +276,269 @@ def generate(name="step42ns", seed=1, shape=None, isa=None, scale=1.0):
         chain(1)
     ops.append(69)
     args.append(0)
+    return np.array(ops, np.uint64), np.array(args, np.uint64)
+
+
+def _find(table, pred):
+    """opcodes of `table` whose micro-op list satisfies pred"""
+    return [c for c, (_, mops) in sorted(table.items()) if pred(mops)]
+
+
+def _generate_stage(name, seed=1, shape=None, isa=None, scale=1.0):
+    """A stage-2/3 column program (step2prev / step3prev / step3,
+    zkevm.chelpers.<step>.parser.cpp): the reference's opcode histogram over
+    the n-domain sections, every store opcode (86-120) writing a column of
+    the program's written set (cm3_n / tmpExp_n, the reference's distinct
+    counts), shifted stores (101-119) at the program's row shift.  Hazards are
+    those the reference avoids: a written column is never read except the
+    cell this row just wrote (store forwarding, same shift), and each written
+    column is written at one shift only (no two rows write one cell)."""
+    shape = shape or load_shape()
+    isa = isa or load_isa()
+    table = isa[name]
+    rng = np.random.default_rng(seed)
+    g = _Gen(name, shape, rng)
+    sh = g.sh
+    hist = {int(k): max(1, int(round(v * scale))) for k, v in sh["opcode_hist"].items()}
+    is_store = lambda c: table[c][1][0][1] is not None and table[c][1][0][1][0] in ("P", "PS")
+    stores = {c: n for c, n in hist.items() if is_store(c)}
+    body = {c: n for c, n in hist.items() if not is_store(c)}
+    # written sets: slots (col, dim) per section, each written at one shift
+    wsec = sorted(sh["writes"])
+    wprob = np.array([sh["writes"][s_]["accesses"] for s_ in wsec], float)
+    wprob /= wprob.sum()
+    n3 = sum(n for c, n in stores.items() if table[c][1][0][1][1] == 3)
+    n1 = sum(stores.values()) - n3
+    slots = {}
+    written = {}
+    for s_ in wsec:
+        width = g.map[s_]["width"]
+        want = min(sh["writes"][s_]["distinct_cols"], width)
+        share3 = n3 * 3 / max(1, n1 + 3 * n3)
+        k3 = int(want * share3 / 3)
+        cols = list(rng.permutation(width))
+        sl, used = [], set()
+        for c in cols:
+            if len(sl) >= k3:
+                break
+            if c + 2 < width and not used & {c, c + 1, c + 2}:
+                sl.append([int(c), 3, None])
+                used |= {c, c + 1, c + 2}
+        for c in cols:
+            if len(used) >= want:
+                break
+            if c not in used:
+                sl.append([int(c), 1, None])
+                used.add(c)
+        slots[s_] = sl
+        written[s_] = used
+    # reads avoid the written columns
+    for s_ in g.rsecs:
+        if s_ in written:
+            width = g.map[s_]["width"]
+            free = np.array(sorted(set(range(width)) - written[s_]), np.int64)
+            n = min(sh["reads"][s_]["distinct_cols"], free.size)
+            g.rcols[s_] = np.sort(rng.choice(free, size=n, replace=False))
+    cells = []  # written (offset, width, dim, shift) cells, for forwarded reads
+    copy1 = _find(table, lambda m: len(m) == 1 and m[0][0] == "copy" and m[0][1][0] == "T1" and m[0][2][0] == "P"
+                  and m[0][2][1] == 1)[0]
+    mk3 = [c for c in _find(table, lambda m: len(m) == 1 and m[0][1][0] == "T3" and
+                            not any(o and o[0] == "T3" for o in m[0][2:]))]
+    seq = np.repeat(np.array(list(body), np.int64), list(body.values()))
+    st = np.repeat(np.array(list(stores), np.int64), list(stores.values()))
+    order = np.concatenate([seq, st])
+    rng.shuffle(order)
+    # stores after their producers: the first 5 % of the program only computes
+    head = max(8, len(order) // 20)
+    order = list(order)
+    first = [c for c in order[:head] if not is_store(c)] + [c for c in order[:head] if is_store(c)]
+    order = first + order[head:]
+    ops, args = [], []
+    n1s, n3s = g.n1, g.n3
+    w1, w3 = [], []  # temp slots written so far
+    front1 = []
+    free1 = list(range(n1s))
+
+    def read_col(s_, dim):
+        """a column (dim 1) or 3 consecutive columns (dim 3) none of which the
+        program writes, from section s_ (another section if s_ has none)"""
+        for s2 in [s_] + [x for x in g.rsecs if x != s_]:
+            cols = g.rcols[s2]
+            if not len(cols):
+                continue
+            width = g.map[s2]["width"]
+            bad = written.get(s2, set())
+            for _ in range(64):
+                c = int(cols[rng.integers(len(cols))])
+                c = min(c, width - dim)
+                if not bad & set(range(c, c + dim)):
+                    return g.map[s2]["offset"] + c, width
+        raise AssertionError("no readable columns")
+
+    def emit(code, pick_dst3=None):
+        nargs, mops = table[int(code)]
+        a = [0] * nargs
+        filled = [False] * nargs
+
+        def put(f, v):
+            if f >= 0 and not filled[f]:
+                a[f] = int(v)
+                filled[f] = True
+
+        for (op, d, x, y) in mops:
+            for o in (x, y):
+                if o is None:
+                    continue
+                k = o[0]
+                if k == "T1" and not filled[o[2]]:
+                    if front1 and rng.random() < 0.85:
+                        put(o[2], front1.pop(len(front1) - 1 - min(int(rng.exponential(2)), len(front1) - 1)))
+                    else:
+                        put(o[2], w1[len(w1) - 1 - min(int(rng.exponential(8)), len(w1) - 1)])
+                elif k == "T3" and not filled[o[2]]:
+                    put(o[2], w3[int(rng.integers(len(w3)))])
+                elif k in ("P", "PS"):
+                    s_ = g.rsecs[rng.choice(len(g.rsecs), p=g.rprob)]
+                    fw = [cl for cl in cells if cl[2] == o[1] and (cl[3] != 0) == (k == "PS")]
+                    fw_s = [cl for cl in fw if cl[4] == s_]
+                    if fw and (rng.random() < 0.05 or (len(g.rcols[s_]) == 0 and fw_s)):
+                        # a cell this row wrote (the same shift): forwarded
+                        cl = (fw_s or fw)[int(rng.integers(len(fw_s or fw)))]
+                        off, w = cl[0], cl[1]
+                    else:
+                        off, w = read_col(s_, o[1])
+                    put(o[2], off)
+                    if k == "P":
+                        put(o[3], w)
+                    else:
+                        put(o[3], g.row_shift)
+                        put(o[4], g.dom)
+                        put(o[5], w)
+                elif k in ("K", "KS"):
+                    put(o[2], rng.integers(g.n_const))
+                    if k == "KS":
+                        put(o[3], g.row_shift)
+                        put(o[4], g.dom)
+                elif k == "L":
+                    put(o[2], int(rng.integers(0, P, dtype=np.uint64)) if rng.random() < 0.3
+                        else int(rng.integers(0, 64)))
+                elif k == "C":
+                    put(o[2], g.chal[rng.integers(len(g.chal))])
+                elif k == "U":
+                    put(o[2], 0)
+            kd = d[0]
+            if kd == "T1" and not filled[d[2]]:
+                s_ = free1.pop(0) if free1 else w1[int(rng.integers(len(w1)))]
+                put(d[2], s_)
+                if s_ not in w1:
+                    w1.append(s_)
+                front1.append(s_)
+                del front1[:-24]
+            elif kd == "T3" and not filled[d[2]]:
+                s_ = pick_dst3 if pick_dst3 is not None else int(rng.integers(n3s))
+                put(d[2], s_)
+                if s_ not in w3:
+                    w3.append(s_)
+            elif kd in ("P", "PS") and not filled[d[2]]:
+                shift = 0 if kd == "P" else g.row_shift
+                for _ in range(1000):
+                    s_ = wsec[rng.choice(len(wsec), p=wprob)]
+                    cand = [x for x in slots[s_] if x[1] == d[1] and x[2] in (None, shift)]
+                    if cand:
+                        break
+                x = cand[int(rng.integers(len(cand)))]
+                x[2] = shift
+                width = g.map[s_]["width"]
+                off = g.map[s_]["offset"] + x[0]
+                put(d[2], off)
+                if kd == "P":
+                    put(d[3], width)
+                else:
+                    put(d[3], g.row_shift)
+                    put(d[4], g.dom)
+                    put(d[5], width)
+                cells.append((off, width, d[1], shift, s_))
+        assert all(filled), (code, mops, filled)
+        ops.append(int(code))
+        args.extend(a)
+
+    for _ in range(4):  # values first: every temporary an op reads is written earlier in the row
+        emit(copy1)
+    for j in range(n3s):
+        emit(mk3[int(rng.integers(len(mk3)))], pick_dst3=j)
+    for code in order:
+        emit(code)
+    return np.array(ops, np.uint64), np.array(args, np.uint64)
+
+
+def _generate_step52ns(seed=1, shape=None, isa=None, scale=1.0):
+    """The FRI polynomial (step52ns, zkevm.chelpers.step52ns.parser.cpp):
+    a Horner chain with v1 over every committed column (opcodes 0 / 16 / 17),
+    saved (3); Horner chains with v2 over (pol - eval) for the evaluations
+    (21 / 18 / 19 / 20) times xDivXSubXi (5), then the primed group times
+    xDivXSubWXi (6), summed (8), stored to f_2ns (15).  Counts follow the
+    reference's histogram; columns from the fork-9 2ns sections, each once
+    per chain, eval indices distinct."""
+    shape = shape or load_shape()
+    isa = isa or load_isa()
+    table = isa["step52ns"]
+    rng = np.random.default_rng(seed)
+    g = _Gen("step52ns", shape, rng)
+    h = {int(k): v for k, v in g.sh["opcode_hist"].items()}
+    sc = lambda c: max(1, int(round(h.get(c, 1) * scale)))
+    ops, args = [], []
+
+    def emit(code, *a):
+        assert len(a) == table[code][0], (code, a)
+        ops.append(code)
+        args.extend(int(x) for x in a)
+
+    # committed columns, each once: dim-1 (16) and dim-3 (17) terms
+    cols1, cols3 = [], []
+    for s_ in g.rsecs:
+        m = g.map[s_]
+        w = m["width"]
+        cs = list(rng.permutation(w))
+        k3 = min(sc(17) * w // max(1, sum(g.map[x]["width"] for x in g.rsecs)), w // 3)
+        used = set()
+        for c in cs:
+            if len([x for x in cols3 if x[2] == s_]) >= k3:
+                break
+            if c + 2 < w and not used & {c, c + 1, c + 2}:
+                cols3.append((m["offset"] + int(c), w, s_))
+                used |= {c, c + 1, c + 2}
+        cols1 += [(m["offset"] + int(c), w, s_) for c in cs if c not in used]
+    rng.shuffle(cols1)
+    rng.shuffle(cols3)
+    cols1 = cols1[:sc(16) + 1]
+    cols3 = cols3[:sc(17)]
+    emit(0, cols1[0][0], cols1[0][1])  # A0 = P * v1
+    terms = [(16, c) for c in cols1[1:]] + [(17, c) for c in cols3]
+    rng.shuffle(terms)
+    for code, c in terms:
+        emit(code, c[0], c[1])  # A0 = A0 * v1 + P
+    emit(3)  # A1 = A0 * v1
+    n_ev = min(int(g.sh["n_evals_used"] or 1972), 1 + int(round(1972 * scale)))
+    evs = list(rng.permutation(max(n_ev, 4)))
+    groups = [(5, evs[:len(evs) * 2 // 3]), (6, evs[len(evs) * 2 // 3:])]  # unprimed x xdiv, primed x xdivw
+    for gi, (xop, ev) in enumerate(groups):
+        if gi:
+            emit(3)  # A1 = A0 * v1 (the running sum, saved)
+        c = cols1[int(rng.integers(len(cols1)))]
+        emit(21, c[0], c[1], ev[0])  # A0 = P - E
+        for e in ev[1:]:
+            r = rng.random()
+            if r < 0.71:
+                c = cols1[int(rng.integers(len(cols1)))]
+                emit(18, c[0], c[1], e)  # A0 = A0 * v2 + (P - E)
+            elif r < 0.88:
+                emit(19, int(rng.integers(g.n_const)), e)  # A0 = A0 * v2 + (K - E)
+            else:
+                c = cols3[int(rng.integers(len(cols3)))] if cols3 else cols1[0]
+                emit(20, c[0], c[1], e)  # A0 = A0 * v2 + (P3 - E)
+        emit(xop)  # A0 *= xDivXSubXi / xDivXSubWXi
+        emit(8)  # A0 = A1 + A0
+    emit(15)  # f_2ns = A0
     return np.array(ops, np.uint64), np.array(args, np.uint64)
 
 
