@@ -1362,8 +1362,55 @@ uint32_t segments_for(const zxp_compiled &cp)
 
 // the kernels of a program: one, or one per segment (scratch(n) returns the
 // carry columns' base for n columns of ld 2^log_dom)
-int build_kernels(const ZxpJitIn &in, std::vector<JitKernel> &ks, const std::function<uint64_t *(uint32_t)> &scratch)
+// An unsigned field of a code object's AMDGPU metadata note (msgpack map:
+// the key string, then its value), e.g. .private_segment_fixed_size (scratch
+// bytes per lane: > 0 means the kernel spills), .vgpr_count, .agpr_count.
+static uint64_t co_note(const std::vector<char> &code, const char *key)
 {
+    const size_t kn = strlen(key);
+    for (size_t at = 0; at + kn + 1 < code.size(); at++) {
+        if (memcmp(code.data() + at, key, kn)) continue;
+        const uint8_t *v = (const uint8_t *)code.data() + at + kn;
+        const size_t left = code.size() - at - kn;
+        if (v[0] < 0x80) return v[0];                                   // positive fixint
+        if (v[0] == 0xcc && left > 1) return v[1];                      // uint8
+        if (v[0] == 0xcd && left > 2) return ((uint64_t)v[1] << 8) | v[2];  // uint16 (big endian)
+        if (v[0] == 0xce && left > 4)
+            return ((uint64_t)v[1] << 24) | ((uint64_t)v[2] << 16) | ((uint64_t)v[3] << 8) | v[4];
+        return 0;
+    }
+    return 0;
+}
+static uint64_t co_scratch_bytes(const std::vector<char> &code) { return co_note(code, ".private_segment_fixed_size"); }
+
+// occupancy decisions already taken in this process: first source -> waves
+// (0: keep it), so repeated evaluations do not reread code objects
+static std::mutex g_waves_mu;
+static std::unordered_map<std::string, uint32_t> g_waves;
+static bool waves_known(const std::string &src, uint32_t &w)
+{
+    std::lock_guard<std::mutex> lk(g_waves_mu);
+    auto it = g_waves.find(src);
+    if (it == g_waves.end()) return false;
+    w = it->second;
+    return true;
+}
+static void waves_remember(const std::string &src, uint32_t w)
+{
+    std::lock_guard<std::mutex> lk(g_waves_mu);
+    g_waves[src] = w;
+}
+
+// may_compile = false (source / cache queries): the occupancy decisions use
+// only code objects already on disk, and stop where one is missing
+int build_kernels(const ZxpJitIn &in, std::vector<JitKernel> &ks, const std::function<uint64_t *(uint32_t)> &scratch,
+                  int only = -1, bool may_compile = true)
+{
+    // code object of a source: 0 found / compiled, 1 not on disk (query mode), < 0 error
+    auto object = [&](const std::string &src, std::vector<char> &code) -> int {
+        if (may_compile) return code_object(src, code);
+        return cache_load(src, code) ? 0 : 1;
+    };
     zxp_compiled view;
     memset(&view, 0, sizeof(view));
     view.instr = in.ins;
@@ -1379,7 +1426,37 @@ int build_kernels(const ZxpJitIn &in, std::vector<JitKernel> &ks, const std::fun
     if (nseg <= 1) {
         ks.resize(1);
         ks[0].bytes = in.bytes;
-        return prepare(in, ks[0]);
+        if ((rc = prepare(in, ks[0]))) return rc;
+        // A kernel the compiler leaves at 169-256 registers runs 2 waves per
+        // SIMD and is latency-bound: compiled again with an occupancy target
+        // of 3 (<= 168; config-4 quotient 186 VGPRs, 15.3 -> 12.7 ms); one
+        // above 256 (1 wave, AGPRs: the reference's step2prev, 512 + spills)
+        // with a target of 2.  Kernels at 3+ waves are left alone (a target
+        // lets the scheduler spend registers: FRI polynomial 8.9 -> 9.2 ms),
+        // as are block-split programs (registers bounded by their blocks).
+        // Decided from the code object's metadata, so the prebuilt cache and
+        // the run agree.  ZKGPU_ZXP_JIT_AUTOWAVES=0 disables.
+        static const bool auto_waves = [] {
+            const char *e = getenv("ZKGPU_ZXP_JIT_AUTOWAVES");
+            return !e || atoi(e) != 0;
+        }();
+        if (auto_waves && in.waves_per_eu == 0 && only <= 0 &&
+            ks[0].src.find("#define ZKJIT_SPLIT 1") == std::string::npos) {
+            uint32_t w = 0;
+            if (!waves_known(ks[0].src, w)) {
+                std::vector<char> code;
+                if ((rc = object(ks[0].src, code))) return rc < 0 ? rc : 0;
+                const uint64_t regs = co_note(code, ".vgpr_count") + co_note(code, ".agpr_count");
+                w = regs > 256 ? 2 : regs > 168 ? 3 : 0;
+                waves_remember(ks[0].src, w);
+            }
+            if (w) {
+                ZxpJitIn in2 = in;
+                in2.waves_per_eu = w;
+                if ((rc = prepare(in2, ks[0]))) return rc;
+            }
+        }
+        return 0;
     }
     std::vector<ZxpSegment> seg;
     uint32_t n_scratch = 0;
@@ -1399,14 +1476,55 @@ int build_kernels(const ZxpJitIn &in, std::vector<JitKernel> &ks, const std::fun
         // occupancy target of a segment (ZKGPU_ZXP_SEG_WAVES, default 4 waves
         // per SIMD = 128 VGPRs): zkEVM-sized quotient at 2^24 rows 0.57 s
         // with the compiler's choice (~250 VGPRs), 0.55 s at 4 waves
+        // A segment whose code spills more than ZKGPU_ZXP_SEG_SPILL_MAX bytes
+        // per lane (default 300) at that target is compiled again one wave
+        // lower (down to 2): the reference's step3 segments spill 324-452
+        // bytes at 4 waves, none at 2.  Small spills stay: on the synthetic
+        // quotient (<= 272 bytes) 4 waves with spills ran 0.54 s, the
+        // spill-free lower targets 0.58 s -- it is HBM-bound, occupancy buys
+        // bandwidth.  ZKGPU_ZXP_SEG_ADAPT=0 keeps the first target.
         static const uint32_t seg_waves = [] {
             const char *e = getenv("ZKGPU_ZXP_SEG_WAVES");
             return (uint32_t)(e ? atoi(e) : 4);
         }();
-        if (!J.waves_per_eu) J.waves_per_eu = seg_waves;
+        static const bool adapt = [] {
+            const char *e = getenv("ZKGPU_ZXP_SEG_ADAPT");
+            return !e || atoi(e) != 0;
+        }();
+        static const uint64_t spill_max = [] {
+            const char *e = getenv("ZKGPU_ZXP_SEG_SPILL_MAX");
+            return (uint64_t)(e ? atoll(e) : 300);
+        }();
+        const bool fixed = J.waves_per_eu != 0;
         J.scratch = scr;
         J.scratch_ld = dom;
+        uint32_t w = fixed ? J.waves_per_eu : seg_waves;
+        J.waves_per_eu = w;
         if ((rc = prepare(J, ks[j]))) return rc;  // 1: unsupported shape -> interpreter for the whole program
+        if (!fixed && adapt && (only < 0 || (size_t)only == j)) {
+            const std::string first = ks[j].src;
+            uint32_t wk = 0;
+            if (waves_known(first, wk)) {
+                if (wk != w) {
+                    J.waves_per_eu = wk;
+                    if ((rc = prepare(J, ks[j]))) return rc;
+                }
+            } else {
+                bool known = true;
+                while (w > 2) {
+                    std::vector<char> code;
+                    if ((rc = object(ks[j].src, code)) < 0) return rc;
+                    if (rc) {  // query mode, not compiled yet: undecided
+                        known = false;
+                        break;
+                    }
+                    if (co_scratch_bytes(code) <= spill_max) break;
+                    J.waves_per_eu = --w;
+                    if ((rc = prepare(J, ks[j]))) return rc;
+                }
+                if (known) waves_remember(first, w);
+            }
+        }
         ks[j].bytes = in.bytes / seg.size() + 8.0 * (seg[j].carry_in + seg[j].carry_out) * (double)dom;
     }
     return 0;
@@ -1419,35 +1537,9 @@ int zxp_jit_run(const ZxpJitIn &in, hipStream_t s)
     std::vector<JitKernel> ks;
     int rc = build_kernels(in, ks, [&](uint32_t n) { return workspace(6, (size_t)n << in.log_dom << 3); });
     if (rc) return rc;
-    if (ks.size() > 1) {
-        std::vector<JitKernel *> pk;
-        for (JitKernel &K : ks) pk.push_back(&K);
-        if ((rc = compile_all(pk))) return rc;
-        return launch_all(ks, in, s);
-    }
-    if ((rc = compile_all({&ks[0]}))) return rc;
-    // A kernel the compiler leaves at 169-256 VGPRs runs 2 waves per SIMD and
-    // is latency-bound; recompile it with an occupancy target of 3 (<= 168
-    // VGPRs).  Config-4 quotient: 186 VGPRs, 15.3 -> 12.7 ms; kernels that
-    // already fit 3+ waves are left alone (a target there lets the scheduler
-    // spend registers: FRI polynomial 8.9 -> 9.2 ms).  Larger kernels (one
-    // wave) and the block-split large programs (compiled for minutes, their
-    // registers bounded by the blocks) are left as they are.
-    // ZKGPU_ZXP_JIT_AUTOWAVES=0 disables.
-    static const bool auto_waves = [] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_AUTOWAVES");
-        return !e || atoi(e) != 0;
-    }();
-    if (auto_waves && in.waves_per_eu == 0 && ks[0].src.find("#define ZKJIT_SPLIT 1") == std::string::npos) {
-        int regs = 0;
-        if (hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, ks[0].fn) == hipSuccess && regs > 168 &&
-            regs <= 256) {
-            ZxpJitIn in3 = in;
-            in3.waves_per_eu = 3;
-            if ((rc = prepare(in3, ks[0]))) return rc;
-            if ((rc = compile_all({&ks[0]}))) return rc;
-        }
-    }
+    std::vector<JitKernel *> pk;
+    for (JitKernel &K : ks) pk.push_back(&K);
+    if ((rc = compile_all(pk))) return rc;
     return launch_all(ks, in, s);
 }
 
@@ -1494,7 +1586,9 @@ extern "C" int zkgpu_zxp_jit_source(const void *instr, uint32_t n_instr, const v
     J.waves_per_eu = getenv("ZKGPU_ZXP_JIT_WAVES") ? (uint32_t)atoi(getenv("ZKGPU_ZXP_JIT_WAVES")) : 0;
     std::vector<JitKernel> ks;
     static uint64_t dummy_scratch;
-    if ((rc = build_kernels(J, ks, [](uint32_t) { return &dummy_scratch; })))
+    const char *only_env = getenv("ZKGPU_ZXP_JIT_ONLY");
+    if ((rc = build_kernels(J, ks, [](uint32_t) { return &dummy_scratch; }, only_env ? atoi(only_env) : -1,
+                            rtc_check == 1 || rtc_check == 2)))
         return rc < 0 ? rc : set_error(ZKGPU_ERR_ARG, "zxp jit: unsupported program shape");
     std::string src;  // the kernels' sources (one per segment)
     for (size_t j = 0; j < ks.size(); j++) {
