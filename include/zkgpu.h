@@ -67,6 +67,10 @@ int zkgpu_gl_ntt(uint64_t *dst, const uint64_t *src, uint64_t n, uint64_t ncols,
  * Row-major in (n x ncols) and out (n_ext x ncols). */
 int zkgpu_gl_extend_pol(uint64_t *out, const uint64_t *in, uint64_t n_ext, uint64_t n, uint64_t ncols);
 
+/* device bytes extend_pol keeps in its grow-only workspaces for ncols
+ * columns (column batches; for the host's memory plan, no GPU needed) */
+uint64_t zkgpu_lde_workspace_bytes(uint64_t n, uint64_t n_ext, uint64_t ncols);
+
 /* device-resident, column-major variants */
 int zkgpu_gl_ntt_dev(uint64_t *dst, uint64_t ld_dst, const uint64_t *src, uint64_t ld_src, uint64_t n,
                      uint64_t ncols, int inverse);
@@ -145,6 +149,8 @@ int zkgpu_fri_transpose_dev(uint64_t *aux, const uint64_t *pol, uint64_t degree,
 
 /* ---- device memory (the host orchestrator owns HBM through these) -------- */
 int zkgpu_dev_malloc(void **ptr, uint64_t bytes);
+/* free / total HBM of the bound device (hipMemGetInfo) */
+int zkgpu_device_memory(uint64_t *free_bytes, uint64_t *total_bytes);
 int zkgpu_dev_free(void *ptr);
 int zkgpu_memcpy_h2d(void *dst, const void *src, uint64_t bytes);
 int zkgpu_memcpy_d2h(void *dst, const void *src, uint64_t bytes);
@@ -165,6 +171,21 @@ typedef struct {
  * buffer gets the deterministic pseudo-random elements rand(seed, stream, col, row). */
 int zkgpu_rand_cols_dev(uint64_t *base, uint64_t ld, const uint32_t *cols, uint32_t ncols, uint64_t nrows,
                         uint64_t seed, uint64_t stream);
+/* the same for a row block of a 2^log_n-row domain: local row r of the
+ * buffer gets global row (row0 + r) mod 2^log_n (halo rows after a block wrap
+ * to the domain's first rows) */
+int zkgpu_rand_cols_rows_dev(uint64_t *base, uint64_t ld, const uint32_t *cols, uint32_t ncols, uint64_t row0,
+                             uint64_t nrows, uint32_t log_n, uint64_t seed, uint64_t stream);
+
+/* Rows of selected columns between column-major device buffers -- the halo
+ * refresh, shifted-store spill and block copies of the row-sharded prover
+ * (host/sharded_starks.hpp): for k < ncols, j < nrows
+ *   dst[dcol_k * dst_ld + dst_row0 + j] = src[scol_k * src_ld + (src_row0 + j) mod 2^src_log_mod]
+ * with dcol_k = dst_cols[k] (k when dst_cols is NULL), likewise scol_k;
+ * src_log_mod = 0: no wrap.  The column lists are host arrays. */
+int zkgpu_copy_rows_dev(uint64_t *dst, uint64_t dst_ld, uint64_t dst_row0, const uint32_t *dst_cols,
+                        const uint64_t *src, uint64_t src_ld, uint64_t src_row0, uint32_t src_log_mod,
+                        const uint32_t *src_cols, uint32_t ncols, uint64_t nrows);
 
 /* Steps::step*_parser_first (steps.hpp:21-58; used at starks.cpp:73,155,193,
  * 241,371): evaluate one expression program (include/zkgpu_zxp.h) over every
@@ -184,7 +205,9 @@ int zkgpu_zxp_eval_dev(const void *instr, uint32_t n_instr, const void *opnd, ui
  * starting at global row row0), zhInv uses N = 2^(log_domain - extend_bits)
  * (row0 must be a multiple of 2^extend_bits), and a read at row shift s >= 0
  * does not wrap: the caller stores the next block's first s rows (the halo)
- * after the block, so every section's ld >= 2^log_rows + s. */
+ * after the block, so every section's ld >= 2^log_rows + s.  A store at row
+ * shift s likewise writes local row i + s: its last s rows land in the halo,
+ * and the caller moves them to the next block (host/sharded_starks.hpp). */
 int zkgpu_zxp_eval_block_dev(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd, uint32_t n_tmp1,
                              uint32_t n_tmp3, const zkgpu_sections *sections, uint32_t log_rows, uint32_t log_domain,
                              const uint64_t *challenges, const uint64_t *publics, uint32_t n_publics,

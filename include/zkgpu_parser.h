@@ -88,6 +88,20 @@ int zkgpu_steps_parser_eval(uint32_t parser, const uint64_t *ops, uint64_t n_ops
                             uint64_t n_args, const zkgpu_pols_section *secs, uint32_t n_secs, uint32_t n_bits,
                             uint32_t n_bits_ext, const zkgpu_steps_params *p);
 
+/* Section mirrors across calls (one proof stages each section once).  With
+ * mirroring on, the device copy of every section a call touches is kept
+ * (keyed by host address, rows and width) and reused by later calls while
+ * valid; a program's own stores keep it valid (written on the device, then
+ * copied back).  Host code that writes a section between calls -- in
+ * Starks::genProof calculateH1H2 (cm2_n, starks.cpp:104-127), calculateZ
+ * (cm3_n, :165-189), every extendPol (cm*_2ns, :53,134,215) and the quotient
+ * split (cm4_2ns, :255-296) -- must invalidate it first.  Off by default;
+ * turning it off releases the mirrors. */
+int zkgpu_steps_mirror(int enable);
+int zkgpu_steps_invalidate(const void *host_section); /* NULL: every mirror */
+void zkgpu_steps_release_mirrors(void);
+uint64_t zkgpu_steps_mirror_bytes(void); /* device bytes the mirrors hold */
+
 #ifdef __cplusplus
 }
 #endif

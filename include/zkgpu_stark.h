@@ -140,13 +140,20 @@ void zkgpu_comm_host_destroy(zkgpu_comm *comm);
 
 /* A prover whose extended (2n) domain is row-sharded over comm->world ranks:
  * rank r holds rows [r 2n/W, (r+1) 2n/W) of every extended section (plus the
- * next block's first 2^blowup rows), its share of the commitments' LDE
- * columns, and the subtrees of its rows; the n-domain sections are whole on
- * every rank.  Every rank calls the same functions in the same order
+ * next block's first 2^blowup rows), rows [r n/W, (r+1) n/W) of every n-domain
+ * section (plus the next block's first rows up to the programs' largest row
+ * shift), its share of the commitments' LDE columns, and the subtrees of its
+ * rows.  Every rank calls the same functions in the same order
  * (witness / set_cm1 / set_const / set_publics / prove are collective) and
  * every rank's zkgpu_stark_prove returns the same proof, equal to
  * zkgpu_stark_create's.  comm is copied; comm->ctx must outlive the handle. */
 int zkgpu_stark_create_sharded(void **handle, const zkgpu_stark_info *info, const zkgpu_comm *comm);
+/* HBM one GPU holds at its peak for this description (its sections, the
+ * transient setup copy of the constants, the library's workspaces): world 0
+ * = zkgpu_stark_create, world W >= 1 = zkgpu_stark_create_sharded over W
+ * ranks.  Host only, no GPU needed; both create calls fail loudly, before
+ * allocating, when it exceeds the device's free memory. */
+int zkgpu_stark_memory_plan(const zkgpu_stark_info *info, uint32_t world, uint64_t *bytes_per_gpu);
 
 #ifdef __cplusplus
 }

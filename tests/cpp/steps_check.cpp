@@ -1,0 +1,293 @@
+// Steps boundary check: zkgpu::StepsGPU (host/zkgpu_steps.hpp) instantiated
+// against stand-ins with the reference's exact shapes -- StepsParams and the
+// Steps interface of src/starkpil/steps.hpp:4-58, Polinomial's
+// address()/degree()/dim() (polinomial.hpp:11-60), ConstantPolsStarks'
+// address()/numPols() (constant_pols_starks.hpp:8-26), ZhInv (zhInv.hpp:13) --
+// and called through a Steps& the way Starks::genProof does
+// (starks.cpp:73,155,193,241,371).  tests/test_cpp_steps.py writes the
+// inputs (a zkEVM-shaped program and its memory map), runs this binary and
+// compares its outputs with the oracle's case-table interpreter.
+//
+// Checked here: every whole-domain entry point of the interface (avx, avx512,
+// the scalar and jump-table variants) gives the same bytes; with section
+// mirrors on, a repeated call served from the device copies gives the same
+// bytes and an invalidated section is re-staged; a per-row entry point fails
+// loudly.  Exit 0 = every check passed; outputs written to argv[2].
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+// ---- stand-ins with the reference's shapes ---------------------------------
+class Goldilocks
+{
+public:
+    struct Element {
+        uint64_t fe;
+    };
+};
+
+class Polinomial
+{
+    Goldilocks::Element *_pAddress = nullptr;
+    uint64_t _degree = 0, _dim = 0;
+    std::vector<Goldilocks::Element> _own;
+
+public:
+    Polinomial(uint64_t degree, uint64_t dim, std::string name = "") : _degree(degree), _dim(dim), _own(degree * dim)
+    {
+        _pAddress = _own.data();
+    }
+    Goldilocks::Element *address(void) { return _pAddress; }
+    uint64_t degree(void) { return _degree; }
+    uint64_t dim(void) { return _dim; }
+};
+
+class ConstantPolsStarks
+{
+    void *_pAddress;
+    uint64_t _degree, _numPols;
+
+public:
+    ConstantPolsStarks(void *pAddress, uint64_t degree, uint64_t numPols)
+        : _pAddress(pAddress), _degree(degree), _numPols(numPols){};
+    inline uint64_t numPols(void) { return _numPols; }
+    void *address(void) { return _pAddress; }
+    uint64_t degree(void) { return _degree; }
+};
+
+class ZhInv
+{
+};
+
+// src/starkpil/steps.hpp:4-58, verbatim in shape
+struct StepsParams {
+    Goldilocks::Element *pols;
+    ConstantPolsStarks *pConstPols;
+    ConstantPolsStarks *pConstPols2ns;
+    Polinomial &challenges;
+    Polinomial &x_n;
+    Polinomial &x_2ns;
+    ZhInv &zi;
+    Polinomial &evals;
+    Polinomial &xDivXSubXi;
+    Polinomial &xDivXSubWXi;
+    Goldilocks::Element *publicInputs;
+    Goldilocks::Element *q_2ns;
+    Goldilocks::Element *f_2ns;
+};
+
+class Steps
+{
+public:
+    virtual void step2prev_first(StepsParams &params, uint64_t i) = 0;
+    virtual void step2prev_i(StepsParams &params, uint64_t i) = 0;
+    virtual void step2prev_last(StepsParams &params, uint64_t i) = 0;
+    virtual void step2prev_parser_first_avx(StepsParams &params, uint64_t nrows, uint64_t nrowsBatch){};
+    virtual void step2prev_parser_first_avx512(StepsParams &params, uint64_t nrows, uint64_t nrowsBatch){};
+
+    virtual void step3prev_first(StepsParams &params, uint64_t i) = 0;
+    virtual void step3prev_i(StepsParams &params, uint64_t i) = 0;
+    virtual void step3prev_last(StepsParams &params, uint64_t i) = 0;
+    virtual void step3prev_parser_first_avx(StepsParams &params, uint64_t nrows, uint64_t nrowsBatch){};
+    virtual void step3prev_parser_first_avx512(StepsParams &params, uint64_t nrows, uint64_t nrowsBatch){};
+
+    virtual void step3_first(StepsParams &params, uint64_t i) = 0;
+    virtual void step3_i(StepsParams &params, uint64_t i) = 0;
+    virtual void step3_last(StepsParams &params, uint64_t i) = 0;
+    virtual void step3_parser_first(StepsParams &params, uint64_t nrows, uint64_t nrowsBatch){};
+    virtual void step3_parser_first_avx(StepsParams &params, uint64_t nrows, uint64_t nrowsBatch){};
+    virtual void step3_parser_first_avx_jump(StepsParams &params, uint64_t nrows, uint64_t nrowsBatch){};
+    virtual void step3_parser_first_avx512(StepsParams &params, uint64_t nrows, uint64_t nrowsBatch){};
+
+    virtual void step42ns_first(StepsParams &params, uint64_t i) = 0;
+    virtual void step42ns_i(StepsParams &params, uint64_t i) = 0;
+    virtual void step42ns_last(StepsParams &params, uint64_t i) = 0;
+    virtual void step42ns_parser_first(StepsParams &params, uint64_t nrows, uint64_t nrowsBatch){};
+    virtual void step42ns_parser_first_avx(StepsParams &params, uint64_t nrows, uint64_t nrowsBatch){};
+    virtual void step42ns_parser_first_avx_jump(StepsParams &params, uint64_t nrows, uint64_t nrowsBatch){};
+    virtual void step42ns_parser_first_avx512(StepsParams &params, uint64_t nrows, uint64_t nrowsBatch){};
+
+    virtual void step52ns_first(StepsParams &params, uint64_t i) = 0;
+    virtual void step52ns_i(StepsParams &params, uint64_t i) = 0;
+    virtual void step52ns_last(StepsParams &params, uint64_t i) = 0;
+
+    virtual void step52ns_parser_first(StepsParams &params, uint64_t nrows, uint64_t nrowsBatch){};
+    virtual void step52ns_parser_first_avx(StepsParams &params, uint64_t nrows, uint64_t nrowsBatch){};
+    virtual void step52ns_parser_first_avx512(StepsParams &params, uint64_t nrows, uint64_t nrowsBatch){};
+};
+
+#include "../../zkevm-prover_amd/host/zkgpu_steps.hpp"
+
+// ---- the check -------------------------------------------------------------
+static int failures = 0;
+static void expect(bool ok, const char *what)
+{
+    printf("%-64s %s\n", what, ok ? "ok" : "FAIL");
+    if (!ok) failures++;
+}
+
+struct Reader {
+    FILE *f;
+    uint64_t u() { uint64_t v = 0; if (fread(&v, 8, 1, f) != 1) throw std::runtime_error("short input"); return v; }
+    void arr(void *dst, uint64_t n)
+    {
+        if (n && fread(dst, 8, n, f) != n) throw std::runtime_error("short input");
+    }
+};
+
+// one whole-domain entry point of the interface, as genProof calls it
+typedef void (Steps::*Entry)(StepsParams &, uint64_t, uint64_t);
+
+int main(int argc, char **argv)
+{
+    if (argc < 3) {
+        fprintf(stderr, "usage: steps_check <input> <output>\n");
+        return 2;
+    }
+    zkgpu::set_error_handler([](const char *where, int code, const char *msg) {
+        throw std::runtime_error(std::string(where) + ": " + msg);
+    });
+    FILE *in = fopen(argv[1], "rb");
+    if (!in) return 2;
+    Reader r{in};
+    if (r.u() != 0x5354455053ULL) return 2;
+    const uint32_t parser = (uint32_t)r.u(), n_bits = (uint32_t)r.u(), n_bits_ext = (uint32_t)r.u();
+    const uint64_t n_const = r.u(), n_publics = r.u(), n_ops = r.u(), n_args = r.u(), n_map = r.u(),
+                   pols_len = r.u(), dom = r.u(), n_evals = r.u(), has_xdiv = r.u();
+    std::vector<uint64_t> ops(n_ops), args(n_args);
+    r.arr(ops.data(), n_ops);
+    r.arr(args.data(), n_args);
+    std::vector<zkgpu_pols_section> map(n_map);
+    for (auto &m : map) {
+        m.section = (uint32_t)r.u();
+        m.reserved = 0;
+        m.offset = r.u();
+        m.width = r.u();
+    }
+    std::vector<Goldilocks::Element> pols(pols_len), pols0(pols_len), cst(dom * n_const), pub(n_publics + 1);
+    r.arr(pols.data(), pols_len);
+    r.arr(cst.data(), dom * n_const);
+    Polinomial challenges(8, 3), x_n(1, 1), x_2ns(1, 1), evals(n_evals ? n_evals : 1, 3), xdiv(dom, 3), xdivw(dom, 3);
+    r.arr(challenges.address(), 24);
+    r.arr(pub.data(), n_publics);
+    r.arr(evals.address(), 3 * n_evals);
+    if (has_xdiv) {
+        r.arr(xdiv.address(), 3 * dom);
+        r.arr(xdivw.address(), 3 * dom);
+    }
+    fclose(in);
+    pols0 = pols;
+    ZhInv zi;
+    ConstantPolsStarks constPols(cst.data(), dom, n_const), constPols2ns(cst.data(), dom, n_const);
+    std::vector<Goldilocks::Element> q(3 * dom), f(3 * dom);
+    StepsParams params = {pols.data(), &constPols, &constPols2ns, challenges, x_n, x_2ns, zi, evals, xdiv, xdivw,
+                          pub.data(), q.data(), f.data()};
+
+    zkgpu::BytecodeProgram progs[5];
+    progs[parser] = zkgpu::BytecodeProgram{ops.data(), n_ops, args.data(), n_args};
+    zkgpu::StepsGPU<Steps, StepsParams> gpu(map.data(), (uint32_t)n_map, n_bits, n_bits_ext, (uint32_t)n_publics,
+                                            progs);
+    Steps &steps = gpu;  // through the reference interface
+
+    std::vector<Entry> entries;
+    std::vector<const char *> names;
+    switch (parser) {
+    case ZKGPU_STEP2PREV:
+        entries = {&Steps::step2prev_parser_first_avx, &Steps::step2prev_parser_first_avx512};
+        names = {"step2prev_parser_first_avx", "step2prev_parser_first_avx512"};
+        break;
+    case ZKGPU_STEP3PREV:
+        entries = {&Steps::step3prev_parser_first_avx, &Steps::step3prev_parser_first_avx512};
+        names = {"step3prev_parser_first_avx", "step3prev_parser_first_avx512"};
+        break;
+    case ZKGPU_STEP3:
+        entries = {&Steps::step3_parser_first_avx, &Steps::step3_parser_first_avx512, &Steps::step3_parser_first,
+                   &Steps::step3_parser_first_avx_jump};
+        names = {"step3_parser_first_avx", "step3_parser_first_avx512", "step3_parser_first",
+                 "step3_parser_first_avx_jump"};
+        break;
+    case ZKGPU_STEP42NS:
+        entries = {&Steps::step42ns_parser_first_avx, &Steps::step42ns_parser_first_avx512,
+                   &Steps::step42ns_parser_first, &Steps::step42ns_parser_first_avx_jump};
+        names = {"step42ns_parser_first_avx", "step42ns_parser_first_avx512", "step42ns_parser_first",
+                 "step42ns_parser_first_avx_jump"};
+        break;
+    default:
+        entries = {&Steps::step52ns_parser_first_avx, &Steps::step52ns_parser_first_avx512,
+                   &Steps::step52ns_parser_first};
+        names = {"step52ns_parser_first_avx", "step52ns_parser_first_avx512", "step52ns_parser_first"};
+    }
+    auto reset = [&] {
+        pols = pols0;
+        std::fill(q.begin(), q.end(), Goldilocks::Element{0});
+        std::fill(f.begin(), f.end(), Goldilocks::Element{0});
+    };
+    auto same = [](const std::vector<Goldilocks::Element> &a, const std::vector<Goldilocks::Element> &b) {
+        return memcmp(a.data(), b.data(), a.size() * 8) == 0;
+    };
+    try {
+        // the reference's call: nrows = the program's domain, a batch size
+        (steps.*entries[0])(params, dom, 4);
+        const std::vector<Goldilocks::Element> pols1 = pols, q1 = q, f1 = f;
+        expect(!same(pols1, pols0) || q1[0].fe || q1[1].fe || f1[0].fe || f1[1].fe, "the program wrote something");
+        for (size_t k = 1; k < entries.size(); k++) {
+            reset();
+            (steps.*entries[k])(params, dom, 4);
+            expect(same(pols, pols1) && same(q, q1) && same(f, f1), (std::string(names[k]) + " == " + names[0]).c_str());
+        }
+        // mirrors: first call stages, a repeat with unchanged inputs is served
+        // from the device copies; an invalidated section is staged again
+        gpu.keep_mirrors(true);
+        reset();
+        (steps.*entries[0])(params, dom, 4);
+        expect(same(pols, pols1) && same(q, q1) && same(f, f1), "with mirrors (first call) == without");
+        const uint64_t mb = zkgpu_steps_mirror_bytes();
+        expect(mb > 0, "mirrors hold the touched sections");
+        if (parser >= ZKGPU_STEP42NS) {  // reads only: a repeat sees the same inputs
+            std::fill(q.begin(), q.end(), Goldilocks::Element{0});
+            std::fill(f.begin(), f.end(), Goldilocks::Element{0});
+            (steps.*entries[0])(params, dom, 4);
+            expect(same(q, q1) && same(f, f1) && zkgpu_steps_mirror_bytes() == mb, "repeat served from the mirrors");
+            // host-side change of a read section, announced: the result follows it
+            for (const auto &m : map) {  // row 0 of every 2ns section
+                if (m.section < 5 || m.section > 9) continue;
+                for (uint64_t c = 0; c < m.width; c++) pols[m.offset + c].fe ^= 1;
+                gpu.invalidate(pols.data() + m.offset);
+            }
+            (steps.*entries[0])(params, dom, 4);
+            expect(!same(q, q1) || !same(f, f1), "an invalidated section is staged again");
+        } else {  // the program's own stores keep its mirrors valid
+            (steps.*entries[0])(params, dom, 4);
+            std::vector<Goldilocks::Element> pols2 = pols;
+            gpu.invalidate((const Goldilocks::Element *)nullptr);
+            pols = pols1;
+            (steps.*entries[0])(params, dom, 4);
+            expect(same(pols, pols2), "second call on mirrors == second call staged");
+        }
+        gpu.keep_mirrors(false);
+        expect(zkgpu_steps_mirror_bytes() == 0, "mirrors released");
+        // a per-row entry point fails loudly
+        bool threw = false;
+        try {
+            steps.step42ns_first(params, 0);
+        } catch (const std::runtime_error &) {
+            threw = true;
+        }
+        expect(threw, "per-row entry point step42ns_first fails loudly");
+        FILE *out = fopen(argv[2], "wb");
+        if (!out) return 2;
+        fwrite(pols1.data(), 8, pols1.size(), out);
+        fwrite(q1.data(), 8, q1.size(), out);
+        fwrite(f1.data(), 8, f1.size(), out);
+        fclose(out);
+    } catch (const std::exception &e) {
+        printf("error: %s\n", e.what());
+        return 1;
+    }
+    printf(failures ? "FAILURES: %d\n" : "ALL OK\n", failures);
+    return failures ? 1 : 0;
+}

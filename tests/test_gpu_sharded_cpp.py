@@ -18,12 +18,19 @@ pytestmark = pytest.mark.gpu
 INSTANCES = {
     "lookups": dict(n_bits=7, blowup_bits=1, t=3, m=2, n_free=2, n_lookups=2, n_queries=8),
     "blowup4": dict(n_bits=8, blowup_bits=2, t=4, m=1, n_lookups=1, q_deg=4, n_queries=12),
+    # the fork-9 zkEVM widths (751 / 168 / 408 / 6 committed, 234 constants,
+    # 389 tmpExp, two plookups; next-row reads and shifted stores in the
+    # n-domain stage programs): BASELINE configs[4]'s shape at 2^10 rows
+    "fork9": dict(fork9=True, n_bits=10),
 }
 
 
 def _inst(name):
     from zkgpu.synthetic import SyntheticStark
-    return SyntheticStark(**INSTANCES[name])
+    a = dict(INSTANCES[name])
+    if a.pop("fork9", False):
+        return SyntheticStark.fork9(**a)
+    return SyntheticStark(**a)
 
 
 def _oracle_json(inst):
@@ -41,6 +48,15 @@ def oracle_proofs(oracle):
 def _assert_same(got, want):
     for k in want:
         assert got[k] == want[k], k
+
+
+def test_fork9_single_gpu_equals_oracle(zkgpu, oracle_proofs):
+    """the unsharded prover at the fork-9 widths"""
+    from zkgpu.stark import GpuStark
+    g = GpuStark(_inst("fork9"))
+    g.witness()
+    _assert_same(g.prove(), oracle_proofs["fork9"])
+    g.close()
 
 
 @pytest.mark.parametrize("name", list(INSTANCES))
@@ -79,7 +95,7 @@ def test_sharded_rejects_bad_world(zkgpu):
         GpuStark(_inst("lookups"), comm=Three())
 
 
-def _worker(rank, world, port, q, name, shm):
+def _worker(rank, world, port, q, name, shm, rows=False):
     import sys
     root_dir = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root_dir, os.path.join(root_dir, "zkevm-prover_amd"), os.path.join(root_dir, "tests")]
@@ -92,7 +108,13 @@ def _worker(rank, world, port, q, name, shm):
         zkgpu.init(0)
         comm = ShmComm(shm, world, rank) if shm else HostStagedComm()
         g = GpuStark(_inst(name), comm=comm)
-        g.witness()
+        if rows:  # the executor's row-major cm1 (each rank takes its rows + halo)
+            from oracle.stark_prover import OracleStark
+            o = OracleStark(_inst(name))
+            o.witness()
+            g.set_cm1(o.S[0])
+        else:
+            g.witness()
         proof = g.prove()
         q.put((rank, proof, g.timers(), None))
         g.close()
@@ -113,21 +135,24 @@ def _free_port():
 
 
 @pytest.mark.parametrize("world,name,comm", [(2, "lookups", "gloo"), (4, "lookups", "gloo"), (2, "blowup4", "gloo"),
-                                             (2, "lookups", "shm"), (4, "blowup4", "shm"), (8, "lookups", "shm")])
+                                             (2, "lookups", "shm"), (4, "blowup4", "shm"), (8, "lookups", "shm"),
+                                             (2, "fork9", "gloo"), (8, "fork9", "shm"), (4, "lookups", "shm-rows")])
 def test_sharded_multiprocess_equals_oracle(oracle_proofs, world, name, comm):
     """gloo = HostStagedComm (Python, torch.distributed); shm = ShmComm
-    (host/comm_host.hpp, shared memory + process-shared barriers)"""
+    (host/comm_host.hpp, shared memory + process-shared barriers); -rows: the
+    trace handed over as the executor's row-major buffer (set_cm1)"""
     import multiprocessing as mp
     import uuid
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    shm = "/zkgpu_t_%s" % uuid.uuid4().hex[:12] if comm == "shm" else None
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, name, shm)) for r in range(world)]
+    shm = "/zkgpu_t_%s" % uuid.uuid4().hex[:12] if comm.startswith("shm") else None
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, name, shm, comm.endswith("-rows")))
+             for r in range(world)]
     for p in procs:
         p.start()
     try:
-        res = [q.get(timeout=100) for _ in range(world)]
+        res = [q.get(timeout=240) for _ in range(world)]
     finally:
         for p in procs:
             p.join(timeout=30)

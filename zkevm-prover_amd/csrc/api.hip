@@ -123,6 +123,27 @@ static uint32_t log2u(uint64_t n)
     return l;
 }
 
+// Columns per extend_pol batch: the batch's coefficients (n words per
+// column) and, on the 6-pass path, its 2n-row scratch live in grow-only
+// workspaces, so the batch bounds that memory -- 2^29 words (4 GiB) of scratch
+// unless ZKGPU_LDE_BATCH_COLS says otherwise (a batch of 32 columns at
+// 2^24 rows still fills the GPU: 2^29 elements per pass).
+static uint64_t lde_batch_cols(uint64_t n_ext, uint64_t ncols)
+{
+    static const uint64_t env = [] {
+        const char *e = getenv("ZKGPU_LDE_BATCH_COLS");
+        return e && atoll(e) > 0 ? (uint64_t)atoll(e) : 0ULL;
+    }();
+    uint64_t batch = env ? env : std::max<uint64_t>(1, (1ULL << 29) / (n_ext ? n_ext : 1));
+    return batch < ncols ? batch : ncols;
+}
+
+static uint64_t lde_workspace_bytes(uint64_t n, uint64_t n_ext, uint64_t ncols)
+{
+    const uint64_t b = lde_batch_cols(n_ext, ncols);
+    return b * n * 8 + (lde3_supported(log2u(n), log2u(n_ext)) ? 0 : b * n_ext * 8);
+}
+
 // device LDE on column-major buffers
 static int extend_pol_dev(uint64_t *out, uint64_t ld_out, const uint64_t *in, uint64_t ld_in, uint64_t n_ext,
                           uint64_t n, uint64_t ncols)
@@ -135,11 +156,7 @@ static int extend_pol_dev(uint64_t *out, uint64_t ld_out, const uint64_t *in, ui
     int rc;
     if ((rc = ensure_post_tables(logn))) return rc;
     Ctx &c = g_ctx;
-    // column batching bounds the scratch and keeps a batch's passes cache-resident
-    uint64_t batch = ncols;
-    const char *env = getenv("ZKGPU_LDE_BATCH_COLS");
-    if (env && atoll(env) > 0) batch = (uint64_t)atoll(env);
-    if (batch > ncols) batch = ncols;
+    const uint64_t batch = lde_batch_cols(n_ext, ncols);
     uint64_t *coef = workspace(0, batch * n * sizeof(uint64_t));
     if (!coef) return ZKGPU_ERR_OOM;
     if (lde3_supported(logn, loge)) {
@@ -307,6 +324,11 @@ int zkgpu_gl_ntt_dev(uint64_t *dst, uint64_t ld_dst, const uint64_t *src, uint64
     int rc;
     if ((rc = require_init())) return rc;
     return ntt_dev(dst, ld_dst, src, ld_src, n, ncols, inverse);
+}
+
+uint64_t zkgpu_lde_workspace_bytes(uint64_t n, uint64_t n_ext, uint64_t ncols)
+{
+    return lde_workspace_bytes(n, n_ext, ncols);
 }
 
 int zkgpu_gl_extend_pol_dev(uint64_t *out, uint64_t ld_out, const uint64_t *in, uint64_t ld_in, uint64_t n_ext,
@@ -705,7 +727,56 @@ int zkgpu_rand_cols_dev(uint64_t *base, uint64_t ld, const uint32_t *cols, uint3
     if (!p) return set_error(ZKGPU_ERR_OOM, "param buffer");
     if ((rc = check_hip(hipMemcpyAsync(p, cols, ncols * 4, hipMemcpyHostToDevice, g_ctx.stream), "H2D"))) return rc;
     if ((rc = check_hip(hipStreamSynchronize(g_ctx.stream), "rand_cols param upload"))) return rc;
-    return rand_cols(base, ld, (const uint32_t *)p, ncols, nrows, seed, stream, g_ctx.stream);
+    return rand_cols(base, ld, (const uint32_t *)p, ncols, nrows, seed, stream, 0, ~0ULL, g_ctx.stream);
+}
+
+int zkgpu_rand_cols_rows_dev(uint64_t *base, uint64_t ld, const uint32_t *cols, uint32_t ncols, uint64_t row0,
+                             uint64_t nrows, uint32_t log_n, uint64_t seed, uint64_t stream)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!ncols || !nrows) return 0;
+    if (log_n > 40 || ncols > 65535 || nrows > ld) return set_error(ZKGPU_ERR_ARG, "rand_cols_rows: bad shape");
+    char *p = param_buf(ncols * 4);
+    if (!p) return set_error(ZKGPU_ERR_OOM, "param buffer");
+    if ((rc = check_hip(hipMemcpyAsync(p, cols, ncols * 4, hipMemcpyHostToDevice, g_ctx.stream), "H2D"))) return rc;
+    if ((rc = check_hip(hipStreamSynchronize(g_ctx.stream), "rand_cols param upload"))) return rc;
+    return rand_cols(base, ld, (const uint32_t *)p, ncols, nrows, seed, stream, row0, (1ULL << log_n) - 1,
+                     g_ctx.stream);
+}
+
+int zkgpu_copy_rows_dev(uint64_t *dst, uint64_t dst_ld, uint64_t dst_row0, const uint32_t *dst_cols,
+                        const uint64_t *src, uint64_t src_ld, uint64_t src_row0, uint32_t src_log_mod,
+                        const uint32_t *src_cols, uint32_t ncols, uint64_t nrows)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!ncols || !nrows) return 0;
+    if (!dst || !src || ncols > 65535 || src_log_mod > 63 || dst_row0 + nrows > dst_ld ||
+        (!src_log_mod && src_row0 + nrows > src_ld) || (src_log_mod && (1ULL << src_log_mod) > src_ld))
+        return set_error(ZKGPU_ERR_ARG, "copy_rows: rows outside the buffers' leading dimensions");
+    const size_t nd = dst_cols ? ncols : 0, ns = src_cols ? ncols : 0;
+    char *p = param_buf((nd + ns) * 4 + 8);
+    if (!p) return set_error(ZKGPU_ERR_OOM, "param buffer");
+    if (nd && (rc = check_hip(hipMemcpyAsync(p, dst_cols, nd * 4, hipMemcpyHostToDevice, g_ctx.stream), "H2D")))
+        return rc;
+    if (ns && (rc = check_hip(hipMemcpyAsync(p + nd * 4, src_cols, ns * 4, hipMemcpyHostToDevice, g_ctx.stream), "H2D")))
+        return rc;
+    if ((nd || ns) && (rc = check_hip(hipStreamSynchronize(g_ctx.stream), "copy_rows param upload"))) return rc;
+    return copy_rows(dst, dst_ld, dst_row0, nd ? (const uint32_t *)p : nullptr, src, src_ld, src_row0,
+                     src_log_mod ? (1ULL << src_log_mod) - 1 : ~0ULL, ns ? (const uint32_t *)(p + nd * 4) : nullptr,
+                     ncols, nrows, g_ctx.stream);
+}
+
+int zkgpu_device_memory(uint64_t *free_bytes, uint64_t *total_bytes)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    size_t f = 0, t = 0;
+    if ((rc = check_hip(hipMemGetInfo(&f, &t), "hipMemGetInfo"))) return rc;
+    if (free_bytes) *free_bytes = f;
+    if (total_bytes) *total_bytes = t;
+    return 0;
 }
 
 static inline uint64_t h_add(uint64_t a, uint64_t b)
@@ -960,9 +1031,9 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
             return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u writes a read-only operand", k);
         // a shifted store (the reference's parser opcodes 101-114 / 119 write
         // pols[off + ((i + s) % N) * stride], step3.parser.cpp) lands on row
-        // (i + s) mod 2^log_dom; a row block without wrap-around has no such row
-        if ((z.kd == DK_C1 || z.kd == DK_C3) && z.id != 0 && !wrap)
-            return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u writes a shifted column in a row block", k);
+        // (i + s) mod 2^log_dom; in a row block (no wrap-around) on local row
+        // i + s, the last s of them in the halo rows (ld checked above), which
+        // the caller hands to the next block's owner
     }
     if (!use_jit) {  // interpreter temporaries live in LDS
         const uint64_t slots = (uint64_t)n_tmp1 + 3ULL * n_tmp3;

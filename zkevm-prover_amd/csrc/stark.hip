@@ -83,14 +83,31 @@ __device__ __forceinline__ uint64_t rand_u64(uint64_t seed, uint64_t stream, uin
     return z >> 1;
 }
 
+// local row r holds global row (row0 + r) & rmask (a row block of a sharded
+// domain, its halo rows wrapping to the domain's first rows)
 __global__ void k_rand_cols(uint64_t *base, uint64_t ld, const uint32_t *cols, uint32_t ncols, uint64_t nrows,
-                            uint64_t seed, uint64_t stream)
+                            uint64_t seed, uint64_t stream, uint64_t row0, uint64_t rmask)
 {
     uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t k = blockIdx.y;
     if (r >= nrows || k >= ncols) return;
     uint32_t c = cols[k];
-    base[(uint64_t)c * ld + r] = rand_u64(seed, stream, c, r);
+    base[(uint64_t)c * ld + r] = rand_u64(seed, stream, c, (row0 + r) & rmask);
+}
+
+// rows of selected columns between two column-major buffers (the halo and
+// block exchanges of the row-sharded prover): dst column dcols[k] (k if
+// null), rows drow0 + j  <-  src column scols[k] (k if null), rows
+// (srow0 + j) & smask.  One wave covers 64 consecutive rows of one column.
+__global__ void k_copy_rows(uint64_t *dst, uint64_t dld, uint64_t drow0, const uint32_t *dcols, const uint64_t *src,
+                            uint64_t sld, uint64_t srow0, uint64_t smask, const uint32_t *scols, uint32_t ncols,
+                            uint64_t nrows)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t k = blockIdx.y;
+    if (j >= nrows || k >= ncols) return;
+    const uint64_t dc = dcols ? dcols[k] : k, sc = scols ? scols[k] : k;
+    dst[dc * dld + drow0 + j] = src[sc * sld + ((srow0 + j) & smask)];
 }
 
 // ---------------------------------------------------------------- ZXP interpreter
@@ -616,12 +633,21 @@ __global__ void k_cols3_to_interleaved(uint64_t *out, const uint64_t *cols, uint
 static inline uint32_t nblk(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
 
 int rand_cols(uint64_t *base, uint64_t ld, const uint32_t *cols_dev, uint32_t ncols, uint64_t nrows, uint64_t seed,
-              uint64_t stream, hipStream_t s)
+              uint64_t stream, uint64_t row0, uint64_t rmask, hipStream_t s)
 {
     if (!ncols || !nrows) return 0;
     hipLaunchKernelGGL(k_rand_cols, dim3(nblk(nrows, 256), ncols), dim3(256), 0, s, base, ld, cols_dev, ncols, nrows,
-                       seed, stream);
+                       seed, stream, row0, rmask);
     return check_launch("k_rand_cols");
+}
+
+int copy_rows(uint64_t *dst, uint64_t dld, uint64_t drow0, const uint32_t *dcols, const uint64_t *src, uint64_t sld,
+              uint64_t srow0, uint64_t smask, const uint32_t *scols, uint32_t ncols, uint64_t nrows, hipStream_t s)
+{
+    if (!ncols || !nrows) return 0;
+    hipLaunchKernelGGL(k_copy_rows, dim3(nblk(nrows, 256), ncols), dim3(256), 0, s, dst, dld, drow0, dcols, src, sld,
+                       srow0, smask, scols, ncols, nrows);
+    return check_launch("k_copy_rows");
 }
 
 int zxp_eval(const ZxpLaunch &L, hipStream_t s)

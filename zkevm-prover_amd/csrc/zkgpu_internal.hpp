@@ -167,7 +167,9 @@ inline void zxp_limbs6(uint64_t c, uint32_t out[6])
 }
 
 int rand_cols(uint64_t *base, uint64_t ld, const uint32_t *cols_dev, uint32_t ncols, uint64_t nrows, uint64_t seed,
-              uint64_t stream, hipStream_t s);
+              uint64_t stream, uint64_t row0, uint64_t rmask, hipStream_t s);
+int copy_rows(uint64_t *dst, uint64_t dld, uint64_t drow0, const uint32_t *dcols, const uint64_t *src, uint64_t sld,
+              uint64_t srow0, uint64_t smask, const uint32_t *scols, uint32_t ncols, uint64_t nrows, hipStream_t s);
 int zxp_eval(const ZxpLaunch &L, hipStream_t s);
 size_t calculate_z_scratch_words(uint64_t n);
 int calculate_z(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,

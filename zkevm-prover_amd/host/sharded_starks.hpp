@@ -2,37 +2,45 @@
 // per GPU (BASELINE configs[4]); included by starks.cpp.
 //
 // The reference proves on one host (Starks::genProof, starks.cpp:9-404).  Here
-// the extended (2n) domain -- the bytes and the hashing -- is partitioned by
-// ROWS over W ranks (B = 2n / W rows each), and every step that touches it
-// works on the rank's rows:
+// BOTH domains are partitioned by ROWS over W ranks, so no rank holds a whole
+// section of the trace:
 //
+//   n domain   rank r holds rows [r nb, (r+1) nb) of cm1_n / cm2_n / cm3_n /
+//       tmpExp_n / const_n (nb = N / W) plus the next block's first hn rows
+//       (hn = the largest row shift the stage programs use: next-row reads,
+//       shifted stores), ld = nb + hn.  The stage programs (step2prev /
+//       step3prev / step3, starks.cpp:73,155,193) run on the rank's rows
+//       (zkgpu_zxp_eval_block_dev, x_i = w^(r nb + i)); afterwards the rows
+//       a shifted store wrote past the block go to the next rank (the
+//       single-GPU store writes (i + s) mod N) and every written column's halo
+//       is refreshed from the next rank, cyclically (the last rank's halo is
+//       row 0: the wrap-around of the reference's (i + 1) % N).  calculateZ:
+//       each rank its block, a scan of the W block totals, the block redone
+//       with the product of the earlier ranks' totals (polinomial.hpp:586-607).
+//       calculateH1H2 (starks.cpp:104-127) is a global multiset sort: f and t
+//       are all-gathered, h1/h2 computed on every rank, each keeps its rows.
 //   commit (stages 1-3 and the constants, starks.cpp:53-57,134-138,215-219)
-//       rank r extends its column share of the section (extendPol, no
-//       communication), ONE exchange sends every other rank its row block of
-//       those columns -- straight from the LDE output, each (column, rank)
-//       slice is contiguous -- plus the 2^blowup halo rows after the block
-//       (read by next-row constraints), received directly into the
-//       halo-padded block (ld B + 2^blowup); each rank hashes its rows as an
-//       exact subtree (merkleTreeGL.cpp:37-44 layout), the W sub-roots are
-//       all-gathered and the top log2 W levels hashed on every rank.
-//   stage 4  the quotient program on the rank's rows (x_i = 7 w^(rB+i),
-//       halo rows, zkgpu_zxp_eval_block_dev); q (2n x 3) is gathered, the
-//       INTT / split / NTT (starks.cpp:255-296) run on every rank, each
-//       commits its rows of the pieces.
+//       the NTT transpose: the rank's rows of every column go to the rank
+//       owning the column (all-to-all; each (column, rank) slice is contiguous
+//       on both sides, received straight into the LDE input), the rank extends
+//       its column share (extendPol, no communication), and a second all-to-all
+//       sends every other rank its 2n-domain row block of those columns plus
+//       the 2^blowup halo rows after it (halos packed, one message per peer).
+//       Each rank hashes its rows as an exact subtree (merkleTreeGL.cpp:37-44
+//       layout), the W sub-roots are all-gathered, the top log2 W levels
+//       hashed on every rank.
+//   stage 4  the quotient program on the rank's 2n rows (x_i = 7 w^(rB+i),
+//       halo rows); q (2n x 3) is gathered, the INTT / split / NTT
+//       (starks.cpp:255-296) run on every rank, each commits its rows.
 //   stage 5  evmap on the rank's n-domain rows, partial sums all-gathered and
 //       added mod p; the FRI program on the rank's rows, f gathered.
 //   FRI      folds on every rank (2n x 3 elements); a layer tree whose
-//       groups split into W blocks is row-sharded like the commits (each
-//       rank hashes its groups' subtree, sub-roots all-gathered, openings
-//       served by the owning rank); smaller layers on every rank.
+//       groups split into W blocks is row-sharded like the commits.
 //   queries  each s0 opening by the rank owning its row (subtree siblings +
 //       top levels), all-gathered.
-// The n-domain sections are whole on every rank; calculateZ is row-sharded
-// (each rank its N/W-row block, a scan of the W block totals, the blocks
-// all-gathered); the other n-domain stage work (step2 / H1H2 / step3prev /
-// step3, starks.cpp:67-211) runs on every rank.  The
-// transcript runs on every rank on identical inputs; the proof is the
-// single-GPU proof bit for bit.
+// The constants are set up once (build / load, untimed) on a transient whole
+// copy, committed, and cut to the rank's rows.  The transcript runs on every
+// rank on identical inputs; the proof is the single-GPU proof bit for bit.
 //
 // Every exchange is a zkgpu_comm call (RCCL over xGMI in production, see
 // comm_rccl.hpp; the tests plug a host-staged one); a rank never sends to
@@ -43,12 +51,16 @@ class ShardedStarks : public Starks
 public:
     zkgpu_comm comm{};
     uint32_t W = 1, R = 0;
-    uint64_t B = 0, H = 0, BH = 0;
-    uint64_t *ext = nullptr;   // LDE of the rank's column share (max share x NE)
-    uint64_t *gath = nullptr;  // q / f gathered (3 x NE)
-    uint64_t *cm4 = nullptr;   // quotient pieces, whole extended domain (n_cm4 x NE)
-    uint64_t *xchg = nullptr;  // all-gather staging, W slots
-    uint64_t slot = 0;
+    uint64_t B = 0, H = 0, BH = 0;     // 2n domain: block rows, halo rows (2^blowup), ld
+    uint64_t nb = 0, hn = 0, ldn = 0;  // n domain: block rows, halo rows, ld
+    uint64_t *ext = nullptr;    // LDE of the rank's column share (max share x NE)
+    uint64_t *coln = nullptr;   // the rank's column share over all N rows (max share x N): the LDE input
+    uint64_t *gath = nullptr;   // q / f gathered (3 x NE)
+    uint64_t *cm4 = nullptr;    // quotient pieces, whole extended domain (n_cm4 x NE)
+    uint64_t *xchg = nullptr;   // all-gather staging, W slots
+    uint64_t *hsend = nullptr, *hrecv = nullptr;  // halo / spill / 2n-halo staging (hcap words each)
+    uint64_t *puw = nullptr;    // one plookup's f, t, h1, h2 over the whole n domain (12 x N)
+    uint64_t slot = 0, hcap = 0;
     struct Tree {
         uint64_t *nodes = nullptr;
         const uint64_t *block = nullptr;
@@ -60,22 +72,80 @@ public:
     std::vector<Tree> ftrees;  // FRI layers (row-sharded where the groups split)
     std::vector<zkgpu_comm_op> ops;
 
-    int create_sharded(const zkgpu_stark_info *in, const zkgpu_comm *c)
+    // the n-domain columns a program writes: all of them (halo refresh) and,
+    // by (section, row shift > 0), the shifted stores (spill to the next rank)
+    struct Stores {
+        std::vector<uint32_t> cols[5];
+        std::vector<std::pair<std::pair<uint32_t, uint32_t>, std::vector<uint32_t>>> shifted;
+    };
+    Stores st1, st2, st3p, st3;
+
+    // shape only (no GPU): what create_sharded checks and allocates
+    int shape(const zkgpu_stark_info *in, uint32_t world, uint32_t rank, bool init)
     {
-        comm = *c;
-        W = c->world;
-        R = c->rank;
-        if (!W || (W & (W - 1)) || R >= W || (W > 1 && !c->exchange))
-            return fail("stark_create_sharded: world %u must be a power of two, rank %u < world, exchange set", W, R);
-        if (load(in)) return -1;
+        W = world;
+        R = rank;
+        if (!W || (W & (W - 1)) || R >= W)
+            return fail("stark_create_sharded: world %u must be a power of two, rank %u < world", W, R);
+        if (load(in, init)) return -1;
         H = 1ULL << eb;
         if (NE % W || N % W || NE / W < 2 * H)
             return fail("stark_create_sharded: 2^%u rows do not split into %u blocks of >= %llu rows", info.n_bits_ext,
                         W, (unsigned long long)(2 * H));
         B = NE / W;
         BH = B + H;
-        if (alloc()) return -1;
+        nb = N / W;
+        hn = 0;
+        const Prog *progs[4] = {&step1, &step2, &step3prev, &step3};
+        Stores *sts[4] = {&st1, &st2, &st3p, &st3};
+        for (int k = 0; k < 4; k++)
+            if (stores_of(*progs[k], *sts[k])) return -1;
+        if (hn > nb)
+            return fail("stark_create_sharded: row shift %llu exceeds the %llu-row n-domain block of %u ranks",
+                        (unsigned long long)hn, (unsigned long long)nb, W);
+        ldn = nb + hn;
+        return 0;
+    }
+
+    int create_sharded(const zkgpu_stark_info *in, const zkgpu_comm *c)
+    {
+        comm = *c;
+        if (shape(in, c->world, c->rank, true)) return -1;
+        if (c->world > 1 && !c->exchange) return fail("stark_create_sharded: the communicator has no exchange");
+        if (check_budget() || alloc()) return -1;
         return build_const();
+    }
+
+    // n-domain shifts of a program (reads and stores; sets hn) and its stores
+    int stores_of(const Prog &p, Stores &st)
+    {
+        std::map<std::pair<uint32_t, uint32_t>, uint32_t> shift_of;  // (section, column) -> store shift
+        std::map<std::pair<uint32_t, uint32_t>, std::vector<uint32_t>> by_shift;
+        for (const zxp_operand &o : p.opnd) {
+            if ((o.kind != ZXP_COL && o.kind != ZXP_COL3) || o.a > SEC_CONST_N) continue;
+            const int32_t sh = (int32_t)o.c;
+            if (sh < 0)
+                return fail("stark_create_sharded: negative row shift %d (the row-sharded prover reads ahead only)", sh);
+            hn = std::max<uint64_t>(hn, (uint64_t)sh);
+        }
+        for (const zxp_instr &in : p.instr) {
+            if (in.dst >= p.opnd.size()) return fail("stark_create_sharded: instruction destination out of range");
+            const zxp_operand &o = p.opnd[in.dst];
+            if ((o.kind != ZXP_COL && o.kind != ZXP_COL3) || o.a > SEC_CONST_N) continue;
+            for (uint32_t c = o.b; c < o.b + (o.kind == ZXP_COL3 ? 3u : 1u); c++) {
+                auto it = shift_of.find({o.a, c});
+                if (it != shift_of.end()) {
+                    if (it->second != o.c)
+                        return fail("stark_create_sharded: section %u column %u stored at two row shifts", o.a, c);
+                    continue;
+                }
+                shift_of[{o.a, c}] = o.c;
+                st.cols[o.a].push_back(c);
+                if (o.c) by_shift[{o.a, o.c}].push_back(c);
+            }
+        }
+        for (auto &kv : by_shift) st.shifted.push_back(kv);
+        return 0;
     }
 
     static uint32_t ceil_div(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
@@ -85,18 +155,31 @@ public:
         lo = r * base + (r < extra ? r : extra);
         hi = lo + base + (r < extra ? 1 : 0);
     }
+    uint64_t r0() const { return (uint64_t)R * nb; }  // global n-domain row of local row 0
+    uint32_t max_share() const
+    {
+        return std::max({1u, ceil_div(info.n_cm1, W), ceil_div(info.n_cm2, W), ceil_div(info.n_cm3, W),
+                         ceil_div(info.n_const, W)});
+    }
 
     int alloc() override
     {
-        if (alloc_n() || alloc_fri()) return -1;
+        if (alloc_fri()) return -1;
+        memset(&S, 0, sizeof S);
+        const uint32_t widths_n[5] = {info.n_cm1, info.n_cm2, info.n_cm3, info.n_tmp, info.n_const};
+        uint32_t wmax = 1;
+        for (int s = 0; s < 5; s++) {
+            if (dalloc(&S.sec[s], (uint64_t)(widths_n[s] ? widths_n[s] : 1) * ldn)) return -1;
+            S.ld[s] = ldn;
+            S.ncols[s] = widths_n[s];
+            wmax = std::max(wmax, widths_n[s]);
+        }
         const uint32_t blk_secs[4] = {SEC_CM1_2NS, SEC_CM2_2NS, SEC_CM3_2NS, SEC_CONST_2NS};
         const uint32_t blk_w[4] = {info.n_cm1, info.n_cm2, info.n_cm3, info.n_const};
-        uint32_t max_share = 1;
         for (int k = 0; k < 4; k++) {
             if (dalloc(&S.sec[blk_secs[k]], (uint64_t)(blk_w[k] ? blk_w[k] : 1) * BH)) return -1;
             S.ld[blk_secs[k]] = BH;
             S.ncols[blk_secs[k]] = blk_w[k];
-            max_share = std::max(max_share, ceil_div(blk_w[k], W));
         }
         if (dalloc(&cm4, (uint64_t)(info.n_cm4 ? info.n_cm4 : 1) * NE)) return -1;
         S.sec[SEC_CM4_2NS] = cm4 + (uint64_t)R * B;
@@ -107,7 +190,13 @@ public:
             S.ld[s] = B;
             S.ncols[s] = 3;
         }
-        if (dalloc(&gath, 3 * NE) || dalloc(&ext, (uint64_t)max_share * NE)) return -1;
+        const uint64_t ms = max_share();
+        if (dalloc(&gath, 3 * NE) || dalloc(&ext, ms * NE) || dalloc(&coln, ms * N)) return -1;
+        // halo staging: the n-domain halos / spills of every column, or the
+        // 2n-domain halos of a column share for every peer
+        hcap = std::max<uint64_t>((uint64_t)5 * wmax * std::max<uint64_t>(hn, 1), (uint64_t)W * ms * H);
+        if (dalloc(&hsend, hcap) || dalloc(&hrecv, hcap)) return -1;
+        if (info.n_pu && dalloc(&puw, 12 * N)) return -1;
         for (auto &t : trees)
             if (dalloc(&t.nodes, zkgpu_gl_merkle_num_elements(B))) return -1;
         slot = std::max<uint64_t>(4, std::max<uint64_t>(3ULL * info.n_ev, (uint64_t)q() * s0_record()));
@@ -120,6 +209,11 @@ public:
         }
         return dalloc(&xchg, slot * W);
     }
+
+    // the constants' whole copy while they are set up and committed
+    uint64_t setup_bytes() const override { return (uint64_t)(info.n_const ? info.n_const : 1) * N * 8; }
+    uint64_t lde_cols_max() const override { return max_share(); }
+    uint64_t prog_rows_max() const override { return std::max(B, nb); }
 
     uint64_t s0_record() const
     {
@@ -207,45 +301,249 @@ public:
         return 0;
     }
 
-    // LDE of the rank's column share, column -> row exchange (with halo), subtree
-    int commit_cols(Tree &t, uint32_t sec_e, const uint64_t *src_n, uint32_t ncols, uint64_t root[4],
+    // ---- n domain
+    // the NTT transpose: rows [0, nb) of every column of n-domain section sec
+    // to the rank owning the column; the rank's share [lo, hi) arrives in
+    // coln (ld N) at rows [s nb, (s+1) nb) from rank s
+    int rows_to_share(uint32_t sec, uint32_t ncols)
+    {
+        uint32_t lo, hi;
+        share(ncols, R, lo, hi);
+        for (uint32_t d = 0; d < W; d++) {
+            uint32_t dlo, dhi;
+            share(ncols, d, dlo, dhi);
+            for (uint32_t c = dlo; c < dhi; c++) {
+                const uint64_t *src = S.sec[sec] + (uint64_t)c * ldn;
+                if (d == R)
+                    CK(zkgpu_memcpy_d2d(coln + (uint64_t)(c - lo) * N + r0(), src, nb * 8));
+                else
+                    op(d, 1, src, nb * 8);
+            }
+        }
+        for (uint32_t s = 0; s < W; s++)
+            if (s != R)
+                for (uint32_t c = lo; c < hi; c++) op(s, 0, coln + (uint64_t)(c - lo) * N + (uint64_t)s * nb, nb * 8);
+        return exchange();
+    }
+
+    // rows [0, hn) of every written column -> the previous rank's halo rows
+    // [nb, nb + hn) (the last rank's halo is the domain's first rows)
+    int refresh_halos(const std::vector<uint32_t> cols[5])
+    {
+        if (!hn) return 0;
+        uint64_t off = 0;
+        for (uint32_t s = 0; s < 5; s++) {
+            const uint32_t n = (uint32_t)cols[s].size();
+            if (!n) continue;
+            if (off + (uint64_t)n * hn > hcap) return fail("halo refresh: %u columns exceed the staging", n);
+            CK(zkgpu_copy_rows_dev(hsend + off, hn, 0, nullptr, S.sec[s], ldn, 0, 0, cols[s].data(), n, hn));
+            off += (uint64_t)n * hn;
+        }
+        if (!off) return 0;
+        const uint64_t *in = hsend;
+        if (W > 1) {
+            op((R + W - 1) % W, 1, hsend, off * 8);
+            op((R + 1) % W, 0, hrecv, off * 8);
+            if (exchange()) return -1;
+            in = hrecv;
+        }
+        off = 0;
+        for (uint32_t s = 0; s < 5; s++) {
+            const uint32_t n = (uint32_t)cols[s].size();
+            if (!n) continue;
+            CK(zkgpu_copy_rows_dev(S.sec[s], ldn, nb, cols[s].data(), in + off, hn, 0, 0, nullptr, n, hn));
+            off += (uint64_t)n * hn;
+        }
+        return 0;
+    }
+
+    // a store at row shift s writes local rows [s, nb + s): rows [nb, nb + s)
+    // are the next rank's first s rows (the single-GPU store wraps mod N)
+    int spill(const Stores &st)
+    {
+        if (st.shifted.empty()) return 0;
+        uint64_t off = 0;
+        for (const auto &g : st.shifted) {
+            const uint32_t sec = g.first.first, sh = g.first.second, n = (uint32_t)g.second.size();
+            if (off + (uint64_t)n * sh > hcap) return fail("shifted-store spill exceeds the staging");
+            CK(zkgpu_copy_rows_dev(hsend + off, sh, 0, nullptr, S.sec[sec], ldn, nb, 0, g.second.data(), n, sh));
+            off += (uint64_t)n * sh;
+        }
+        const uint64_t *in = hsend;
+        if (W > 1) {
+            op((R + 1) % W, 1, hsend, off * 8);
+            op((R + W - 1) % W, 0, hrecv, off * 8);
+            if (exchange()) return -1;
+            in = hrecv;
+        }
+        off = 0;
+        for (const auto &g : st.shifted) {
+            const uint32_t sec = g.first.first, sh = g.first.second, n = (uint32_t)g.second.size();
+            CK(zkgpu_copy_rows_dev(S.sec[sec], ldn, 0, g.second.data(), in + off, sh, 0, 0, nullptr, n, sh));
+            off += (uint64_t)n * sh;
+        }
+        return 0;
+    }
+
+    // an n-domain stage program over the rank's rows, then the spill of its
+    // shifted stores and the halo refresh of everything it wrote
+    int run_n(const Prog &p, const Stores &st, const uint64_t ch[24])
+    {
+        if (p.instr.empty()) return 0;
+        uint32_t log_nb = 0;
+        while ((1ULL << log_nb) < nb) log_nb++;
+        const uint64_t ev0[3] = {0, 0, 0};
+        CK(zkgpu_zxp_eval_block_dev(p.instr.data(), (uint32_t)p.instr.size(), p.opnd.data(), (uint32_t)p.opnd.size(),
+                                    p.n_tmp1 ? p.n_tmp1 : 1, p.n_tmp3 ? p.n_tmp3 : 1, &S, log_nb, info.n_bits, ch,
+                                    publics.data(), (uint32_t)publics.size(), ev0, 0, nullptr, nullptr, 0,
+                                    pw(w_of(info.n_bits), r0())));
+        if (spill(st)) return -1;
+        return refresh_halos(st.cols);
+    }
+
+    const uint64_t *ncol(uint32_t ev_sec, uint32_t col, uint64_t row, uint64_t &ld) const override
+    {
+        if (ev_sec == SEC_CM4_2NS) return Starks::ncol(ev_sec, col, row, ld);  // the pieces are whole
+        ld = ldn;
+        const uint32_t s = ev_sec == SEC_CONST_2NS ? (uint32_t)SEC_CONST_N : ev_sec - SEC_CM1_2NS + SEC_CM1_N;
+        return S.sec[s] + (uint64_t)col * ldn + (row - r0());
+    }
+
+    // ---- setup and trace
+    // constants: a transient whole copy (rand + L_first + step0, or the
+    // host's rows), committed from it, then cut to the rank's rows
+    int const_from_whole(uint64_t *whole)
+    {
+        uint32_t lo, hi;
+        share(info.n_const, R, lo, hi);
+        if (commit_cols(trees[4], SEC_CONST_2NS, whole + (uint64_t)lo * N, N, info.n_const, verkey, nullptr, nullptr,
+                        nullptr))
+            return -1;
+        CK(zkgpu_copy_rows_dev(S.sec[SEC_CONST_N], ldn, 0, nullptr, whole, N, r0(), info.n_bits, nullptr,
+                               info.n_const, ldn));
+        CK(zkgpu_synchronize());
+        return 0;
+    }
+
+    int build_const() override
+    {
+        void *w = nullptr;
+        CK(zkgpu_dev_malloc(&w, (uint64_t)(info.n_const ? info.n_const : 1) * N * 8));
+        uint64_t *whole = (uint64_t *)w;
+        const zkgpu_sections blocks = S;
+        S.sec[SEC_CONST_N] = whole;  // Starks::build_const's fill on the whole domain ...
+        S.ld[SEC_CONST_N] = N;
+        int rc = fill_const();
+        S = blocks;
+        if (!rc) rc = const_from_whole(whole);  // ... then the commit and the cut
+        zkgpu_dev_free(w);
+        if (!rc) init_publics();
+        return rc;
+    }
+
+    int set_const(const uint64_t *rows) override
+    {
+        void *w = nullptr, *tmp = nullptr;
+        CK(zkgpu_dev_malloc(&w, (uint64_t)(info.n_const ? info.n_const : 1) * N * 8));
+        int rc = zkgpu_dev_malloc(&tmp, (uint64_t)(info.n_const ? info.n_const : 1) * N * 8);
+        if (!rc) rc = zkgpu_memcpy_h2d(tmp, rows, (uint64_t)info.n_const * N * 8);
+        if (!rc) rc = zkgpu_rows_to_cols_dev((uint64_t *)w, N, (const uint64_t *)tmp, N, info.n_const);
+        if (!rc) rc = zkgpu_synchronize();
+        if (tmp) zkgpu_dev_free(tmp);
+        if (rc) {
+            zkgpu_dev_free(w);
+            return fail("set_const: %s", zkgpu_last_error());
+        }
+        rc = const_from_whole((uint64_t *)w);
+        zkgpu_dev_free(w);
+        return rc;
+    }
+
+    int commit_const() override { return fail("stark (sharded): constants are committed from their whole copy"); }
+
+    // the executor's row-major buffer: the rank takes rows [r0, r0 + ldn) mod N
+    int set_cm1(const uint64_t *rows) override
+    {
+        void *tmp = nullptr;
+        const uint64_t w = info.n_cm1, first = std::min(ldn, N - r0());
+        CK(zkgpu_dev_malloc(&tmp, w * ldn * 8));
+        int rc = zkgpu_memcpy_h2d(tmp, rows + r0() * w, first * w * 8);
+        if (!rc && ldn > first) rc = zkgpu_memcpy_h2d((uint64_t *)tmp + first * w, rows, (ldn - first) * w * 8);
+        if (!rc) rc = zkgpu_rows_to_cols_dev(S.sec[SEC_CM1_N], ldn, (const uint64_t *)tmp, ldn, info.n_cm1);
+        if (!rc) rc = zkgpu_synchronize();
+        zkgpu_dev_free(tmp);
+        if (rc) return fail("set_cm1: %s", zkgpu_last_error());
+        return 0;
+    }
+
+    int witness() override
+    {
+        CK(zkgpu_memset_dev(S.sec[SEC_CM1_N], 0, (uint64_t)info.n_cm1 * ldn * 8));
+        CK(zkgpu_rand_cols_rows_dev(S.sec[SEC_CM1_N], ldn, random_cols.data(), (uint32_t)random_cols.size(), r0(), ldn,
+                                    info.n_bits, info.seed, 0));
+        uint64_t ch[24] = {0};
+        if (run_n(step1, st1, ch)) return -1;
+        CK(zkgpu_synchronize());
+        return 0;
+    }
+
+    // ---- commits
+    // LDE of the rank's column share (src: its first column, ld src_ld),
+    // column -> row exchange (halos packed), subtree
+    int commit_cols(Tree &t, uint32_t sec_e, const uint64_t *src, uint64_t src_ld, uint32_t ncols, uint64_t root[4],
                     const char *lde_name, const char *xchg_name, const char *tree_name)
     {
         uint32_t lo, hi;
         share(ncols, R, lo, hi);
+        const uint32_t ms = max_share();
         uint64_t *blk = S.sec[sec_e];
         tstart();
-        if (hi > lo) CK(zkgpu_gl_extend_pol_dev(ext, NE, src_n + (uint64_t)lo * N, N, NE, N, hi - lo));
+        if (hi > lo) CK(zkgpu_gl_extend_pol_dev(ext, NE, src, src_ld, NE, N, hi - lo));
         if (lde_name && tstop(lde_name)) return -1;
         tstart();
         for (uint32_t d = 0; d < W; d++) {
-            if (d == R) continue;
-            const uint64_t hb = (uint64_t)((d + 1) % W) * B;  // the halo: the next block's first rows
-            for (uint32_t c = 0; c < hi - lo; c++) {
-                op(d, 1, ext + c * NE + (uint64_t)d * B, B * 8);
-                op(d, 1, ext + c * NE + hb, H * 8);
-            }
+            if (d == R || hi == lo) continue;
+            for (uint32_t c = 0; c < hi - lo; c++) op(d, 1, ext + c * NE + (uint64_t)d * B, B * 8);
+            // the halo: the next block's first H rows, packed per peer
+            CK(zkgpu_copy_rows_dev(hsend + (uint64_t)d * ms * H, H, 0, nullptr, ext, NE, (uint64_t)((d + 1) % W) * B, 0,
+                                   nullptr, hi - lo, H));
+            op(d, 1, hsend + (uint64_t)d * ms * H, (uint64_t)(hi - lo) * H * 8);
         }
         for (uint32_t s = 0; s < W; s++) {
-            if (s == R) continue;
             uint32_t slo, shi;
             share(ncols, s, slo, shi);
-            for (uint32_t c = slo; c < shi; c++) {
-                op(s, 0, blk + (uint64_t)c * BH, B * 8);
-                op(s, 0, blk + (uint64_t)c * BH + B, H * 8);
-            }
+            if (s == R || shi == slo) continue;
+            for (uint32_t c = slo; c < shi; c++) op(s, 0, blk + (uint64_t)c * BH, B * 8);
+            op(s, 0, hrecv + (uint64_t)s * ms * H, (uint64_t)(shi - slo) * H * 8);
         }
-        const uint64_t hb = (uint64_t)((R + 1) % W) * B;
-        for (uint32_t c = lo; c < hi; c++) {
+        for (uint32_t c = lo; c < hi; c++)
             CK(zkgpu_memcpy_d2d(blk + (uint64_t)c * BH, ext + (c - lo) * NE + (uint64_t)R * B, B * 8));
-            CK(zkgpu_memcpy_d2d(blk + (uint64_t)c * BH + B, ext + (c - lo) * NE + hb, H * 8));
-        }
+        if (hi > lo)
+            CK(zkgpu_copy_rows_dev(blk + (uint64_t)lo * BH, BH, B, nullptr, ext, NE, (uint64_t)((R + 1) % W) * B, 0,
+                                   nullptr, hi - lo, H));
         if (exchange()) return -1;
+        for (uint32_t s = 0; s < W; s++) {
+            uint32_t slo, shi;
+            share(ncols, s, slo, shi);
+            if (s == R || shi == slo) continue;
+            CK(zkgpu_copy_rows_dev(blk + (uint64_t)slo * BH, BH, B, nullptr, hrecv + (uint64_t)s * ms * H, H, 0, 0,
+                                   nullptr, shi - slo, H));
+        }
         if (xchg_name && tstop(xchg_name)) return -1;
         tstart();
         if (merkelize(t, blk, BH, ncols, root)) return -1;
         if (tree_name && tstop(tree_name)) return -1;
         return 0;
+    }
+
+    // a stage's n-domain section: transpose to column shares, then commit
+    int commit_n(Tree &t, uint32_t sec_n, uint32_t sec_e, uint32_t ncols, uint64_t root[4], const char *lde_name,
+                 const char *xchg_name, const char *tree_name)
+    {
+        tstart();
+        if (rows_to_share(sec_n, ncols)) return -1;
+        if (xchg_name && tstop((std::string(xchg_name) + "_T").c_str())) return -1;
+        return commit_cols(t, sec_e, coln, N, ncols, root, lde_name, xchg_name, tree_name);
     }
 
     bool fri_sharded(uint64_t ngroups) const { return W > 1 && ngroups % W == 0 && ngroups / W >= 2; }
@@ -302,12 +600,6 @@ public:
         return 0;
     }
 
-    int commit_const() override
-    {
-        return commit_cols(trees[4], SEC_CONST_2NS, S.sec[SEC_CONST_N], info.n_const, verkey, nullptr, nullptr,
-                           nullptr);
-    }
-
     // F_p^3 product on the host (x^3 = x + 1)
     static void mul3(uint64_t r[3], const uint64_t a[3], const uint64_t b[3])
     {
@@ -322,20 +614,19 @@ public:
     }
 
     // calculateZ (starks.cpp:146-224, polinomial.hpp:586-607) over the rank's
-    // N/W-row block: z = prod of the ratios before each row, the block total
+    // block: z = prod of the ratios before each row, the block total
     // all-gathered, the block redone with z0 = the product of the earlier
-    // ranks' totals (rank 0's is already final), then the blocks all-gathered
-    // so every rank holds the whole column (the n-domain sections are whole)
+    // ranks' totals (rank 0's is already final); then the z halos
     int z_all() override
     {
-        const uint64_t nb = N / W, r0 = (uint64_t)R * nb;
+        Stores zs;
         for (uint32_t zi = 0; zi < info.n_zctx; zi++) {
-            uint64_t *z = S.sec[SEC_CM3_N] + (uint64_t)zctx[3 * zi + 2] * N;
-            const uint64_t *num = S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * zi] * N;
-            const uint64_t *den = S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * zi + 1] * N;
+            uint64_t *z = S.sec[SEC_CM3_N] + (uint64_t)zctx[3 * zi + 2] * ldn;
+            const uint64_t *num = S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * zi] * ldn;
+            const uint64_t *den = S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * zi + 1] * ldn;
             const uint64_t one[3] = {1, 0, 0};
             uint64_t tot[3];
-            CK(zkgpu_calculate_z_block_dev(z + r0, N, num + r0, N, den + r0, N, nb, one, tot));
+            CK(zkgpu_calculate_z_block_dev(z, ldn, num, ldn, den, ldn, nb, one, tot));
             std::vector<uint64_t> all;
             if (allgather(tot, 3, all)) return -1;
             uint64_t pre[3] = {1, 0, 0}, acc[3] = {1, 0, 0};
@@ -345,14 +636,47 @@ public:
             }
             if (acc[0] != 1 || acc[1] || acc[2]) return fail("calculateZ: grand product %u does not close", zi);
             if (pre[0] != 1 || pre[1] || pre[2])
-                CK(zkgpu_calculate_z_block_dev(z + r0, N, num + r0, N, den + r0, N, nb, pre, tot));
-            for (uint32_t d = 0; d < W; d++)
-                if (d != R)
-                    for (int c = 0; c < 3; c++) op(d, 1, z + (uint64_t)c * N + r0, nb * 8);
-            for (uint32_t s = 0; s < W; s++)
-                if (s != R)
-                    for (int c = 0; c < 3; c++) op(s, 0, z + (uint64_t)c * N + (uint64_t)s * nb, nb * 8);
+                CK(zkgpu_calculate_z_block_dev(z, ldn, num, ldn, den, ldn, nb, pre, tot));
+            for (uint32_t c = 0; c < 3; c++) zs.cols[SEC_CM3_N].push_back(zctx[3 * zi + 2] + c);
+        }
+        return refresh_halos(zs.cols);
+    }
+
+    // calculateH1H2 (starks.cpp:104-127) of every plookup: a global multiset
+    // sort, so f and t are all-gathered, h1 / h2 computed whole on every rank
+    // and each keeps its rows (with the halo: no refresh needed)
+    int h1h2_all() override
+    {
+        for (uint32_t k = 0; k < info.n_pu; k++) {
+            const uint32_t *q = &pu[5 * k];
+            const uint32_t d = q[4];
+            uint64_t *fw = puw, *tw = puw + 3 * N, *h1w = puw + 6 * N, *h2w = puw + 9 * N;
+            for (uint32_t part = 0; part < 2; part++) {
+                uint64_t *whole = part ? tw : fw;
+                const uint32_t c0 = q[part];
+                for (uint32_t c = 0; c < d; c++) {
+                    const uint64_t *mine = S.sec[SEC_TMP_N] + (uint64_t)(c0 + c) * ldn;
+                    CK(zkgpu_memcpy_d2d(whole + (uint64_t)c * N + r0(), mine, nb * 8));
+                    for (uint32_t p = 0; p < W; p++) {
+                        if (p == R) continue;
+                        op(p, 1, mine, nb * 8);
+                        op(p, 0, whole + (uint64_t)c * N + (uint64_t)p * nb, nb * 8);
+                    }
+                }
+            }
             if (exchange()) return -1;
+            uint64_t miss = 0;
+            const int rc = zkgpu_h1h2_dev(h1w, N, h2w, N, fw, N, tw, N, N, d, &miss);
+            if (rc) {
+                if (miss != ~0ULL)
+                    return fail("Polinomial::calculateH1H2() Number not included: w=%llu plookup_number=%u",
+                                (unsigned long long)miss, k);
+                return fail("calculateH1H2: %s", zkgpu_last_error());
+            }
+            CK(zkgpu_copy_rows_dev(S.sec[SEC_CM2_N] + (uint64_t)q[2] * ldn, ldn, 0, nullptr, h1w, N, r0(), info.n_bits,
+                                   nullptr, d, ldn));
+            CK(zkgpu_copy_rows_dev(S.sec[SEC_CM2_N] + (uint64_t)q[3] * ldn, ldn, 0, nullptr, h2w, N, r0(), info.n_bits,
+                                   nullptr, d, ldn));
         }
         return 0;
     }
@@ -381,41 +705,41 @@ public:
         uint64_t roots[4][4];
         std::vector<uint64_t> evals(3 * info.n_ev);
         // STAGE 1 (starks.cpp:49-63)
-        if (commit_cols(trees[0], SEC_CM1_2NS, S.sec[SEC_CM1_N], info.n_cm1, roots[0], "STARK_STEP_1_LDE",
-                        "STARK_STEP_1_EXCHANGE", "STARK_STEP_1_MERKLETREE"))
+        if (commit_n(trees[0], SEC_CM1_N, SEC_CM1_2NS, info.n_cm1, roots[0], "STARK_STEP_1_LDE",
+                     "STARK_STEP_1_EXCHANGE", "STARK_STEP_1_MERKLETREE"))
             return -1;
         tr.put(roots[0], 4);
-        // STAGE 2 (:65-144), n domain on every rank
+        // STAGE 2 (:65-144), n domain on the rank's rows
         tr.get_field(ch + 0);
         tr.get_field(ch + 3);
         tstart();
-        if (run(step2, false, ch, evals.data(), 0)) return -1;
+        if (run_n(step2, st2, ch)) return -1;
         if (tstop("STARK_STEP_2_CALCULATE_EXPS")) return -1;
         if (info.n_pu) {
             tstart();
             if (h1h2_all()) return -1;
             if (tstop("STARK_STEP_2_CALCULATEH1H2")) return -1;
         }
-        if (commit_cols(trees[1], SEC_CM2_2NS, S.sec[SEC_CM2_N], info.n_cm2, roots[1], "STARK_STEP_2_LDE",
-                        "STARK_STEP_2_EXCHANGE", "STARK_STEP_2_MERKLETREE"))
+        if (commit_n(trees[1], SEC_CM2_N, SEC_CM2_2NS, info.n_cm2, roots[1], "STARK_STEP_2_LDE",
+                     "STARK_STEP_2_EXCHANGE", "STARK_STEP_2_MERKLETREE"))
             return -1;
         tr.put(roots[1], 4);
         // STAGE 3 (:146-224)
         tr.get_field(ch + 6);
         tr.get_field(ch + 9);
         tstart();
-        if (run(step3prev, false, ch, evals.data(), 0)) return -1;
+        if (run_n(step3prev, st3p, ch)) return -1;
         if (tstop("STARK_STEP_3_CALCULATE_EXPS")) return -1;
         tstart();
         if (z_all()) return -1;
         if (tstop("STARK_STEP_3_CALCULATE_Z")) return -1;
         if (!step3.instr.empty()) {
             tstart();
-            if (run(step3, false, ch, evals.data(), 0)) return -1;
+            if (run_n(step3, st3, ch)) return -1;
             if (tstop("STARK_STEP_3_CALCULATE_EXPS_2")) return -1;
         }
-        if (commit_cols(trees[2], SEC_CM3_2NS, S.sec[SEC_CM3_N], info.n_cm3, roots[2], "STARK_STEP_3_LDE",
-                        "STARK_STEP_3_EXCHANGE", "STARK_STEP_3_MERKLETREE"))
+        if (commit_n(trees[2], SEC_CM3_N, SEC_CM3_2NS, info.n_cm3, roots[2], "STARK_STEP_3_LDE",
+                     "STARK_STEP_3_EXCHANGE", "STARK_STEP_3_MERKLETREE"))
             return -1;
         tr.put(roots[2], 4);
         // STAGE 4 (:226-296): the quotient on the rank's rows
@@ -438,10 +762,8 @@ public:
         if (tstop("STARK_STEP_5_LEv_LpEv")) return -1;
         tstart();
         {
-            const uint64_t nloc = N / W;
             std::vector<uint64_t> part(3 * info.n_ev), all;
-            if (evmap_rows((uint64_t)R * nloc, nloc, part.data()) || allgather(part.data(), part.size(), all))
-                return -1;
+            if (evmap_rows(r0(), nb, part.data()) || allgather(part.data(), part.size(), all)) return -1;
             for (size_t i = 0; i < evals.size(); i++) {
                 unsigned __int128 acc = 0;
                 for (uint32_t s = 0; s < W; s++) acc += all[s * evals.size() + i];

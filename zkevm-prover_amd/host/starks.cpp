@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -168,6 +169,9 @@ public:
     uint64_t verkey[4];
     std::vector<uint64_t> publics;
     std::vector<std::pair<std::string, double>> timers;
+    // memory plan: with `dry` set, dalloc only adds up the bytes (no device)
+    bool dry = false;
+    uint64_t planned = 0;
 
     virtual ~Starks()
     {
@@ -176,6 +180,11 @@ public:
 
     int dalloc(uint64_t **p, uint64_t elems)
     {
+        if (dry) {
+            planned += elems * 8;
+            *p = (uint64_t *)(uintptr_t)4096;  // never dereferenced: the plan allocates nothing
+            return 0;
+        }
         void *v = nullptr;
         CK(zkgpu_dev_malloc(&v, elems * 8));
         allocs.push_back(v);
@@ -183,14 +192,55 @@ public:
         return 0;
     }
 
+    // HBM a prover of this description holds at its peak: its own buffers
+    // (alloc), the transient setup buffers and the library's grow-only
+    // workspaces (extend_pol's column batches, the NTT scratch, the
+    // expression programs' segment carries, calculateH1H2's table)
+    virtual uint64_t setup_bytes() const { return 0; }
+    virtual uint64_t lde_cols_max() const
+    {
+        return std::max({info.n_cm1, info.n_cm2, info.n_cm3, info.n_const, 1u});
+    }
+    virtual uint64_t prog_rows_max() const { return NE; }
+    int plan(uint64_t *bytes)
+    {
+        dry = true;
+        planned = 0;
+        const int rc = alloc();
+        dry = false;
+        if (rc) return -1;
+        const uint64_t ntt_ws = std::max<uint64_t>(3, info.n_cm4) * NE * 8;  // ntt_dev scratch (workspace slot 1)
+        const uint64_t lde_ws = zkgpu_lde_workspace_bytes(N, NE, lde_cols_max());
+        const uint64_t prog_ws = 64ULL * prog_rows_max() * 8;  // <= 64 carried columns between program segments
+        const uint64_t h1h2_ws = info.n_pu ? 32ULL * N : 0;    // 2N-slot table + counts + scan
+        *bytes = planned + setup_bytes() + std::max(lde_ws, ntt_ws + zkgpu_lde_workspace_bytes(N, NE, 0)) + prog_ws +
+                 h1h2_ws + 24ULL * N;  // + calculateZ scratch
+        planned = 0;
+        return 0;
+    }
+    // fail loudly, before any allocation, when the plan exceeds the free HBM
+    int check_budget()
+    {
+        uint64_t need = 0, avail = 0, total = 0;
+        if (plan(&need)) return -1;
+        CK(zkgpu_device_memory(&avail, &total));
+        if (need > avail)
+            return fail("stark_create: this prover needs %.1f GB of HBM per GPU (%u-row trace, %u/%u/%u/%u committed "
+                        "columns, %u constants), the device has %.1f GB free of %.1f GB",
+                        need / 1e9, (unsigned)N, info.n_cm1, info.n_cm2, info.n_cm3, info.n_cm4, info.n_const,
+                        avail / 1e9, total / 1e9);
+        return 0;
+    }
+
     int create(const zkgpu_stark_info *in)
     {
-        if (load(in) || alloc()) return -1;
+        if (load(in) || check_budget() || alloc()) return -1;
         return build_const();
     }
 
-    // validate the description, keep the programs, bind the device
-    int load(const zkgpu_stark_info *in)
+    // validate the description, keep the programs, bind the device (init =
+    // false: the memory plan only, no GPU)
+    int load(const zkgpu_stark_info *in, bool init = true)
     {
         info = *in;
         random_cols.assign(in->random_cols, in->random_cols + in->n_random_cols);
@@ -244,7 +294,7 @@ public:
         N = 1ULL << in->n_bits;
         NE = 1ULL << in->n_bits_ext;
         eb = in->n_bits_ext - in->n_bits;
-        CK(zkgpu_init(-1));
+        if (init) CK(zkgpu_init(-1));
         return 0;
     }
 
@@ -297,10 +347,11 @@ public:
         return 0;
     }
 
-    int build_const()
+    // constants (setup): pseudo-random columns, L_first = [1, 0, ...], then
+    // step0, on the whole n domain of S.sec[SEC_CONST_N] (ld N)
+    int fill_const()
     {
         const zkgpu_stark_info *in = &info;
-        // constants (setup): pseudo-random columns, L_first = [1, 0, ...], then step0
         CK(zkgpu_memset_dev(S.sec[SEC_CONST_N], 0, (uint64_t)in->n_const * N * 8));
         if (!random_const.empty())
             CK(zkgpu_rand_cols_dev(S.sec[SEC_CONST_N], N, random_const.data(), (uint32_t)random_const.size(), N,
@@ -311,9 +362,17 @@ public:
             uint64_t ch0[24] = {0}, ev0[3] = {0, 0, 0};
             if (run(step0, false, ch0, ev0, 0)) return -1;
         }
-        if (commit_const()) return -1;
-        publics.resize(in->n_publics);
-        for (uint32_t k = 0; k < in->n_publics; k++) publics[k] = rand_u64(in->seed, 2, k, 0);
+        return 0;
+    }
+    void init_publics()
+    {
+        publics.resize(info.n_publics);
+        for (uint32_t k = 0; k < info.n_publics; k++) publics[k] = rand_u64(info.seed, 2, k, 0);
+    }
+    virtual int build_const()
+    {
+        if (fill_const() || commit_const()) return -1;
+        init_publics();
         return 0;
     }
 
@@ -326,7 +385,7 @@ public:
         return 0;
     }
 
-    int witness()
+    virtual int witness()
     {
         CK(zkgpu_memset_dev(S.sec[SEC_CM1_N], 0, (uint64_t)info.n_cm1 * N * 8));
         CK(zkgpu_rand_cols_dev(S.sec[SEC_CM1_N], N, random_cols.data(), (uint32_t)random_cols.size(), N, info.seed, 0));
@@ -337,7 +396,7 @@ public:
         return 0;
     }
 
-    int set_cm1(const uint64_t *rows)
+    virtual int set_cm1(const uint64_t *rows)
     {
         void *tmp = nullptr;
         CK(zkgpu_dev_malloc(&tmp, (uint64_t)info.n_cm1 * N * 8));
@@ -351,7 +410,7 @@ public:
 
     // constant polynomials from the reference's .const file layout (N rows x
     // nConstants, ConstantPolsStarks, starks.hpp:94-116), their LDE and tree
-    int set_const(const uint64_t *rows)
+    virtual int set_const(const uint64_t *rows)
     {
         void *tmp = nullptr;
         CK(zkgpu_dev_malloc(&tmp, (uint64_t)(info.n_const ? info.n_const : 1) * N * 8));
@@ -501,7 +560,7 @@ public:
     }
 
     // calculateH1H2 of every plookup (starks.cpp:104-127), n domain
-    int h1h2_all()
+    virtual int h1h2_all()
     {
         for (uint32_t k = 0; k < info.n_pu; k++) {
             const uint32_t *q = &pu[5 * k];
@@ -569,6 +628,16 @@ public:
         return 0;
     }
 
+    // the n-domain values of an evMap entry's polynomial (section_2ns ev_sec,
+    // column col) from global row `row` on, and their leading dimension
+    virtual const uint64_t *ncol(uint32_t ev_sec, uint32_t col, uint64_t row, uint64_t &ld) const
+    {
+        ld = N;
+        if (ev_sec == SEC_CM4_2NS) return cm4_n + (uint64_t)col * N + row;
+        const uint32_t s = ev_sec == SEC_CONST_2NS ? (uint32_t)SEC_CONST_N : ev_sec - SEC_CM1_2NS + SEC_CM1_N;
+        return S.sec[s] + (uint64_t)col * N + row;
+    }
+
     // Starks::evmap over n-domain rows [k0, k0 + nrows) (starks.cpp:556-669;
     // the row sum is linear, so row blocks give partial sums)
     int evmap_rows(uint64_t k0, uint64_t nrows, uint64_t *evals_out)
@@ -577,12 +646,7 @@ public:
         std::vector<uint64_t> lds(info.n_ev);
         std::vector<uint32_t> dims(info.n_ev), primes(info.n_ev);
         for (uint32_t e = 0; e < info.n_ev; e++) {
-            const uint32_t sec = ev[4 * e];
-            const uint64_t *base = sec == SEC_CM4_2NS ? cm4_n
-                                   : sec == SEC_CONST_2NS ? S.sec[SEC_CONST_N]
-                                                          : S.sec[sec - SEC_CM1_2NS + SEC_CM1_N];
-            cols[e] = base + (uint64_t)ev[4 * e + 1] * N + k0;
-            lds[e] = N;
+            cols[e] = ncol(ev[4 * e], ev[4 * e + 1], k0, lds[e]);
             dims[e] = ev[4 * e + 2];
             primes[e] = ev[4 * e + 3];
         }
@@ -805,6 +869,20 @@ int zkgpu_stark_create_sharded(void **handle, const zkgpu_stark_info *info, cons
     }
     *handle = s;
     return 0;
+}
+
+int zkgpu_stark_memory_plan(const zkgpu_stark_info *info, uint32_t world, uint64_t *bytes_per_gpu)
+{
+    if (!info || !bytes_per_gpu) return zkgpu_host::fail("stark_memory_plan: null argument");
+    *bytes_per_gpu = 0;
+    if (world == 0) {
+        Starks s;
+        if (s.load(info, false)) return -1;
+        return s.plan(bytes_per_gpu);
+    }
+    ShardedStarks s;
+    if (s.shape(info, world, 0, false)) return -1;
+    return s.plan(bytes_per_gpu);
 }
 
 int zkgpu_comm_rccl_unique_id(uint8_t id[128])

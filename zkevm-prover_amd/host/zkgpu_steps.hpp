@@ -20,9 +20,19 @@
 //                                                    starkInfo.starkStruct.nBitsExt, starkInfo.nPublics, progs);
 //     starkZkevm->genProof(fproof, publics, zkevmVerkey, &zkevmSteps);   // prover.cpp:577
 // where `map` lists the StarkInfo sections (mapOffsets / mapSectionsN,
-// stark_info.cpp:473-482) as zkgpu_pols_section entries.  The per-row entry
-// points (step*_first / _i / _last) belong to the non-parser code path
-// (definitions.hpp:79-90 selects the parsers for zkEVM) and fail loudly here.
+// stark_info.cpp:473-482) as zkgpu_pols_section entries.  Every whole-domain
+// entry point of the interface -- _parser_first_avx / _avx512 and the
+// scalar _parser_first / _avx_jump variants (steps.hpp:39-56; the jump tables
+// of zkevm.chelpers.step3.parser.cpp:978 / step42ns.parser.cpp:1475 evaluate
+// the same bytecode) -- runs the program on the GPU; none is the base class's
+// silent no-op.  The per-row entry points (step*_first / _i / _last) belong to
+// the non-parser code path (definitions.hpp:79-90 selects the parsers for
+// zkEVM) and fail loudly.
+//
+// keep_mirrors(true): sections stay on the device between calls
+// (zkgpu_steps_mirror); the caller invalidates a section its own code writes
+// (invalidate(section pointer), see include/zkgpu_parser.h for the genProof
+// call sites).
 //
 // Errors follow the reference (zklog.error + exitProcess, exit_process.cpp:7)
 // through zkgpu::error_handler() of host/zkgpu_goldilocks.hpp.
@@ -76,6 +86,23 @@ public:
     void step52ns_parser_first_avx512(Params &p, uint64_t nrows, uint64_t) override
     {
         run(ZKGPU_STEP52NS, p, nrows);
+    }
+    // the scalar and jump-table variants of the same evaluations
+    void step3_parser_first(Params &p, uint64_t nrows, uint64_t) override { run(ZKGPU_STEP3, p, nrows); }
+    void step3_parser_first_avx_jump(Params &p, uint64_t nrows, uint64_t) override { run(ZKGPU_STEP3, p, nrows); }
+    void step42ns_parser_first(Params &p, uint64_t nrows, uint64_t) override { run(ZKGPU_STEP42NS, p, nrows); }
+    void step42ns_parser_first_avx_jump(Params &p, uint64_t nrows, uint64_t) override
+    {
+        run(ZKGPU_STEP42NS, p, nrows);
+    }
+    void step52ns_parser_first(Params &p, uint64_t nrows, uint64_t) override { run(ZKGPU_STEP52NS, p, nrows); }
+
+    // device mirrors of the sections between calls (include/zkgpu_parser.h)
+    void keep_mirrors(bool on) { check(zkgpu_steps_mirror(on ? 1 : 0), "StepsGPU::keep_mirrors"); }
+    template <typename E>
+    void invalidate(const E *section)
+    {
+        check(zkgpu_steps_invalidate(section), "StepsGPU::invalidate");
     }
 
     // per-row entry points of the non-parser path: not offered on the GPU

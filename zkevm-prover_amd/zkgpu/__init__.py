@@ -72,6 +72,10 @@ _SIGS = {
     "zkgpu_memcpy_d2d": (ctypes.c_int, [vp, vp, u64]),
     "zkgpu_memset_dev": (ctypes.c_int, [vp, ctypes.c_int, u64]),
     "zkgpu_rand_cols_dev": (ctypes.c_int, [vp, u64, vp, u32, u64, u64, u64]),
+    "zkgpu_rand_cols_rows_dev": (ctypes.c_int, [vp, u64, vp, u32, u64, u64, u32, u64, u64]),
+    "zkgpu_copy_rows_dev": (ctypes.c_int, [vp, u64, u64, vp, vp, u64, u64, u32, vp, u32, u64]),
+    "zkgpu_device_memory": (ctypes.c_int, [pu64, pu64]),
+    "zkgpu_lde_workspace_bytes": (u64, [u64, u64, u64]),
     "zkgpu_zxp_eval_dev": (ctypes.c_int, [vp, u32, vp, u32, u32, u32, vp, u32, vp, vp, u32, vp, u32, vp, vp, u32,
                                           u64]),
     "zkgpu_zxp_compile": (ctypes.c_int, [vp, u32, vp, u32, u32, u32, vp, vp, u32, vp, u32, u32, vp]),

@@ -76,6 +76,8 @@ def slib():
             ("zkgpu_stark_last_error", ctypes.c_char_p, []),
             ("zkgpu_stark_create_sharded", ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(_Info),
                                                           ctypes.POINTER(Comm)]),
+            ("zkgpu_stark_memory_plan", ctypes.c_int, [ctypes.POINTER(_Info), ctypes.c_uint32,
+                                                       ctypes.POINTER(u64)]),
             ("zkgpu_comm_rccl_unique_id", ctypes.c_int, [vp]),
             ("zkgpu_comm_rccl_create", ctypes.c_int, [ctypes.POINTER(Comm), vp, ctypes.c_uint32, ctypes.c_uint32]),
             ("zkgpu_comm_rccl_destroy", None, [ctypes.POINTER(Comm)]),
@@ -224,38 +226,55 @@ class HostStagedComm:
         pass
 
 
+def make_info(inst, keep):
+    """zkgpu_stark_info of a SyntheticStark instance; the arrays it points
+    into are appended to `keep` (they must outlive the struct)."""
+    info = _Info()
+    info.n_bits, info.n_bits_ext, info.n_queries = inst.n_bits, inst.n_bits_ext, inst.n_queries
+    info.n_fri_steps = len(inst.fri_steps)
+    for i, s in enumerate(inst.fri_steps):
+        info.fri_steps[i] = s
+    info.n_cm1, info.n_cm2, info.n_cm3, info.n_cm4 = inst.n_cm1, inst.n_cm2, inst.n_cm3, inst.n_cm4
+    info.n_tmp, info.n_const, info.n_publics = inst.n_tmp, inst.n_const, inst.n_publics
+    info.q_deg, info.l_first, info.n_k, info.seed = inst.q_deg, inst.l_first, inst.n_k, inst.seed
+    rc = np.array(inst.random_cm1_cols(), np.uint32)
+    zc = np.array(inst.z_ctx, np.uint32).reshape(-1)
+    ev = np.array(inst.evmap, np.uint32).reshape(-1)
+    rk = np.array(inst.random_const_cols(), np.uint32)
+    pu = np.array(inst.pu, np.uint32).reshape(-1)
+    keep += [rc, zc, ev, rk, pu]
+    info.n_random_const, info.random_const = rk.size, rk.ctypes.data
+    info.n_pu, info.pu = len(inst.pu), (pu.ctypes.data if pu.size else None)
+    info.n_random_cols, info.random_cols = rc.size, rc.ctypes.data
+    info.n_zctx, info.zctx = len(inst.z_ctx), zc.ctypes.data
+    info.n_ev, info.ev = len(inst.evmap), ev.ctypes.data
+    for name in ("step0", "step1", "step2", "step3prev", "step3", "step42ns", "step52ns"):
+        prog = inst.programs.get(name)
+        if prog is None:
+            continue
+        ins, opn = prog.arrays()
+        ins, opn = np.ascontiguousarray(ins), np.ascontiguousarray(opn)
+        keep += [ins, opn]
+        setattr(info, name, _Prog(ins.ctypes.data, ins.shape[0], opn.ctypes.data, opn.shape[0],
+                                  max(prog.n_tmp1, 1), max(prog.n_tmp3, 1)))
+    return info
+
+
+def memory_plan(inst, world=0):
+    """HBM bytes per GPU of a prover of this instance (zkgpu_stark_memory_plan:
+    world 0 = one GPU, W = row-sharded over W ranks); no GPU needed."""
+    keep = []
+    info = make_info(inst, keep)
+    out = ctypes.c_uint64(0)
+    _check(slib().zkgpu_stark_memory_plan(ctypes.byref(info), world, ctypes.byref(out)), "zkgpu_stark_memory_plan")
+    return out.value
+
+
 class GpuStark:
     def __init__(self, inst, comm=None):
         self.inst = inst
         self._keep = []
-        info = _Info()
-        info.n_bits, info.n_bits_ext, info.n_queries = inst.n_bits, inst.n_bits_ext, inst.n_queries
-        info.n_fri_steps = len(inst.fri_steps)
-        for i, s in enumerate(inst.fri_steps):
-            info.fri_steps[i] = s
-        info.n_cm1, info.n_cm2, info.n_cm3, info.n_cm4 = inst.n_cm1, inst.n_cm2, inst.n_cm3, inst.n_cm4
-        info.n_tmp, info.n_const, info.n_publics = inst.n_tmp, inst.n_const, inst.n_publics
-        info.q_deg, info.l_first, info.n_k, info.seed = inst.q_deg, inst.l_first, inst.n_k, inst.seed
-        rc = np.array(inst.random_cm1_cols(), np.uint32)
-        zc = np.array(inst.z_ctx, np.uint32).reshape(-1)
-        ev = np.array(inst.evmap, np.uint32).reshape(-1)
-        rk = np.array(inst.random_const_cols(), np.uint32)
-        pu = np.array(inst.pu, np.uint32).reshape(-1)
-        self._keep += [rc, zc, ev, rk, pu]
-        info.n_random_const, info.random_const = rk.size, rk.ctypes.data
-        info.n_pu, info.pu = len(inst.pu), (pu.ctypes.data if pu.size else None)
-        info.n_random_cols, info.random_cols = rc.size, rc.ctypes.data
-        info.n_zctx, info.zctx = len(inst.z_ctx), zc.ctypes.data
-        info.n_ev, info.ev = len(inst.evmap), ev.ctypes.data
-        for name in ("step0", "step1", "step2", "step3prev", "step3", "step42ns", "step52ns"):
-            prog = inst.programs.get(name)
-            if prog is None:
-                continue
-            ins, opn = prog.arrays()
-            ins, opn = np.ascontiguousarray(ins), np.ascontiguousarray(opn)
-            self._keep += [ins, opn]
-            setattr(info, name, _Prog(ins.ctypes.data, ins.shape[0], opn.ctypes.data, opn.shape[0],
-                                      max(prog.n_tmp1, 1), max(prog.n_tmp3, 1)))
+        info = make_info(inst, self._keep)
         self._info = info
         self.h = ctypes.c_void_p()
         self.comm = comm

@@ -29,6 +29,16 @@ Starks::genProof (starks.cpp:9-404):
                  + Horner_v2(p' - p(w xi)) x/(x - w xi)                (step52ns form)
   FRI        FRIProve::prove (friProve.cpp), queries on the 5 trees.
 
+Width fillers (n_free2 / n_free_tmp / n_free3; the fork-9 widths 751 / 168 /
+408 / 389 tmpExp / 234 constants, commit_pols.hpp:1736-1737):
+extra committed / tmpExp columns derived row-locally by the stage programs --
+step2: cm2 fillers from cm1 (one factor at the next row) and the constants;
+step3prev: tmpExp fillers from the cm2 fillers at the next row; step3: cm3
+fillers from the tmpExp fillers at the next row, every other one stored at
+the next row (the shifted stores of step3.parser.cpp opcodes 101-114).  They
+are committed, evaluated (evMap) and enter the FRI polynomial like every
+committed column; no constraint reads them.
+
 The constraint/expression programs are emitted in the ZXP format
 (include/zkgpu_zxp.h) and evaluated by the GPU expression kernel (product) and
 by the oracle's C evaluator (tests).  The instance is valid: a correct prover
@@ -101,7 +111,7 @@ class Program:
 
 class SyntheticStark:
     def __init__(self, n_bits=10, blowup_bits=1, t=4, m=2, n_k=3, n_queries=16, fri_steps=None, n_publics=8,
-                 seed=0x5EED, n_free=0, n_lookups=2, q_deg=2, with_step3=True):
+                 seed=0x5EED, n_free=0, n_lookups=2, q_deg=2, with_step3=True, n_free2=0, n_free3=0, n_free_tmp=0):
         self.n_bits = n_bits
         self.n_bits_ext = n_bits + blowup_bits
         self.blowup_bits = blowup_bits
@@ -128,14 +138,18 @@ class SyntheticStark:
             cm2 += 2 * d
             tmp += 2 * d + 6
             cm3 += 3
-        self.n_cm2 = cm2
+        self.cm2_free = list(range(cm2, cm2 + n_free2))
+        self.n_cm2 = cm2 + n_free2
         # post-Z stage-3 column (starks.cpp:193-208: step3 runs after calculateZ
         # and writes cm3/tmpExp columns that depend on Z): W = Z_0 * a_0 + K_0
         # (an F_p^3 column: the verifier only sees whole evaluations of Z)
         self.with_step3 = bool(with_step3)
         self.cm3_w = cm3 if self.with_step3 else None
-        self.n_cm3 = cm3 + (3 if self.with_step3 else 0)
-        self.n_tmp = tmp
+        cm3 += 3 if self.with_step3 else 0
+        self.cm3_free = list(range(cm3, cm3 + n_free3))
+        self.n_cm3 = cm3 + n_free3
+        self.tmp_free = list(range(tmp, tmp + n_free_tmp))
+        self.n_tmp = tmp + n_free_tmp
         # quotient pieces: the constraints have degree <= 3, so pieces >= 2 are
         # zero polynomials; q_deg > 2 (blowup >= 4) still exercises the split
         assert 2 <= q_deg <= (1 << blowup_bits)
@@ -194,6 +208,12 @@ class SyntheticStark:
             ev.append((SEC_CM3_2NS, lk["z"], 3, 1))
         if self.with_step3:
             ev.append((SEC_CM3_2NS, self.cm3_w, 3, 0))
+        for j, c in enumerate(self.cm2_free):
+            ev.append((SEC_CM2_2NS, c, 1, 0))
+            if j % 4 == 0:
+                ev.append((SEC_CM2_2NS, c, 1, 1))
+        for c in self.cm3_free:
+            ev.append((SEC_CM3_2NS, c, 1, 0))
         for p in range(self.q_deg):
             ev.append((SEC_CM4_2NS, 3 * p, 3, 0))
         self.evmap = ev
@@ -303,6 +323,12 @@ class SyntheticStark:
             f, t = self._lk_ft(p, k, SEC_CM1_N, SEC_CONST_N, 0)
             p.op(COPY, self._lk_col(p, SEC_TMP_N, lk["f"], lk["dim"]), f)
             p.op(COPY, self._lk_col(p, SEC_TMP_N, lk["t"], lk["dim"]), t)
+        # cm2 fillers: a * b' + K
+        if self.cm2_free:
+            r = p.tmp1()
+            for j, c in enumerate(self.cm2_free):
+                p.op(MUL, r, p.col(SEC_CM1_N, (7 * j) % self.n_cm1), p.col(SEC_CM1_N, (13 * j + 5) % self.n_cm1, 1))
+                p.op(ADD, p.col(SEC_CM2_N, c), r, p.col(SEC_CONST_N, j % self.n_const))
         return p
 
     def _prog_step3prev(self):
@@ -325,6 +351,11 @@ class SyntheticStark:
             h1n = self._lk_col(p, SEC_CM2_N, lk["h1"], d, 1)
             self._emit_lk_num_den(p, lk, f, tt, tn, h1, h2, h1n, p.col3(SEC_TMP_N, lk["num"]),
                                   p.col3(SEC_TMP_N, lk["den"]))
+        # tmpExp fillers: (cm2 filler)' + a
+        for j, c in enumerate(self.tmp_free):
+            src = (p.col(SEC_CM2_N, self.cm2_free[j % len(self.cm2_free)], 1) if self.cm2_free
+                   else p.col(SEC_CM1_N, j % self.n_cm1, 1))
+            p.op(ADD, p.col(SEC_TMP_N, c), src, p.col(SEC_CM1_N, (11 * j) % self.n_cm1))
         return p
 
     def _prog_step3(self):
@@ -336,6 +367,14 @@ class SyntheticStark:
         z0 = self.z_ctx[0][2]
         p.op(MUL, t, p.col3(SEC_CM3_N, z0), p.col(SEC_CM1_N, 0))
         p.op(ADD, p.col3(SEC_CM3_N, self.cm3_w), t, p.col(SEC_CONST_N, 0))
+        # cm3 fillers: (tmpExp filler)' * a + K, odd ones stored at the next row
+        if self.cm3_free:
+            r = p.tmp1()
+            for j, c in enumerate(self.cm3_free):
+                src = (p.col(SEC_TMP_N, self.tmp_free[j % len(self.tmp_free)], 1) if self.tmp_free
+                       else p.col(SEC_CM1_N, j % self.n_cm1, 1))
+                p.op(MUL, r, src, p.col(SEC_CM1_N, (17 * j + 1) % self.n_cm1))
+                p.op(ADD, p.col(SEC_CM3_N, c, j % 2), r, p.col(SEC_CONST_N, (3 * j) % self.n_const))
         return p
 
     def constraints(self, p, nxt):
@@ -439,6 +478,8 @@ class SyntheticStark:
         cols += [(SEC_CM3_2NS, lk["z"], 3) for lk in self.lookups]
         if self.with_step3:
             cols += [(SEC_CM3_2NS, self.cm3_w, 3)]
+        cols += [(SEC_CM2_2NS, c, 1) for c in self.cm2_free]
+        cols += [(SEC_CM3_2NS, c, 1) for c in self.cm3_free]
         cols += [(SEC_CM4_2NS, 3 * q, 3) for q in range(self.q_deg)]
         return cols
 
@@ -485,6 +526,19 @@ class SyntheticStark:
             "randomCm1Cols": self.random_cm1_cols(), "randomConst": self.random_const_cols(),
             "zCtx": self.z_ctx, "puCtx": self.pu, "evMap": self.evmap,
         }
+
+    @classmethod
+    def fork9(cls, n_bits=10, **kw):
+        """The fork-9 zkEVM widths (commit_pols.hpp:1736-1737):
+        cm1 / cm2 / cm3 / cm4 = 751 / 168 / 408 / 6 committed columns, 234
+        constants, 389 tmpExp columns, two plookups, blowup 2."""
+        a = dict(n_bits=n_bits, blowup_bits=1, t=4, m=2, n_k=230, n_free=736, n_lookups=2, q_deg=2,
+                 n_free2=154, n_free3=393, n_free_tmp=357, n_queries=8)
+        a.update(kw)
+        inst = cls(**a)
+        assert (inst.n_cm1, inst.n_cm2, inst.n_cm3, inst.n_cm4, inst.n_const, inst.n_tmp) == \
+            (751, 168, 408, 6, 234, 389), "fork-9 widths"
+        return inst
 
     def random_cm1_cols(self):
         return [c for c in range(3 * self.t + self.n_free) if c >= 3 * self.t or c % 3 != 2]
