@@ -73,6 +73,9 @@ def parse():
                          "configs[4] (one proof over all ranks, strong scaling); step42ns = the quotient program of "
                          "the reference's zkEVM shape on the 2^(log_n+1) extended domain")
     ap.add_argument("--queries", type=int, default=128)
+    ap.add_argument("--fork9", action="store_true",
+                    help="stark / stark-sharded: the fork-9 widths (751/168/408/6 committed, 234 constants, 389 "
+                         "tmpExp; SyntheticStark.fork9) instead of config-4's")
     ap.add_argument("--s42-scale", type=float, default=1.0,
                     help="step42ns workload: fraction of the reference step42ns opcode counts")
     ap.add_argument("--s42-jit", action="store_true", help="step42ns workload: the compiled kernel (else interpreter)")
@@ -88,10 +91,10 @@ def parse():
 
 
 # ---------------------------------------------------------------- instances
-def stark_instance(log_n, blow, ncols, n_queries):
+def stark_instance(log_n, blow, ncols, n_queries, fork9=False):
     """cm1 = ncols, cm2 = 26, cm3 = 27, cm4 = 6, 30
     constants, qDeg 2, FRI steps [nBitsExt, -4, ..., 5], n_queries queries
-    (synthetic AIR, zkgpu/synthetic.py)."""
+    (synthetic AIR, zkgpu/synthetic.py); fork9: the zkEVM's widths."""
     from zkgpu.synthetic import SyntheticStark
     nbe = log_n + blow
     steps = [nbe]
@@ -99,6 +102,8 @@ def stark_instance(log_n, blow, ncols, n_queries):
         steps.append(steps[-1] - 4)
     if steps[-1] > 5:
         steps.append(5)
+    if fork9:
+        return SyntheticStark.fork9(n_bits=log_n, n_queries=n_queries, fri_steps=steps)
     # cm1 = 3t constrained triples + free columns + 3 lookup columns (A, B, C);
     # cm2 = 6 h groups (18) + plookup h1/h2 (3+3+1+1) = 26; cm3 = 18 + 2 plookup
     # Z + the step3 column W = 27; constants = 26 K + L_first + 3 tables = 30
@@ -612,7 +617,7 @@ def main():
                 sc.commit(trace)
         elif args.workload == "stark":
             from zkgpu.stark import GpuStark
-            inst = stark_instance(args.log_n, args.blowup_bits, C, args.queries)
+            inst = stark_instance(args.log_n, args.blowup_bits, C, args.queries, args.fork9)
             gs = GpuStark(inst)  # setup: constants, constant LDE + tree (untimed; files in the reference)
             gs.witness()         # executor stand-in: committed trace cm1 in HBM (untimed)
 
@@ -629,7 +634,7 @@ def main():
         elif args.workload == "stark-sharded":
             # the C++ row-sharded prover (host/sharded_starks.hpp) over RCCL
             from zkgpu.stark import GpuStark, RcclComm
-            inst = stark_instance(args.log_n, args.blowup_bits, C, args.queries)
+            inst = stark_instance(args.log_n, args.blowup_bits, C, args.queries, args.fork9)
             comm = RcclComm()
             gs = GpuStark(inst, comm=comm)
             gs.witness()
@@ -691,8 +696,10 @@ def main():
                            inst.fri_steps, args.queries))
             parallelism = "replicas x%d (one independent proof per GPU)" % world
         elif args.workload == "stark-sharded":
-            workload = ("ONE config-4 STARK proof (2^%d trace, %d cm1 cols, %d queries) row-sharded over %d rank(s)"
-                        % (args.log_n, C, args.queries, world))
+            workload = ("ONE %s STARK proof (2^%d trace, cm1/cm2/cm3/cm4 = %d/%d/%d/%d, %d constants, %d queries) "
+                        "row-sharded over %d rank(s): n and 2n domains by rows, NTT-transpose all-to-all per commit"
+                        % ("fork-9-width" if args.fork9 else "config-4", args.log_n, inst.n_cm1, inst.n_cm2,
+                           inst.n_cm3, inst.n_cm4, inst.n_const, args.queries, world))
             parallelism = ("one proof, extended domain row-sharded x%d (%s): RCCL exchange column->row blocks + "
                            "halo rows per commit, q/f row gathers" % (world, "C++ prover, host/sharded_starks.hpp"
                                                                      if args.sharded_impl == "cpp" else
