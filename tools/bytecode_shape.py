@@ -10,6 +10,14 @@ tests/golden/zkevm_bytecode_shape.json, from which
 zkgpu/synthetic_bytecode.py builds programs of the same shape for the GPU
 tests and the step42ns bench (the GPU box has no reference tree).
 
+The column reads' locality is kept as a statistic too ("reuse"): in
+program order, every read of a column (memory-map section or constant) is
+either a first touch or a re-read at some LRU stack distance (the number of
+distinct columns read since this one was last read).  The histogram of those
+distances, in power-of-two buckets, lets the generator reproduce how closely
+the reference's programs cluster their re-reads -- which decides how many of
+the compiled kernels' column loads hit the L2.
+
 Usage: tools/bytecode_shape.py [out.json]
 """
 import collections
@@ -34,6 +42,34 @@ def section_of(off, stride):
     raise ValueError((off, stride))
 
 
+class Lru:
+    """LRU stack of keys: access(k) -> stack distance (None on first touch)"""
+
+    def __init__(self):
+        self.stack = []  # most recent last
+
+    def access(self, k):
+        try:
+            i = self.stack.index(k)
+        except ValueError:
+            self.stack.append(k)
+            return None
+        d = len(self.stack) - 1 - i
+        self.stack.pop(i)
+        self.stack.append(k)
+        return d
+
+
+def reuse_hist(dists, first):
+    """{"first": first touches, "buckets": counts of d in [0], [1], [2, 3], [4, 7], ...}"""
+    b = [0] * 16
+    for d in dists:
+        b[min(15, d.bit_length())] += 1
+    while b and b[-1] == 0:
+        b.pop()
+    return {"first": first, "buckets": b}
+
+
 def shape(name, isa):
     ops, args = parser_isa.load_bytecode(name)
     table = isa[name]
@@ -43,6 +79,15 @@ def shape(name, isa):
     writes = collections.defaultdict(collections.Counter)
     shifts, moduli = collections.Counter(), collections.Counter()
     chal, pub, ev, kcols = collections.Counter(), set(), set(), set()
+    lru, dists, first = Lru(), [], 0
+
+    def touch(key):
+        nonlocal first
+        d = lru.access(key)
+        if d is None:
+            first += 1
+        else:
+            dists.append(d)
     ia = 0
     for o in ops:
         e = table[int(o)]
@@ -56,11 +101,14 @@ def shape(name, isa):
                     sec, col = section_of(off, stride)
                     for c in range(x[1]):
                         (writes if role == "w" else reads)[sec][col + c] += 1
+                    if role == "r":
+                        touch((sec, col))
                     if k == "PS":
                         shifts[int(args[ia + x[3]])] += 1
                         moduli[int(args[ia + x[4]])] += 1
                 elif k in ("K", "KS"):
                     kcols.add(int(args[ia + x[1]]))
+                    touch(("const", int(args[ia + x[1]])))
                     if k == "KS":
                         shifts[int(args[ia + x[2]])] += 1
                         moduli[int(args[ia + x[3]])] += 1
@@ -83,6 +131,7 @@ def shape(name, isa):
         "challenges": {str(k): v for k, v in sorted(chal.items())},
         "max_public": max(pub) if pub else None, "n_evals_used": len(ev), "max_eval": max(ev) if ev else None,
         "const_cols": len(kcols),
+        "reuse": reuse_hist(dists, first),
     }
 
 

@@ -11,7 +11,12 @@ fork-9 memory map:
   * body: the non-chain opcodes in random order, operands drawn like the
     reference's (columns of the map's sections in proportion to its reads,
     next-row accesses at the program's row shift, constants, literals,
-    challenges 0-3, publics);
+    challenges 0-3, publics); step42ns draws its columns and constants with
+    the reference's locality -- first touches and re-reads at LRU stack
+    distances sampled from the "reuse" histogram (tools/bytecode_shape.py),
+    so the compiled kernels find as many re-reads in the caches as the
+    reference's program would (uniform draws re-read columns ~15x farther
+    apart);
   * results: a fraction of the base-field values are constraint results,
     folded into an F_p^3 accumulator by the fused Horner opcodes (step42ns
     84 / 87: acc = (acc + c) * challenges[4]) -- interleaved with the body so
@@ -96,6 +101,35 @@ class _Gen:
         return self.map[s]["offset"] + c, width
 
 
+class _Reuse:
+    """Column / constant keys drawn with a program's reuse statistics
+    (shape["programs"][name]["reuse"]): a first touch with the reference's
+    first-touch fraction, else the key at an LRU stack distance from its
+    power-of-two histogram."""
+
+    def __init__(self, stats, rng, new_key, p_first=None):
+        self.rng = rng
+        self.new_key = new_key  # () -> a key, preferring ones not touched yet
+        b = np.array(stats["buckets"], float)
+        self.p_first = stats["first"] / (stats["first"] + b.sum()) if p_first is None else p_first
+        self.bp = b / b.sum()
+        self.stack = []  # most recent last
+
+    def draw(self):
+        k = None
+        if self.stack and self.rng.random() >= self.p_first:
+            b = int(self.rng.choice(len(self.bp), p=self.bp))
+            d = 0 if b == 0 else int(self.rng.integers(1 << (b - 1), 1 << b))
+            if d < len(self.stack):
+                k = self.stack[len(self.stack) - 1 - d]
+        if k is None:
+            k = self.new_key()
+        if k in self.stack:
+            self.stack.remove(k)
+        self.stack.append(k)
+        return k
+
+
 def generate(name="step42ns", seed=1, shape=None, isa=None, scale=1.0):
     """(ops, args) uint64 arrays of a synthetic program shaped like the
     reference's `name` program: step42ns (constraint quotient), step2prev /
@@ -128,6 +162,35 @@ def _generate_step42ns(seed=1, shape=None, isa=None, scale=1.0):
     g = _Gen(name, shape, rng)
     hist = {int(k): max(1, int(round(v * scale))) for k, v in g.sh["opcode_hist"].items()}
     n84, n87 = hist.pop(84, 0), hist.pop(87, 0)
+    # columns / constants with the reference's locality (first touches from a
+    # shuffled pool per section, then any column of the section's subset)
+    pools = {s: list(rng.permutation(g.rcols[s])) for s in g.rsecs}
+
+    def new_col():
+        s = g.rsecs[rng.choice(len(g.rsecs), p=g.rprob)]
+        c = int(pools[s].pop()) if pools[s] else int(g.rcols[s][rng.integers(len(g.rcols[s]))])
+        return (s, c)
+    kpool = list(rng.permutation(g.n_const))
+
+    def new_const():
+        return int(kpool.pop()) if kpool else int(rng.integers(g.n_const))
+    reuse = g.sh.get("reuse")
+    # first touches at the rate that reads every column of the reference's
+    # distinct sets once over the program's column reads
+    n_pool = sum(len(p_) for p_ in pools.values())
+    n_reads = scale * sum(g.sh["reads"][s]["accesses"] for s in g.rsecs)
+    rcol = _Reuse(reuse, rng, new_col, min(1.0, n_pool / max(n_reads, 1.0))) if reuse else None
+    rconst = _Reuse(reuse, rng, new_const) if reuse else None
+
+    def col(dim):
+        if rcol is None:
+            return g.col(dim)
+        s, c = rcol.draw()
+        width = g.map[s]["width"]
+        return g.map[s]["offset"] + min(c, width - dim), width
+
+    def const():
+        return rconst.draw() if rconst else int(rng.integers(g.n_const))
     hist.pop(69, None)
     body = np.repeat(np.array(list(hist), np.int64), list(hist.values()))
     rng.shuffle(body)
@@ -168,7 +231,7 @@ def _generate_step42ns(seed=1, shape=None, isa=None, scale=1.0):
     # the previous row's value
     for _ in range(4):
         s_ = free1.pop(0)
-        off, w = g.col(1)
+        off, w = col(1)
         ops.append(79)
         args.extend([s_, off, w])
         written1.append(s_)
@@ -209,7 +272,7 @@ def _generate_step42ns(seed=1, shape=None, isa=None, scale=1.0):
                     if s_ is not None:
                         released3.append(s_)
                 elif k in ("P", "PS"):
-                    off, w = g.col(o[1])
+                    off, w = col(o[1])
                     put(o[2], off)
                     if k == "P":
                         put(o[3], w)
@@ -218,9 +281,9 @@ def _generate_step42ns(seed=1, shape=None, isa=None, scale=1.0):
                         put(o[4], g.dom)
                         put(o[5], w)
                 elif k == "K":
-                    put(o[2], rng.integers(g.n_const))
+                    put(o[2], const())
                 elif k == "KS":
-                    put(o[2], rng.integers(g.n_const))
+                    put(o[2], const())
                     put(o[3], g.row_shift)
                     put(o[4], g.dom)
                 elif k == "L":
