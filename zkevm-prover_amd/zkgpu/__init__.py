@@ -16,7 +16,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libzkgpu.so")
+# ZKGPU_LIB_DIR: an alternative build of both libraries (A/B runs of compiler options)
+LIB_DIR = os.environ.get("ZKGPU_LIB_DIR") or os.path.join(PKG_ROOT, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libzkgpu.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "zkgpu.h")
 
 P = 0xFFFFFFFF00000001

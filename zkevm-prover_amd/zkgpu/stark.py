@@ -13,7 +13,8 @@ import numpy as np
 from . import ZkgpuError, lib as _zk_lib
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-STARK_LIB = os.path.join(os.path.dirname(_HERE), "lib", "libzkgpu_stark.so")
+STARK_LIB = os.path.join(os.environ.get("ZKGPU_LIB_DIR") or os.path.join(os.path.dirname(_HERE), "lib"),
+                         "libzkgpu_stark.so")
 P = 0xFFFFFFFF00000001
 
 
