@@ -73,6 +73,10 @@ def parse():
                          "configs[4] (one proof over all ranks, strong scaling); step42ns = the quotient program of "
                          "the reference's zkEVM shape on the 2^(log_n+1) extended domain")
     ap.add_argument("--queries", type=int, default=128)
+    ap.add_argument("--no-sharded", action="store_true",
+                    help="stark workload: skip the one-proof-over-all-ranks measurement (configs[4])")
+    ap.add_argument("--sharded-timeout", type=int, default=300,
+                    help="seconds each sharded child run may take before it is killed and reported as failed")
     ap.add_argument("--fork9", action="store_true",
                     help="stark / stark-sharded: the fork-9 widths (751/168/408/6 committed, 234 constants, 389 "
                          "tmpExp; SyntheticStark.fork9) instead of config-4's")
@@ -567,6 +571,68 @@ def handoff_measure(n, C, dev, torch, zkgpu, s_per_proof):
     return res
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def sharded_children(args, world, rank, local, dist, torch):
+    """configs[4]: ONE proof over all ranks (zkgpu_stark_create_sharded, RCCL
+    over xGMI), measured by child processes -- one per rank, on the rank's
+    GPU, with their own rendezvous -- so that a failure there (the RCCL path
+    has never run between GPUs on the builder's one-GPU lease) cannot take
+    the replica measurement above with it: a child that fails or outlives
+    --sharded-timeout is killed and reported.  Runs: the config-4 instance at
+    every world size, and the fork-9 widths (751/168/408/6, 92 GB per rank at
+    W = 8) where the plan fits (W >= 4).  Returns rank 0's summary."""
+    import signal
+    import subprocess
+    runs = [("config4", [])]
+    if world >= 4:
+        runs.append(("fork9", ["--fork9"]))
+    out = {}
+    for name, extra in runs:
+        port = _free_port() if rank == 0 else 0
+        if world > 1:
+            t = torch.tensor([port], dtype=torch.int64, device="cuda")
+            dist.broadcast(t, 0)
+            port = int(t.item())
+        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(local), WORLD_SIZE=str(world),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        cmd = [sys.executable, os.path.abspath(__file__), "--workload", "stark-sharded", "--steps", "3", "--warmup",
+               "1", "--no-cpu", "--log-n", str(args.log_n), "--blowup-bits", str(args.blowup_bits), "--ncols",
+               str(args.ncols), "--queries", str(args.queries)] + extra
+        t0 = time.time()
+        p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                             start_new_session=True)
+        try:
+            so, se = p.communicate(timeout=args.sharded_timeout)
+            rc = p.returncode
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            so, se = p.communicate()
+            rc = "timeout"
+        if world > 1:
+            dist.barrier()
+        if rank != 0:
+            continue
+        line = next((ln for ln in reversed(so.splitlines()) if ln.startswith('{"metric"')), None)
+        if rc != 0 or line is None:
+            out[name] = {"error": "exit %s" % rc, "stderr_tail": se[-600:], "wall_s": round(time.time() - t0, 1)}
+            continue
+        d = json.loads(line)
+        st = d.get("stages_ms") or {}
+        out[name] = {"value": d["value"], "unit": d["unit"], "n_gpus": d["n_gpus"], "ms_per_step": d["ms_per_step"],
+                     "scaling": "strong", "workload": d["config"]["workload"],
+                     "exchange_ms": round(sum(v for k, v in st.items() if "EXCHANGE" in k), 3),
+                     "stages_ms": st, "wall_s": round(time.time() - t0, 1)}
+    return out if rank == 0 else None
+
+
 def cpu_full_main(args):
     """Time the oracle prover once at the full config-4 size (rank 0, no GPU)."""
     res = cpu_baseline_stark(args.log_n, args.blowup_bits, args.ncols, args.queries)
@@ -598,6 +664,7 @@ def main():
     C = args.ncols
     res = {"metric": METRIC}
     gs = ss = inst = None
+    sharded = None
     lde = roof = handoff = quotient = None
     if args.workload == "lde":
         lde, roof = lde_measure(args, dev, torch, world, dist)
@@ -671,6 +738,12 @@ def main():
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
             quotient = quotient_measure(args, dev, torch, world, dist)
+        if args.workload == "stark" and not args.no_sharded:
+            gs = None  # the replica prover's HBM back for the children
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            zkgpu.release()  # and the library's workspaces (this process is done with the GPU)
+            sharded = sharded_children(args, world, rank, local, dist, torch)
 
     if rank == 0:
         cpu = None
@@ -751,6 +824,8 @@ def main():
             res["handoff"] = handoff
         if quotient is not None:
             res["quotient_zkevm_shaped"] = quotient
+        if sharded is not None:
+            res["sharded_one_proof"] = sharded
         if kernels is not None:
             res["kernels"] = kernel_table(kernels)
             if args.workload == "stark" and args.log_n == 23 and C == 100:

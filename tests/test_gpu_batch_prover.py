@@ -67,16 +67,20 @@ def _sharded_run(cfg, world, comm):
     return [err for _, err in outs]
 
 
-@pytest.mark.parametrize("world,comm", [(2, "host"), (4, "host"), (1, "rccl")])
-def test_batch_prover_sharded(oracle, tmp_path, world, comm):
+@pytest.mark.parametrize("world,comm,fork9", [(2, "host", False), (4, "host", False), (1, "rccl", False),
+                                              (8, "host", True)])
+def test_batch_prover_sharded(oracle, tmp_path, world, comm, fork9):
     """--shard r/W: W driver processes prove ONE proof row-sharded
     (zkgpu_stark_create_sharded); rank 0's zkin equals the oracle's.  host =
     shared-memory exchange (the W processes share the one GPU here); rccl at
-    world 1 exercises the id file and communicator set-up."""
+    world 1 exercises the id file and communicator set-up; fork9: the
+    zkEVM's widths (751 / 168 / 408 / 6 committed, 234 constants) from the
+    reference's file formats over 8 ranks."""
     import zkgpu.starkinfo as zs
     from oracle.stark_prover import OracleStark
     from zkgpu.synthetic import SyntheticStark
-    inst = SyntheticStark(n_bits=9, blowup_bits=1, t=4, m=2, n_lookups=1, n_queries=12)
+    inst = (SyntheticStark.fork9(n_bits=10, n_queries=8) if fork9 else
+            SyntheticStark(n_bits=9, blowup_bits=1, t=4, m=2, n_lookups=1, n_queries=12))
     o = OracleStark(inst)
     o.witness()
     proof = o.prove()

@@ -60,12 +60,15 @@ def _eval(oracle, prog, S, sc, dom):
 
 def _inst(**kw):
     from zkgpu.synthetic import SyntheticStark
+    if kw.pop("fork9", False):  # the fork-9 widths, next-row reads and shifted stores (synthetic.py)
+        return SyntheticStark.fork9(**kw)
     return SyntheticStark(**kw)
 
 
 @pytest.mark.parametrize("kw", [dict(n_bits=8, t=4, m=2, n_queries=8), dict(n_bits=7, blowup_bits=2, t=3, m=1,
                                                                              n_lookups=1, q_deg=4, n_queries=6),
-                                dict(n_bits=7, t=5, m=3, n_lookups=0, with_step3=False, n_queries=4)])
+                                dict(n_bits=7, t=5, m=3, n_lookups=0, with_step3=False, n_queries=4),
+                                dict(fork9=True, n_bits=7, n_queries=4)])
 def test_loader_recovers_instance(oracle, tmp_path, kw):
     import zkgpu.starkinfo as zs
     inst = _inst(**kw)
