@@ -210,8 +210,9 @@ public:
         return dalloc(&xchg, slot * W);
     }
 
-    // the constants' whole copy while they are set up and committed
-    uint64_t setup_bytes() const override { return (uint64_t)(info.n_const ? info.n_const : 1) * N * 8; }
+    // the constants' whole copy while they are set up and committed (set_const:
+    // plus the row-major staging of the host's rows)
+    uint64_t setup_bytes() const override { return 2ULL * (info.n_const ? info.n_const : 1) * N * 8; }
     uint64_t lde_cols_max() const override { return max_share(); }
     uint64_t prog_rows_max() const override { return std::max(B, nb); }
 
