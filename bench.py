@@ -587,7 +587,7 @@ def sharded_children(args, world, rank, local, dist, torch):
     has never run between GPUs on the builder's one-GPU lease) cannot take
     the replica measurement above with it: a child that fails or outlives
     --sharded-timeout is killed and reported.  Runs: the config-4 instance at
-    every world size, and the fork-9 widths (751/168/408/6, 92 GB per rank at
+    every world size, and the fork-9 widths (751/168/408/6, 120 GB per rank at
     W = 8) where the plan fits (W >= 4).  Returns rank 0's summary."""
     import signal
     import subprocess
