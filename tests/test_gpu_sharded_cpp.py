@@ -70,7 +70,8 @@ def test_sharded_world1_equals_oracle(zkgpu, oracle_proofs, name):
     g.witness()
     _assert_same(g.prove(), oracle_proofs[name])
     t = g.timers()
-    assert "STARK_STEP_1_EXCHANGE" in t and "STARK_TOTAL" in t
+    # one rank: the LDE goes straight into the row block, no exchange
+    assert "STARK_TOTAL" in t and "STARK_STEP_1_LDE" in t and not any("EXCHANGE" in k for k in t)
     g.close()
 
 

@@ -51,8 +51,8 @@ class ShardedStarks : public Starks
 public:
     zkgpu_comm comm{};
     uint32_t W = 1, R = 0;
-    uint64_t B = 0, H = 0, BH = 0;     // 2n domain: block rows, halo rows (2^blowup), ld
-    uint64_t nb = 0, hn = 0, ldn = 0;  // n domain: block rows, halo rows, ld
+    uint64_t B = 0, H = 0, BH = 0;     // 2n domain: block rows, halo rows (2^blowup), ld (>= B + H)
+    uint64_t nb = 0, hn = 0, ldn = 0;  // n domain: block rows, halo rows, ld (>= nb + hn)
     uint64_t *ext = nullptr;    // LDE of the rank's column share (max share x NE)
     uint64_t *coln = nullptr;   // the rank's column share over all N rows (max share x N): the LDE input
     uint64_t *gath = nullptr;   // q / f gathered (3 x NE)
@@ -93,7 +93,10 @@ public:
             return fail("stark_create_sharded: 2^%u rows do not split into %u blocks of >= %llu rows", info.n_bits_ext,
                         W, (unsigned long long)(2 * H));
         B = NE / W;
-        BH = B + H;
+        // leading dimensions padded to whole 512-byte runs: every column starts
+        // on a cache-line boundary (an LDE into a block with ld 2^24 + 2 ran 12 %
+        // slower than into ld 2^24)
+        BH = B + ((H + 63) & ~63ULL);
         nb = N / W;
         hn = 0;
         const Prog *progs[4] = {&step1, &step2, &step3prev, &step3};
@@ -103,7 +106,7 @@ public:
         if (hn > nb)
             return fail("stark_create_sharded: row shift %llu exceeds the %llu-row n-domain block of %u ranks",
                         (unsigned long long)hn, (unsigned long long)nb, W);
-        ldn = nb + hn;
+        ldn = nb + ((hn + 63) & ~63ULL);
         return 0;
     }
 
@@ -191,7 +194,7 @@ public:
             S.ncols[s] = 3;
         }
         const uint64_t ms = max_share();
-        if (dalloc(&gath, 3 * NE) || dalloc(&ext, ms * NE) || dalloc(&coln, ms * N)) return -1;
+        if (dalloc(&gath, 3 * NE) || (W > 1 && (dalloc(&ext, ms * NE) || dalloc(&coln, ms * N)))) return -1;
         // halo staging: the n-domain halos / spills of every column, or the
         // 2n-domain halos of a column share for every peer
         hcap = std::max<uint64_t>((uint64_t)5 * wmax * std::max<uint64_t>(hn, 1), (uint64_t)W * ms * H);
@@ -498,6 +501,16 @@ public:
         share(ncols, R, lo, hi);
         const uint32_t ms = max_share();
         uint64_t *blk = S.sec[sec_e];
+        if (W == 1) {  // one rank: the LDE straight into the block, then its halo (the first rows)
+            tstart();
+            CK(zkgpu_gl_extend_pol_dev(blk, BH, src, src_ld, NE, N, ncols));
+            CK(zkgpu_copy_rows_dev(blk, BH, B, nullptr, blk, BH, 0, 0, nullptr, ncols, H));
+            if (lde_name && tstop(lde_name)) return -1;
+            tstart();
+            if (merkelize(t, blk, BH, ncols, root)) return -1;
+            if (tree_name && tstop(tree_name)) return -1;
+            return 0;
+        }
         tstart();
         if (hi > lo) CK(zkgpu_gl_extend_pol_dev(ext, NE, src, src_ld, NE, N, hi - lo));
         if (lde_name && tstop(lde_name)) return -1;
@@ -541,6 +554,8 @@ public:
     int commit_n(Tree &t, uint32_t sec_n, uint32_t sec_e, uint32_t ncols, uint64_t root[4], const char *lde_name,
                  const char *xchg_name, const char *tree_name)
     {
+        if (W == 1)  // the rank holds every row: no transpose
+            return commit_cols(t, sec_e, S.sec[sec_n], ldn, ncols, root, lde_name, xchg_name, tree_name);
         tstart();
         if (rows_to_share(sec_n, ncols)) return -1;
         if (xchg_name && tstop((std::string(xchg_name) + "_T").c_str())) return -1;
