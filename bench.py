@@ -408,13 +408,14 @@ def step42ns_setup(args, dev, torch, g):
     prog = zp.convert(zp.STEP42NS, ops, a, secs, shape["n_bits"], shape["n_bits_ext"])
     log_dom = args.log_n + 1
     NE = 1 << log_dom
+    LD = NE + int(os.environ.get("ZKGPU_S42_PAD", "0"))  # column stride (A/B of padded sections)
     dsecs = {}
     cols = 0
     for sec, _, w in secs:
         if sec >= 5:
-            dsecs[sec] = (torch.randint(0, 2**63 - 1, (w, NE), dtype=torch.int64, device=dev, generator=g), NE, w)
+            dsecs[sec] = (torch.randint(0, 2**63 - 1, (w, LD), dtype=torch.int64, device=dev, generator=g), LD, w)
             cols += w
-    dsecs[9] = (torch.randint(0, 2**63 - 1, (shape["n_const"], NE), dtype=torch.int64, device=dev, generator=g), NE,
+    dsecs[9] = (torch.randint(0, 2**63 - 1, (shape["n_const"], LD), dtype=torch.int64, device=dev, generator=g), LD,
                 shape["n_const"])
     cols += shape["n_const"]
     q = torch.zeros((3, NE), dtype=torch.int64, device=dev)
