@@ -588,13 +588,14 @@ def sharded_children(args, world, rank, local, dist, torch):
     has never run between GPUs on the builder's one-GPU lease) cannot take
     the replica measurement above with it: a child that fails or outlives
     --sharded-timeout is killed and reported.  Runs: the config-4 instance at
-    every world size, and the fork-9 widths (751/168/408/6, 120 GB per rank at
-    W = 8) where the plan fits (W >= 4).  Returns rank 0's summary."""
+    every world size, and the fork-9 widths (751/168/408/6): 2^23 rows from
+    W = 4 (190 GB per rank; 120 GB at W = 8), 2^22 rows on 1-2 ranks.  Returns
+    rank 0's summary."""
     import signal
     import subprocess
-    runs = [("config4", [])]
-    if world >= 4:
-        runs.append(("fork9", ["--fork9"]))
+    # fork-9 widths: 2^23 rows from W = 4 (plan 190 GB per rank), 2^22 rows
+    # below it (2^23 needs 386 GB on one GPU, 317 GB per rank at W = 2)
+    runs = [("config4", []), ("fork9", ["--fork9"] + (["--log-n", "22"] if world < 4 and args.log_n > 22 else []))]
     out = {}
     for name, extra in runs:
         port = _free_port() if rank == 0 else 0
@@ -606,7 +607,7 @@ def sharded_children(args, world, rank, local, dist, torch):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         cmd = [sys.executable, os.path.abspath(__file__), "--workload", "stark-sharded", "--steps", "3", "--warmup",
                "1", "--no-cpu", "--log-n", str(args.log_n), "--blowup-bits", str(args.blowup_bits), "--ncols",
-               str(args.ncols), "--queries", str(args.queries)] + extra
+               str(args.ncols), "--queries", str(args.queries)] + extra  # (a later --log-n wins)
         t0 = time.time()
         p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                              start_new_session=True)

@@ -13,6 +13,12 @@ its structure, so one compile serves every proof (the reference likewise
 ships its expression code compiled, chelpers/*.cpp).  No GPU needed (hiprtc
 cross-compiles).
 
+The STARK instances bench.py proves at 2^23 (the synthetic config-4
+instance and the fork-9-width one of the sharded runs, bench.stark_instance)
+are compiled too, one process per program: their kernels are what the
+driver's bench runs, and the fork-9 ones take minutes of hiprtc that a rank
+must not spend inside its timed child.
+
 Usage: tools/jit_prebuild.py [--check] [--prune] [--quarter-only | --full-only] [-j N]
        (--check: report cache hits only; --prune: delete the cache entries
        this run neither found nor compiled -- a hit refreshes the entry's mtime)
@@ -47,47 +53,70 @@ def consts():
             rng.integers(0, P, (2048, 3), dtype=np.uint64))
 
 
-def one(scale, seg, name):
-    """child: compile segment `seg` of program `name` at `scale` (cache hit: no-op)"""
+# bench.py's STARK instances at its default size (configs[3] / configs[4])
+STARKS = (("config4", False), ("fork9", True))
+STARK_PROGS = ("step0", "step1", "step2", "step3prev", "step3", "step42ns", "step52ns")
+
+
+def stark_program(inst_name, pname):
+    sys.path.insert(0, ROOT)
+    import bench
+    inst = bench.stark_instance(23, 1, 100, 128, dict(STARKS)[inst_name])
+    return inst.programs.get(pname)
+
+
+def get_program(spec):
+    kind, a, b = spec.split(":")
+    return program(float(b), a) if kind == "shaped" else stark_program(a, b)
+
+
+def one(spec, seg):
+    """child: compile segment `seg` of program `spec` (cache hit: no-op)"""
     import zkgpu
     os.environ["ZKGPU_ZXP_JIT_ONLY"] = str(seg)
-    zkgpu.zxp_jit_source(program(scale, name), *consts(), rtc_check=1)
+    zkgpu.zxp_jit_source(get_program(spec), *consts(), rtc_check=1)
 
 
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "--one":
-        one(float(sys.argv[2]), int(sys.argv[3]), sys.argv[4])
+        one(sys.argv[2], int(sys.argv[3]))
         return
     import zkgpu
     t_start = time.time() - 1
     check = "--check" in sys.argv
     jobs = int(sys.argv[sys.argv.index("-j") + 1]) if "-j" in sys.argv else min(16, os.cpu_count() or 1)
     scales = SCALES[:1] if "--quarter-only" in sys.argv else SCALES[1:] if "--full-only" in sys.argv else SCALES
-    work = [("step42ns", sc) for sc in scales]
+    work = [("shaped:step42ns:%g" % sc, "step42ns-shaped (seed 1, scale %g)" % sc) for sc in scales]
     if "--quarter-only" not in sys.argv:
-        work += [(o, 1.0) for o in OTHERS]
-    for pname, scale in work:
-        name = "%s-shaped (seed 1, scale %g)" % (pname, scale)
-        prog = program(scale, pname)
+        work += [("shaped:%s:1" % o, "%s-shaped (seed 1, scale 1)" % o) for o in OTHERS]
+        if "--full-only" not in sys.argv:
+            work += [("stark:%s:%s" % (i, p), "STARK %s %s" % (i, p)) for i, _ in STARKS for p in STARK_PROGS
+                     if stark_program(i, p) is not None]
+    # (spec, segment) units of every uncached program, compiled in parallel processes
+    units, todo = [], []
+    for spec, name in work:
+        prog = get_program(spec)
         hit = zkgpu.zxp_jit_cached(prog, *consts())
         if check or hit:
             print("%s: %s" % (name, "cached" if hit else "NOT cached"))
             continue
         nseg = max(1, zkgpu.zxp_jit_source(prog, *consts()).count("// ---- segment "))
-        t = time.time()
-        pending = list(range(nseg))
-        running = []
-        while pending or running:
-            while pending and len(running) < jobs:
-                j = pending.pop(0)
-                running.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "--one", str(scale),
-                                                 str(j), pname]))
-            running[0].wait()
-            if running[0].returncode:
-                raise SystemExit("%s: segment compile failed (rc %d)" % (name, running[0].returncode))
-            running.pop(0)
+        units += [(spec, j) for j in range(nseg)]
+        todo.append((spec, name, prog, nseg))
+    t = time.time()
+    running = []
+    while units or running:
+        while units and len(running) < jobs:
+            spec, j = units.pop(0)
+            running.append((spec, subprocess.Popen([sys.executable, os.path.abspath(__file__), "--one", spec, str(j)])))
+        spec, pr = running[0]
+        pr.wait()
+        if pr.returncode:
+            raise SystemExit("%s: segment compile failed (rc %d)" % (spec, pr.returncode))
+        running.pop(0)
+    for spec, name, prog, nseg in todo:
         assert zkgpu.zxp_jit_cached(prog, *consts()), name
-        print("%s: %d kernel(s) compiled in %.1f s" % (name, nseg, time.time() - t), flush=True)
+        print("%s: %d kernel(s) compiled (all units: %.1f s)" % (name, nseg, time.time() - t), flush=True)
     if "--prune" in sys.argv and not check:
         d = os.path.join(ROOT, "zkevm-prover_amd", "jitcache")
         old = [f for f in os.listdir(d) if f.endswith(".co") and os.path.getmtime(os.path.join(d, f)) < t_start]

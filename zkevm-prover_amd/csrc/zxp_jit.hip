@@ -24,12 +24,14 @@
 #include <unistd.h>
 #include <utime.h>
 
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <map>
 #include <set>
 #include <mutex>
+#include <chrono>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -400,8 +402,13 @@ int code_object(const std::string &src, std::vector<char> &code, bool *cached = 
         return 0;
     }
     int rc;
+    static const bool log = getenv("ZKGPU_JIT_LOG") && atoi(getenv("ZKGPU_JIT_LOG"));
+    const auto t0 = std::chrono::steady_clock::now();
     if ((rc = rtc_compile(src, code))) return rc;
     cache_store(src, code);
+    if (log)  // cache misses (tools/jit_prebuild.py fills the cache ahead of time)
+        fprintf(stderr, "[zkgpu jit] cache miss: %s compiled in %.1f s\n", cache_key(src).c_str(),
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     return 0;
 }
 

@@ -101,6 +101,10 @@ _SIGS = {
     # include/zkgpu_parser.h (bindings in zkgpu/parser.py)
     "zkgpu_parser_convert": (ctypes.c_int, [u32, vp, u64, vp, u64, vp, u32, u32, u32, vp]),
     "zkgpu_steps_parser_eval": (ctypes.c_int, [u32, vp, u64, vp, u64, vp, u32, u32, u32, vp]),
+    "zkgpu_steps_mirror": (ctypes.c_int, [ctypes.c_int]),
+    "zkgpu_steps_invalidate": (ctypes.c_int, [vp]),
+    "zkgpu_steps_release_mirrors": (None, []),
+    "zkgpu_steps_mirror_bytes": (u64, []),
 }
 
 
