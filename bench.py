@@ -75,7 +75,7 @@ def parse():
     ap.add_argument("--queries", type=int, default=128)
     ap.add_argument("--no-sharded", action="store_true",
                     help="stark workload: skip the one-proof-over-all-ranks measurement (configs[4])")
-    ap.add_argument("--sharded-timeout", type=int, default=300,
+    ap.add_argument("--sharded-timeout", type=int, default=150,
                     help="seconds each sharded child run may take before it is killed and reported as failed")
     ap.add_argument("--fork9", action="store_true",
                     help="stark / stark-sharded: the fork-9 widths (751/168/408/6 committed, 234 constants, 389 "
@@ -597,7 +597,12 @@ def sharded_children(args, world, rank, local, dist, torch):
     # below it (2^23 needs 386 GB on one GPU, 317 GB per rank at W = 2)
     runs = [("config4", []), ("fork9", ["--fork9"] + (["--log-n", "22"] if world < 4 and args.log_n > 22 else []))]
     out = {}
+    failed = False
     for name, extra in runs:
+        if failed:  # the same code path again: do not spend another timeout on it
+            if rank == 0:
+                out[name] = {"error": "skipped after a failed run"}
+            continue
         port = _free_port() if rank == 0 else 0
         if world > 1:
             t = torch.tensor([port], dtype=torch.int64, device="cuda")
@@ -618,8 +623,12 @@ def sharded_children(args, world, rank, local, dist, torch):
             os.killpg(p.pid, signal.SIGKILL)
             so, se = p.communicate()
             rc = "timeout"
-        if world > 1:
-            dist.barrier()
+        if world > 1:  # every rank learns whether any child failed
+            f = torch.tensor([0 if rc == 0 else 1], dtype=torch.int64, device="cuda")
+            dist.all_reduce(f)
+            failed = int(f.item()) > 0
+        else:
+            failed = rc != 0
         if rank != 0:
             continue
         line = next((ln for ln in reversed(so.splitlines()) if ln.startswith('{"metric"')), None)
