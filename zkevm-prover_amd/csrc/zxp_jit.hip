@@ -25,6 +25,7 @@
 #include <utime.h>
 
 #include <chrono>
+#include <cctype>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -136,6 +137,11 @@ __device__ __forceinline__ uint4 kpre(const uint32_t *kl, size_t lo)
     return *(const __attribute__((address_space(1))) uint4 *)(kl + lo + 4 * threadIdx.x);
 }
 __device__ __forceinline__ void kput(uint32_t *dst, uint4 v) { *(uint4 *)(dst + 4 * threadIdx.x) = v; }
+__device__ __forceinline__ uint64_t zk_cs(uint64_t *slot, uint64_t v)
+{
+    *slot = v;
+    return v;
+}
 __device__ __forceinline__ int zk_one()
 {
     int c;
@@ -178,6 +184,14 @@ extern "C" __global__ void __launch_bounds__(256) ZKJIT_WAVES zxp_jit(const JitP
 #define CPTR(j) (const_cast<uint64_t *>(p.cp[j]))
 #endif
 #define C(j, sh, ii) gload(CPTR(j) + ((ii + (uint64_t)(sh)) & m))
+#if ZKJIT_LCACHE
+    // compiler-managed column cache (lds_column_cache): slot s of this lane
+    // (ZKJIT_ROWS rows per thread: slot s of row r at (s ROWS + r))
+    __shared__ uint64_t zkc[ZKJIT_LCACHE * ZKJIT_ROWS * 256];
+    uint64_t *const zkc_ = zkc + threadIdx.x;
+#define LC(s, r) (zkc_[((s) * ZKJIT_ROWS + (r)) * 256])
+#define CS(j, sh, ii, s, r) zk_cs(zkc_ + ((s) * ZKJIT_ROWS + (r)) * 256, C(j, sh, ii))
+#endif
 // scratch columns of a segmented program (csrc/zxp_segment.hpp) are stored
 // where the value is defined, not deferred to the end of the row
 #if ZKJIT_KL_CHUNK
@@ -475,6 +489,128 @@ static std::string expand_rows(const std::string &text, uint32_t rows)
         pos = eol + 1;
     }
     return out;
+}
+
+// Compiler-managed LDS column cache for block-split programs.  A large
+// program's kernel is HBM-bound on re-reads: it loads a column again at every
+// use, and a re-read hits the 4 MB L2 of an XCD only within ~16 columns (512
+// waves x 512 bytes per column in flight).  The whole read
+// sequence is known here, so each lane keeps up to `slots` column values in
+// LDS chosen by Belady's rule (on a miss, evict the value whose next read is
+// furthest away, or bypass when the new value's next read is further still):
+// a read of a cached value becomes an LDS read, LC(s), and a read that enters
+// the cache stores its value as it loads it, CS(..., s).  The body is
+// rewritten textually: every column read is a C(j,sh,i`) token, in emission
+// order, one statement per line.  Within a line the operand evaluation order
+// is unspecified, so a slot read or filled on a line is not evicted on that
+// line.  Columns the kernel stores to are never cached.  Reads within `gap`
+// reads of the previous one are left to the L1/L2.  Returns the number of
+// cached reads (LDS hits).
+static size_t lds_column_cache(std::string &body, int slots, int gap)
+{
+    struct Rd {
+        size_t pos, len;
+        uint64_t key;
+        uint32_t line;
+    };
+    std::vector<Rd> rd;
+    std::set<uint32_t> stored;
+    auto ident = [](char c) { return isalnum((unsigned char)c) || c == '_'; };
+    auto num = [&](size_t &q, int64_t &v) {
+        const char *b = body.c_str() + q;
+        char *e;
+        v = strtoll(b, &e, 10);
+        if (e == b) return false;
+        q += (size_t)(e - b);
+        return true;
+    };
+    uint32_t line = 0;
+    for (size_t q = 0; q < body.size(); q++) {
+        const char ch = body[q];
+        if (ch == '\n') {
+            line++;
+            continue;
+        }
+        if (q > 0 && ident(body[q - 1])) continue;
+        if (ch == 'C' && body.compare(q, 2, "C(") == 0) {
+            size_t t = q + 2;
+            int64_t j, sh;
+            if (!num(t, j) || body[t] != ',') continue;
+            t++;
+            if (!num(t, sh) || body.compare(t, 4, ",i`)") != 0) continue;
+            rd.push_back({q, t + 4 - q, ((uint64_t)(uint32_t)j << 32) | (uint32_t)(int32_t)sh, line});
+        } else if (ch == 'Z' && (body.compare(q, 6, "ZK_ST(") == 0 || body.compare(q, 7, "ZK_STS(") == 0)) {
+            size_t t = q + (body[q + 5] == 'S' ? 7 : 6);
+            int64_t j;
+            if (num(t, j)) stored.insert((uint32_t)j);
+        }
+    }
+    const uint64_t INF = ~0ULL;
+    std::vector<uint64_t> nx(rd.size(), INF);
+    {
+        std::map<uint64_t, size_t> last;
+        for (size_t r = rd.size(); r-- > 0;) {
+            auto it = last.find(rd[r].key);
+            if (it != last.end()) nx[r] = it->second;
+            last[rd[r].key] = r;
+        }
+    }
+    std::vector<uint64_t> slot_key(slots, INF), slot_nu(slots, INF);
+    std::map<uint64_t, int> where;
+    std::vector<int> act(rd.size(), -1), hit(rd.size(), 0);
+    std::vector<uint32_t> pinned_line(slots, UINT32_MAX);
+    size_t hits = 0;
+    for (size_t r = 0; r < rd.size(); r++) {
+        const Rd &x = rd[r];
+        if (stored.count((uint32_t)(x.key >> 32))) continue;
+        auto it = where.find(x.key);
+        if (it != where.end()) {
+            const int sl = it->second;
+            act[r] = sl;
+            hit[r] = 1;
+            hits++;
+            pinned_line[sl] = x.line;
+            slot_nu[sl] = nx[r];
+            if (nx[r] == INF) {  // last read: the slot is free again
+                where.erase(it);
+                slot_key[sl] = INF;
+            }
+            continue;
+        }
+        if (nx[r] == INF || nx[r] - r <= (uint64_t)gap) continue;
+        int v = -1;
+        for (int sl = 0; sl < slots; sl++) {
+            if (pinned_line[sl] == x.line) continue;
+            if (slot_key[sl] == INF) {
+                v = sl;
+                break;
+            }
+            if (v < 0 || slot_nu[sl] > slot_nu[v]) v = sl;
+        }
+        if (v < 0 || (slot_key[v] != INF && slot_nu[v] <= nx[r])) continue;  // bypass
+        if (slot_key[v] != INF) where.erase(slot_key[v]);
+        slot_key[v] = x.key;
+        slot_nu[v] = nx[r];
+        where[x.key] = v;
+        pinned_line[v] = x.line;
+        act[r] = v;
+    }
+    if (!hits) return 0;
+    std::string out;
+    out.reserve(body.size() + rd.size() * 4);
+    size_t at = 0;
+    for (size_t r = 0; r < rd.size(); r++) {
+        if (act[r] < 0) continue;
+        out.append(body, at, rd[r].pos - at);
+        if (hit[r])  // (~: the row of the line, expand_rows)
+            appendf(out, "LC(%d,~)", act[r]);
+        else
+            appendf(out, "CS(%s,%d,~)", body.substr(rd[r].pos + 2, rd[r].len - 3).c_str(), act[r]);
+        at = rd[r].pos + rd[r].len;
+    }
+    out.append(body, at, std::string::npos);
+    body.swap(out);
+    return hits;
 }
 
 int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const uint64_t *> &cp,
@@ -1135,6 +1271,22 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         src += "#define ZKJIT_WAVES\n";
     const uint32_t rows = jit_rows(split);
     appendf(src, "#define ZKJIT_ROWS %u\n", rows);
+    {
+        // LDS column cache (lds_column_cache): block-split programs;
+        // ZKGPU_ZXP_JIT_LCACHE slots per lane and row (LDS: 2 KB per slot, row
+        // and workgroup), ZKGPU_ZXP_JIT_LCACHE_GAP reads left to the caches
+        static const int lslots = [] {
+            const char *e = getenv("ZKGPU_ZXP_JIT_LCACHE");
+            const int v = e ? atoi(e) : 12;
+            return v < 0 ? 0 : v > 32 ? 32 : v;
+        }();
+        static const int lgap = [] {
+            const char *e = getenv("ZKGPU_ZXP_JIT_LCACHE_GAP");
+            return e ? atoi(e) : 0;
+        }();
+        const bool lc = split && lslots > 0 && lds_column_cache(body, lslots, lgap) > 0;
+        appendf(src, "#define ZKJIT_LCACHE %d\n", lc ? lslots : 0);
+    }
     src += k_kernel_head;
     // per-row text carries a ` (-> _r) and ~ (-> r) on its line; expand()
     // writes such a line once per row
