@@ -319,3 +319,21 @@ def test_full_proof_bit_exact_jit(oracle, zkgpu, monkeypatch):
     for k in ref:
         assert got[k] == ref[k], k
     g.close()
+
+
+def test_fork9_widths_proof_bit_exact_jit(oracle, zkgpu, monkeypatch):
+    """The fork-9-width instance (751/168/408/6 columns) with every program
+    compiled: its step2 / step42ns / step52ns are block-split kernels (>= 1,000
+    instructions) with the LDS column cache (csrc/zxp_jit.hip
+    lds_column_cache), the code objects prebuilt by tools/jit_prebuild.py."""
+    from zkgpu.synthetic import SyntheticStark
+    from zkgpu.stark import GpuStark
+    monkeypatch.setenv("ZKGPU_ZXP_JIT", "2")
+    inst = SyntheticStark.fork9(n_bits=10, n_queries=8)
+    o, ref = oracle_proof(inst)
+    g = GpuStark(inst)
+    g.witness()
+    got = g.prove()
+    for k in ref:
+        assert got[k] == ref[k], k
+    g.close()
