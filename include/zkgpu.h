@@ -261,6 +261,19 @@ int zkgpu_evmap_dev(uint64_t *evals_out, const uint64_t *const *cols, const uint
 /* xDivXSubXi / xDivXSubWXi (starks.cpp:344-366) over x_k = 7 w_{2n}^k, k < 2^n_bits_ext;
  * w = Goldilocks::w(n_bits).  Outputs interleaved (2n x 3), device. */
 int zkgpu_xdivxsub_dev(uint64_t *xdiv, uint64_t *xdivw, const uint64_t xi[3], uint32_t n_bits, uint32_t n_bits_ext);
+/* The same for rows [row0, row0 + nrows) of the extended domain only, written
+ * at their places (xdiv + 3 row0 ...): a row-sharded prover's block. */
+int zkgpu_xdivxsub_rows_dev(uint64_t *xdiv, uint64_t *xdivw, const uint64_t xi[3], uint32_t n_bits,
+                            uint32_t n_bits_ext, uint64_t row0, uint64_t nrows);
+/* LEv / LpEv (starks.cpp:308-324: INTT_N of the powers of xi and of w_N xi),
+ * rows [row0, row0 + nrows) in closed form: LEv[k] = ((1 - xi^N) / N) x_k /
+ * (x_k - xi) with x_k = w_N^k (LpEv: w_N xi) -- the same field values, row by
+ * row, so each rank computes only its own rows.  lev / lpev: 3 columns of
+ * leading dimension ld holding rows row0.. at offset 0.  Fails
+ * (ZKGPU_ERR_ARG) when xi lies in the base field, where a denominator may
+ * vanish: interpolate (zkgpu_ext_powers_dev + zkgpu_gl_ntt_dev) instead. */
+int zkgpu_lagrange_xi_rows_dev(uint64_t *lev, uint64_t *lpev, uint64_t ld, const uint64_t xi[3], uint32_t n_bits,
+                               uint64_t row0, uint64_t nrows);
 
 /* base^k for k < n into 3 columns of ld (LEv / LpEv, starks.cpp:308-324) */
 int zkgpu_ext_powers_dev(uint64_t *out, uint64_t ld, const uint64_t base[3], uint64_t n);

@@ -337,3 +337,57 @@ def test_fork9_widths_proof_bit_exact_jit(oracle, zkgpu, monkeypatch):
     for k in ref:
         assert got[k] == ref[k], k
     g.close()
+
+
+@pytest.mark.parametrize("row0,nrows", [(0, 1 << 11), (512, 1024), (1536, 512), (3, 1000)])
+def test_xdivxsub_rows_dev(oracle, zkgpu, row0, nrows):
+    """A row block of xDivXSub (the sharded prover's rank block) equals those
+    rows of the whole-domain oracle; rows outside the block stay untouched."""
+    import torch
+    rng = np.random.default_rng(5)
+    nb, nbe = 10, 11
+    ne = 1 << nbe
+    xi = rand_gl(rng, 3)
+    x = np.zeros(ne, np.uint64)
+    oracle.lib().oc_powers(oracle._p(x), 7, oracle.gl_w(nbe), ne)
+    a = np.zeros((ne, 3), np.uint64)
+    b = np.zeros((ne, 3), np.uint64)
+    oracle.lib().oc_xdivxsub(oracle._p(a), oracle._p(b), oracle._p(x), ne, oracle._p(xi), oracle.gl_w(nb))
+    da = torch.full((3 * ne,), 7, dtype=torch.int64, device="cuda:0")
+    db = torch.full((3 * ne,), 7, dtype=torch.int64, device="cuda:0")
+    zkgpu.xdivxsub_rows_dev(da, db, xi, nb, nbe, row0, nrows)
+    torch.cuda.synchronize()
+    ga, gb = zkgpu.from_device(da).reshape(-1, 3), zkgpu.from_device(db).reshape(-1, 3)
+    assert np.array_equal(ga[row0:row0 + nrows], a[row0:row0 + nrows])
+    assert np.array_equal(gb[row0:row0 + nrows], b[row0:row0 + nrows])
+    assert (ga[:row0] == 7).all() and (ga[row0 + nrows:] == 7).all()
+
+
+@pytest.mark.parametrize("row0,nrows", [(0, 1 << 12), (1024, 1024), (77, 3000)])
+def test_lagrange_xi_rows_dev(oracle, zkgpu, row0, nrows):
+    """LEv / LpEv in closed form == the reference's INTT of the powers of xi
+    and w xi (starks.cpp:308-324), on any row block; a base-field xi is
+    refused (the prover interpolates then)."""
+    import torch
+    rng = np.random.default_rng(6)
+    nbits = 12
+    n = 1 << nbits
+    xi = rand_gl(rng, 3)
+    w = oracle.gl_w(nbits)
+    ref = []
+    for base in (xi, np.array([oracle.gl_mul(int(xi[0]), w), oracle.gl_mul(int(xi[1]), w),
+                               oracle.gl_mul(int(xi[2]), w)], np.uint64)):
+        pw = np.zeros((n, 3), np.uint64)
+        acc = np.array([1, 0, 0], np.uint64)
+        for k in range(n):
+            pw[k] = acc
+            acc = oracle.gl3_mul(acc, base)
+        ref.append(oracle.ntt(pw, inverse=True))
+    lev = torch.zeros((3, nrows), dtype=torch.int64, device="cuda:0")
+    lpev = torch.zeros((3, nrows), dtype=torch.int64, device="cuda:0")
+    zkgpu.lagrange_xi_rows_dev(lev, lpev, nrows, xi, nbits, row0, nrows)
+    torch.cuda.synchronize()
+    assert np.array_equal(zkgpu.from_device(lev).T, ref[0][row0:row0 + nrows])
+    assert np.array_equal(zkgpu.from_device(lpev).T, ref[1][row0:row0 + nrows])
+    with pytest.raises(zkgpu.ZkgpuError, match="base field"):
+        zkgpu.lagrange_xi_rows_dev(lev, lpev, nrows, np.array([5, 0, 0], np.uint64), nbits, row0, nrows)

@@ -1253,6 +1253,60 @@ int zkgpu_xdivxsub_dev(uint64_t *xdiv, uint64_t *xdivw, const uint64_t xi[3], ui
     return xdivxsub(xdiv, xdivw, xi, h_w(n_bits), n_bits_ext, g_ctx.stream);
 }
 
+int zkgpu_xdivxsub_rows_dev(uint64_t *xdiv, uint64_t *xdivw, const uint64_t xi[3], uint32_t n_bits,
+                            uint32_t n_bits_ext, uint64_t row0, uint64_t nrows)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (n_bits_ext > TW_MAX_LOG || n_bits > n_bits_ext) return set_error(ZKGPU_ERR_ARG, "xdivxsub_rows: bits");
+    if (row0 > (1ULL << n_bits_ext) || nrows > (1ULL << n_bits_ext) - row0)
+        return set_error(ZKGPU_ERR_ARG, "xdivxsub_rows: rows [%llu, +%llu) outside the domain",
+                         (unsigned long long)row0, (unsigned long long)nrows);
+    return xdivxsub_rows(xdiv, xdivw, xi, h_w(n_bits), n_bits_ext, row0, nrows, g_ctx.stream);
+}
+
+// F_p^3 helpers for the closed-form weights (host)
+static void h3_mul(uint64_t r[3], const uint64_t a[3], const uint64_t b[3])
+{
+    // x^3 = x + 1
+    const uint64_t c0 = h_mul(a[0], b[0]);
+    const uint64_t c1 = (uint64_t)(((unsigned __int128)h_mul(a[0], b[1]) + h_mul(a[1], b[0])) % ZK_P);
+    const uint64_t c2 =
+        (uint64_t)(((unsigned __int128)h_mul(a[0], b[2]) + h_mul(a[1], b[1]) + h_mul(a[2], b[0])) % ZK_P);
+    const uint64_t c3 = (uint64_t)(((unsigned __int128)h_mul(a[1], b[2]) + h_mul(a[2], b[1])) % ZK_P);
+    const uint64_t c4 = h_mul(a[2], b[2]);
+    r[0] = (uint64_t)(((unsigned __int128)c0 + c3) % ZK_P);
+    r[1] = (uint64_t)(((unsigned __int128)c1 + c3 + c4) % ZK_P);
+    r[2] = (uint64_t)(((unsigned __int128)c2 + c4) % ZK_P);
+}
+
+int zkgpu_lagrange_xi_rows_dev(uint64_t *lev, uint64_t *lpev, uint64_t ld, const uint64_t xi[3], uint32_t n_bits,
+                               uint64_t row0, uint64_t nrows)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (n_bits > TW_MAX_LOG) return set_error(ZKGPU_ERR_ARG, "lagrange_xi_rows: bits");
+    const uint64_t N = 1ULL << n_bits;
+    if (row0 > N || nrows > N - row0 || (nrows && ld < nrows))
+        return set_error(ZKGPU_ERR_ARG, "lagrange_xi_rows: rows [%llu, +%llu) outside the domain or ld too small",
+                         (unsigned long long)row0, (unsigned long long)nrows);
+    const uint64_t x[3] = {xi[0] % ZK_P, xi[1] % ZK_P, xi[2] % ZK_P};
+    if (x[1] == 0 && x[2] == 0)  // xi in the base field: x_k - xi may vanish; the caller interpolates instead
+        return set_error(ZKGPU_ERR_ARG, "lagrange_xi_rows: xi lies in the base field");
+    // scale = (1 - xi^N) / N
+    uint64_t p[3] = {1, 0, 0}, b[3] = {x[0], x[1], x[2]};
+    for (uint64_t e = N; e; e >>= 1) {
+        if (e & 1) h3_mul(p, p, b);
+        h3_mul(b, b, b);
+    }
+    const uint64_t ninv = h_inv(N % ZK_P);
+    const uint64_t scale[3] = {h_mul((1 + ZK_P - p[0]) % ZK_P, ninv), h_mul((ZK_P - p[1]) % ZK_P, ninv),
+                               h_mul((ZK_P - p[2]) % ZK_P, ninv)};
+    const uint64_t w = h_w(n_bits);
+    const uint64_t wx[3] = {h_mul(x[0], w), h_mul(x[1], w), h_mul(x[2], w)};
+    return xdiv_rows(lev, lpev, ld, 0, x, wx, 1, scale, n_bits, row0, nrows, g_ctx.stream);
+}
+
 int zkgpu_ext_powers_dev(uint64_t *out, uint64_t ld, const uint64_t base[3], uint64_t n)
 {
     int rc;

@@ -12,7 +12,7 @@
 //                   ratio num/den (chunked Montgomery batch inversion), then a
 //                   3-phase parallel exclusive prefix product in F_p^3.
 //   k_evmap         Starks::evmap (starks.cpp:556-669): sum_k L(k) pol[k << eb]
-//   k_xdivxsub      starks.cpp:344-366
+//   k_xdiv_rows     xDivXSub (starks.cpp:344-366), LEv / LpEv closed form
 //   k_ext_powers    LEv / LpEv power sequences (starks.cpp:308-324)
 //   k_qsplit        quotient split (starks.cpp:264-281)
 // F_p^3 arithmetic is associative/commutative and exact, so any reduction
@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(ZXP_THREADS) k_zxp_eval(ZxpEnv e)
 //               block scan -> per-thread exclusive prefixes + tile total
 //   k_z_totals: exclusive prefix of the tile totals (one workgroup)
 //   k_z_apply:  z = tile prefix * thread prefix * running product, through LDS
-constexpr int BI_CHUNK = 16;  // k_xdivxsub / k_ext: rows per thread sharing one inversion
+constexpr int BI_CHUNK = 16;  // k_xdiv_rows / k_ext: rows per thread sharing one inversion
 constexpr int SCAN_THREADS = 256;
 constexpr int Z_PER = 4;
 constexpr uint64_t Z_TILE = SCAN_THREADS * Z_PER;
@@ -523,24 +523,34 @@ __global__ void k_evmap_sum_subs(uint64_t *evals, const uint64_t *partial, const
 
 // ---------------------------------------------------------------- xDivXSub
 // xdiv[k] = x_k / (x_k - xi), xdivw[k] = x_k / (x_k - w xi), x_k = 7 * omega_2n^k
-__global__ void __launch_bounds__(256) k_xdivxsub(uint64_t *xdiv, uint64_t *xdivw, gl3 xi, gl3 wxi, uint32_t logn,
-                                                  const uint64_t *tw_lo, const uint64_t *tw_hi)
+// out_w[k] = scale * x_k / (x_k - a_w), x_k = shift * omega_{2^logn}^(row0 + k),
+// k < nrows, w = 0, 1; BI_CHUNK rows per thread share one F_p^3 inversion.
+// interleaved: out_w + 3 k + c (the xDivXSub layout), else out_w + c ld + k.
+// xDivXSubXi / WXi (starks.cpp:344-366): shift 7 on the extended domain,
+// scale 1.  LEv / LpEv (starks.cpp:308-324, INTT of the powers of xi and
+// w xi): with x_k = w_N^k, (1/N) sum_j xi^j w^-jk = ((1 - xi^N) / N) x_k /
+// (x_k - xi), the same field value row by row.
+__global__ void __launch_bounds__(256) k_xdiv_rows(uint64_t *out0, uint64_t *out1, uint64_t ld, int interleaved,
+                                                   gl3 a0, gl3 a1, uint64_t shift, gl3 scale, uint32_t logn,
+                                                   uint64_t row0, uint64_t nrows, const uint64_t *tw_lo,
+                                                   const uint64_t *tw_hi)
 {
     const uint64_t n = 1ULL << logn;
     const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool unit = scale.v[0] == 1 && scale.v[1] == 0 && scale.v[2] == 0;
     for (int which = 0; which < 2; which++) {
-        const gl3 s = which ? wxi : xi;
-        uint64_t *out = which ? xdivw : xdiv;
+        const gl3 s = which ? a1 : a0;
+        uint64_t *out = which ? out1 : out0;
         gl3 pre[BI_CHUNK];
         uint64_t xs[BI_CHUNK];
         gl3 acc{{1, 0, 0}};
 #pragma unroll
         for (int j = 0; j < BI_CHUNK; j++) {
             uint64_t k = t + j * T;
-            uint64_t ex = (k & (n - 1)) << (TW_MAX_LOG - logn);
-            xs[j] = gl_mul(7, gl_mul(tw_lo[ex & (TW_LEVEL_SIZE - 1)], tw_hi[ex >> TW_LEVEL_BITS]));
-            gl3 d = k < n ? gl3{{gl_sub(xs[j], s.v[0]), gl_neg(s.v[1]), gl_neg(s.v[2])}} : gl3{{1, 0, 0}};
+            uint64_t ex = ((row0 + k) & (n - 1)) << (TW_MAX_LOG - logn);
+            xs[j] = gl_mul(shift, gl_mul(tw_lo[ex & (TW_LEVEL_SIZE - 1)], tw_hi[ex >> TW_LEVEL_BITS]));
+            gl3 d = k < nrows ? gl3{{gl_sub(xs[j], s.v[0]), gl_neg(s.v[1]), gl_neg(s.v[2])}} : gl3{{1, 0, 0}};
             acc = j ? gl3_mul(acc, d) : d;
             pre[j] = acc;
         }
@@ -550,12 +560,20 @@ __global__ void __launch_bounds__(256) k_xdivxsub(uint64_t *xdiv, uint64_t *xdiv
             const int j = BI_CHUNK - 1 - jj;
             uint64_t k = t + j * T;
             gl3 dinv = j ? gl3_mul(inv, pre[j - 1]) : inv;
-            if (k < n) {
+            if (k < nrows) {
                 gl3 d{{gl_sub(xs[j], s.v[0]), gl_neg(s.v[1]), gl_neg(s.v[2])}};
-                gl3 r = gl3_canon(gl3_mul1(dinv, xs[j]));
-                out[3 * k] = r.v[0];
-                out[3 * k + 1] = r.v[1];
-                out[3 * k + 2] = r.v[2];
+                gl3 r = gl3_mul1(dinv, xs[j]);
+                if (!unit) r = gl3_mul(r, scale);
+                r = gl3_canon(r);
+                if (interleaved) {
+                    out[3 * k] = r.v[0];
+                    out[3 * k + 1] = r.v[1];
+                    out[3 * k + 2] = r.v[2];
+                } else {
+                    out[k] = r.v[0];
+                    out[ld + k] = r.v[1];
+                    out[2 * ld + k] = r.v[2];
+                }
                 inv = gl3_mul(inv, d);
             }
         }
@@ -730,18 +748,33 @@ int evmap_groups(uint64_t *evals, const void *groups_dev, uint32_t n_groups, uin
     return check_launch("k_evmap_groups");
 }
 
+static gl3 h_gl3(const uint64_t v[3]) { return gl3{{v[0] % ZK_P, v[1] % ZK_P, v[2] % ZK_P}}; }
+
+int xdiv_rows(uint64_t *out0, uint64_t *out1, uint64_t ld, int interleaved, const uint64_t a0[3],
+              const uint64_t a1[3], uint64_t shift, const uint64_t scale[3], uint32_t logn, uint64_t row0,
+              uint64_t nrows, hipStream_t s)
+{
+    if (!nrows) return 0;
+    Ctx &c = ctx();
+    const uint64_t threads = (nrows + BI_CHUNK - 1) / BI_CHUNK;
+    prof_begin(s);
+    hipLaunchKernelGGL(k_xdiv_rows, dim3(nblk(threads, 256)), dim3(256), 0, s, out0, out1, ld, interleaved, h_gl3(a0),
+                       h_gl3(a1), shift, h_gl3(scale), logn, row0, nrows, c.tw_lo[0], c.tw_hi[0]);
+    prof_end("k_xdiv_rows", 48.0 * nrows, s);
+    return check_launch("k_xdiv_rows");
+}
+
 int xdivxsub(uint64_t *xdiv, uint64_t *xdivw, const uint64_t xi[3], uint64_t w, uint32_t logn, hipStream_t s)
 {
-    Ctx &c = ctx();
-    gl3 x{{xi[0] % ZK_P, xi[1] % ZK_P, xi[2] % ZK_P}};
-    gl3 wx{{h_mul(x.v[0], w), h_mul(x.v[1], w), h_mul(x.v[2], w)}};
-    uint64_t n = 1ULL << logn;
-    uint64_t threads = (n + BI_CHUNK - 1) / BI_CHUNK;
-    prof_begin(s);
-    hipLaunchKernelGGL(k_xdivxsub, dim3(nblk(threads, 256)), dim3(256), 0, s, xdiv, xdivw, x, wx, logn, c.tw_lo[0],
-                       c.tw_hi[0]);
-    prof_end("k_xdivxsub", 48.0 * n, s);
-    return check_launch("k_xdivxsub");
+    return xdivxsub_rows(xdiv, xdivw, xi, w, logn, 0, 1ULL << logn, s);
+}
+
+int xdivxsub_rows(uint64_t *xdiv, uint64_t *xdivw, const uint64_t xi[3], uint64_t w, uint32_t logn, uint64_t row0,
+                  uint64_t nrows, hipStream_t s)
+{
+    const uint64_t wx[3] = {h_mul(xi[0] % ZK_P, w), h_mul(xi[1] % ZK_P, w), h_mul(xi[2] % ZK_P, w)};
+    const uint64_t one[3] = {1, 0, 0};
+    return xdiv_rows(xdiv + 3 * row0, xdivw + 3 * row0, 0, 1, xi, wx, 7, one, logn, row0, nrows, s);
 }
 
 int ext_powers(uint64_t *out, uint64_t ld, const uint64_t base[3], uint64_t n, hipStream_t s)

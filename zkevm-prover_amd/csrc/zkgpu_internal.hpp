@@ -182,6 +182,11 @@ int evmap_groups(uint64_t *evals, const void *groups_dev, uint32_t n_groups, uin
                  uint32_t n_ev, uint32_t n_sub, const uint64_t *lev, const uint64_t *lpev, uint64_t l_ld, uint64_t n, uint32_t eb,
                  uint64_t *partial, hipStream_t s);
 int xdivxsub(uint64_t *xdiv, uint64_t *xdivw, const uint64_t xi[3], uint64_t w, uint32_t logn, hipStream_t s);
+int xdivxsub_rows(uint64_t *xdiv, uint64_t *xdivw, const uint64_t xi[3], uint64_t w, uint32_t logn, uint64_t row0,
+                  uint64_t nrows, hipStream_t s);
+int xdiv_rows(uint64_t *out0, uint64_t *out1, uint64_t ld, int interleaved, const uint64_t a0[3],
+              const uint64_t a1[3], uint64_t shift, const uint64_t scale[3], uint32_t logn, uint64_t row0,
+              uint64_t nrows, hipStream_t s);
 int ext_powers(uint64_t *out, uint64_t ld, const uint64_t base[3], uint64_t n, hipStream_t s);
 int scale_powers(uint64_t *cols, uint64_t ld, uint32_t ncols, uint64_t n, uint64_t base, hipStream_t s);
 int qsplit(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t qdeg,

@@ -32,8 +32,9 @@
 //   stage 4  the quotient program on the rank's 2n rows (x_i = 7 w^(rB+i),
 //       halo rows); q (2n x 3) is gathered, the INTT / split / NTT
 //       (starks.cpp:255-296) run on every rank, each commits its rows.
-//   stage 5  evmap on the rank's n-domain rows, partial sums all-gathered and
-//       added mod p; the FRI program on the rank's rows, f gathered.
+//   stage 5  LEv / LpEv (closed form) and evmap on the rank's n-domain rows,
+//       partial sums all-gathered and added mod p; xDivXSub and the FRI
+//       program on the rank's 2n rows, f gathered.
 //   FRI      folds on every rank (2n x 3 elements); a layer tree whose
 //       groups split into W blocks is row-sharded like the commits.
 //   queries  each s0 opening by the rank owning its row (subtree siblings +
@@ -774,7 +775,7 @@ public:
         tstart();
         uint64_t *xi = ch + 21;
         tr.get_field(xi);
-        if (lagrange_xi(xi)) return -1;
+        if (lagrange_xi(xi, r0(), nb)) return -1;  // the rank's rows only
         if (tstop("STARK_STEP_5_LEv_LpEv")) return -1;
         tstart();
         {
@@ -791,7 +792,7 @@ public:
         tr.get_field(ch + 15);
         tr.get_field(ch + 18);
         tstart();
-        CK(zkgpu_xdivxsub_dev(xdiv, xdivw, xi, info.n_bits, info.n_bits_ext));
+        CK(zkgpu_xdivxsub_rows_dev(xdiv, xdivw, xi, info.n_bits, info.n_bits_ext, (uint64_t)R * B, B));
         if (tstop("STARK_STEP_5_XDIVXSUB")) return -1;
         tstart();
         const uint64_t xo = 3ULL * R * B;  // xdiv rows are interleaved F_p^3

@@ -541,7 +541,7 @@ public:
         // polynomial of degree < N is the same, the field sums are exact, and
         // contiguous n-domain columns read half the lines of the strided
         // extension rows.
-        if (lagrange_xi(xi)) return -1;
+        if (lagrange_xi(xi, 0, N)) return -1;
         if (tstop("STARK_STEP_5_LEv_LpEv")) return -1;
         tstart();
         if (evmap_rows(0, N, evals.data())) return -1;
@@ -592,9 +592,15 @@ public:
         return 0;
     }
 
-    // LEv / LpEv: the n-domain Lagrange weights of xi and w xi (see prove)
-    int lagrange_xi(const uint64_t xi[3])
+    // LEv / LpEv: the n-domain Lagrange weights of xi and w xi (see prove),
+    // rows [row0, row0 + nrows) in closed form (zkgpu_lagrange_xi_rows_dev);
+    // the whole domain by interpolation when xi lies in the base field
+    int lagrange_xi(const uint64_t xi[3], uint64_t row0, uint64_t nrows)
     {
+        if (xi[1] % P || xi[2] % P) {
+            CK(zkgpu_lagrange_xi_rows_dev(lev + row0, lpev + row0, N, xi, info.n_bits, row0, nrows));
+            return 0;
+        }
         uint64_t wN = w_of(info.n_bits);
         uint64_t xis[3], wxis[3];
         for (int k = 0; k < 3; k++) {

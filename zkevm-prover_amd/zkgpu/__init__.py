@@ -87,6 +87,8 @@ _SIGS = {
     "zkgpu_calculate_z_block_dev": (ctypes.c_int, [vp, u64, vp, u64, vp, u64, u64, vp, vp]),
     "zkgpu_evmap_dev": (ctypes.c_int, [vp, vp, vp, vp, vp, u32, vp, vp, u64, u64, u32]),
     "zkgpu_xdivxsub_dev": (ctypes.c_int, [vp, vp, vp, u32, u32]),
+    "zkgpu_xdivxsub_rows_dev": (ctypes.c_int, [vp, vp, vp, u32, u32, u64, u64]),
+    "zkgpu_lagrange_xi_rows_dev": (ctypes.c_int, [vp, vp, u64, vp, u32, u64, u64]),
     "zkgpu_ext_powers_dev": (ctypes.c_int, [vp, u64, vp, u64]),
     "zkgpu_qsplit_dev": (ctypes.c_int, [vp, u64, vp, u64, u64, u32, u64]),
     "zkgpu_scale_by_powers_dev": (ctypes.c_int, [vp, u64, u32, u64, u64]),
@@ -347,6 +349,21 @@ def xdivxsub_dev(xdiv, xdivw, xi, n_bits, n_bits_ext):
     x = _np(xi)
     _check(lib().zkgpu_xdivxsub_dev(_addr(xdiv), _addr(xdivw), x.ctypes.data, n_bits, n_bits_ext),
            "zkgpu_xdivxsub_dev")
+
+
+def xdivxsub_rows_dev(xdiv, xdivw, xi, n_bits, n_bits_ext, row0, nrows):
+    """rows [row0, row0 + nrows) of xdivxsub_dev, written at their places"""
+    x = _np(xi)
+    _check(lib().zkgpu_xdivxsub_rows_dev(_addr(xdiv), _addr(xdivw), x.ctypes.data, n_bits, n_bits_ext, row0, nrows),
+           "zkgpu_xdivxsub_rows_dev")
+
+
+def lagrange_xi_rows_dev(lev, lpev, ld, xi, n_bits, row0, nrows):
+    """LEv / LpEv rows [row0, row0 + nrows) in closed form (3 columns of
+    leading dimension ld each, row row0 at offset 0)"""
+    x = _np(xi)
+    _check(lib().zkgpu_lagrange_xi_rows_dev(_addr(lev), _addr(lpev), ld, x.ctypes.data, n_bits, row0, nrows),
+           "zkgpu_lagrange_xi_rows_dev")
 
 
 def ext_powers_dev(out, ld, base, n):
