@@ -525,20 +525,19 @@ __global__ void k_evmap_sum_subs(uint64_t *evals, const uint64_t *partial, const
 // xdiv[k] = x_k / (x_k - xi), xdivw[k] = x_k / (x_k - w xi), x_k = 7 * omega_2n^k
 // out_w[k] = scale * x_k / (x_k - a_w), x_k = shift * omega_{2^logn}^(row0 + k),
 // k < nrows, w = 0, 1; BI_CHUNK rows per thread share one F_p^3 inversion.
-// interleaved: out_w + 3 k + c (the xDivXSub layout), else out_w + c ld + k.
+// interleaved (scale 1): out_w + 3 k + c (the xDivXSub layout), else out_w + c ld + k.
 // xDivXSubXi / WXi (starks.cpp:344-366): shift 7 on the extended domain,
 // scale 1.  LEv / LpEv (starks.cpp:308-324, INTT of the powers of xi and
 // w xi): with x_k = w_N^k, (1/N) sum_j xi^j w^-jk = ((1 - xi^N) / N) x_k /
 // (x_k - xi), the same field value row by row.
-__global__ void __launch_bounds__(256) k_xdiv_rows(uint64_t *out0, uint64_t *out1, uint64_t ld, int interleaved,
-                                                   gl3 a0, gl3 a1, uint64_t shift, gl3 scale, uint32_t logn,
-                                                   uint64_t row0, uint64_t nrows, const uint64_t *tw_lo,
-                                                   const uint64_t *tw_hi)
+template <bool INTERLEAVED>
+__global__ void __launch_bounds__(256) k_xdiv_rows(uint64_t *out0, uint64_t *out1, uint64_t ld, gl3 a0, gl3 a1,
+                                                   uint64_t shift, gl3 scale, uint32_t logn, uint64_t row0,
+                                                   uint64_t nrows, const uint64_t *tw_lo, const uint64_t *tw_hi)
 {
     const uint64_t n = 1ULL << logn;
     const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool unit = scale.v[0] == 1 && scale.v[1] == 0 && scale.v[2] == 0;
     for (int which = 0; which < 2; which++) {
         const gl3 s = which ? a1 : a0;
         uint64_t *out = which ? out1 : out0;
@@ -563,9 +562,9 @@ __global__ void __launch_bounds__(256) k_xdiv_rows(uint64_t *out0, uint64_t *out
             if (k < nrows) {
                 gl3 d{{gl_sub(xs[j], s.v[0]), gl_neg(s.v[1]), gl_neg(s.v[2])}};
                 gl3 r = gl3_mul1(dinv, xs[j]);
-                if (!unit) r = gl3_mul(r, scale);
+                if constexpr (!INTERLEAVED) r = gl3_mul(r, scale);  // (xDivXSub: scale 1)
                 r = gl3_canon(r);
-                if (interleaved) {
+                if constexpr (INTERLEAVED) {
                     out[3 * k] = r.v[0];
                     out[3 * k + 1] = r.v[1];
                     out[3 * k + 2] = r.v[2];
@@ -758,8 +757,15 @@ int xdiv_rows(uint64_t *out0, uint64_t *out1, uint64_t ld, int interleaved, cons
     Ctx &c = ctx();
     const uint64_t threads = (nrows + BI_CHUNK - 1) / BI_CHUNK;
     prof_begin(s);
-    hipLaunchKernelGGL(k_xdiv_rows, dim3(nblk(threads, 256)), dim3(256), 0, s, out0, out1, ld, interleaved, h_gl3(a0),
-                       h_gl3(a1), shift, h_gl3(scale), logn, row0, nrows, c.tw_lo[0], c.tw_hi[0]);
+    const gl3 sc = h_gl3(scale);
+    if (interleaved && !(sc.v[0] == 1 && sc.v[1] == 0 && sc.v[2] == 0))
+        return set_error(ZKGPU_ERR_ARG, "xdiv_rows: the interleaved form has scale 1");
+    if (interleaved)
+        hipLaunchKernelGGL(k_xdiv_rows<true>, dim3(nblk(threads, 256)), dim3(256), 0, s, out0, out1, ld, h_gl3(a0),
+                           h_gl3(a1), shift, sc, logn, row0, nrows, c.tw_lo[0], c.tw_hi[0]);
+    else
+        hipLaunchKernelGGL(k_xdiv_rows<false>, dim3(nblk(threads, 256)), dim3(256), 0, s, out0, out1, ld, h_gl3(a0),
+                           h_gl3(a1), shift, sc, logn, row0, nrows, c.tw_lo[0], c.tw_hi[0]);
     prof_end("k_xdiv_rows", 48.0 * nrows, s);
     return check_launch("k_xdiv_rows");
 }
