@@ -49,13 +49,25 @@ __device__ __forceinline__ void gstore_out(uint64_t *p, uint64_t v) { *(gf64_t *
 // any u64 -> [0, p)   (x < 2^64 < 2p, so one conditional subtraction)
 __device__ __forceinline__ uint64_t gl_canon(uint64_t a) { return a >= ZK_P ? a - ZK_P : a; }
 
+// ZK_RB = 1 (a translation unit's choice, e.g. a run-time compiled
+// expression kernel): gl_add / gl_sub take the rare second correction behind
+// a wave-uniform branch, as gl_add_rb / gl_sub_rb below
+#ifndef ZK_RB
+#define ZK_RB 0
+#endif
+
 // a + b (mod p), any inputs, lazy output
 __device__ __forceinline__ uint64_t gl_add(uint64_t a, uint64_t b)
 {
     uint64_t s, s2;
     bool c = __builtin_add_overflow(a, b, &s);  // a + b = s + 2^64 c  ==  s + EPS c
     bool c2 = __builtin_add_overflow(s, c ? ZK_EPS : 0ULL, &s2);
+#if ZK_RB
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(c2) != 0, 0)) s2 += c2 ? ZK_EPS : 0ULL;
+    return s2;
+#else
     return s2 + (c2 ? ZK_EPS : 0ULL);  // c2 => s2 < EPS: no third carry
+#endif
 }
 
 // a - b (mod p), any inputs, lazy output
@@ -64,10 +76,39 @@ __device__ __forceinline__ uint64_t gl_sub(uint64_t a, uint64_t b)
     uint64_t d, d2;
     bool br = __builtin_sub_overflow(a, b, &d);  // a - b = d - 2^64 br  ==  d - EPS br
     bool br2 = __builtin_sub_overflow(d, br ? ZK_EPS : 0ULL, &d2);
+#if ZK_RB
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(br2) != 0, 0)) d2 -= br2 ? ZK_EPS : 0ULL;
+    return d2;
+#else
     return d2 - (br2 ? ZK_EPS : 0ULL);  // br2 => d2 > 2^64 - EPS: no third borrow
+#endif
 }
 
 __device__ __forceinline__ uint64_t gl_neg(uint64_t a) { return gl_sub(0, a); }
+
+// gl_add / gl_sub with the second correction behind a wave-uniform branch.
+// The second carry (borrow) needs a + b - 2^64 >= 2^64 - EPS (b - a >= p):
+// about 2^-32 per operation on lazy values, so a wave almost never takes
+// it; the ballot is the compare's own lane mask, the branch is scalar, and
+// the common path saves the select and the 64-bit add.  Same values as
+// gl_add / gl_sub, bit for bit.
+__device__ __forceinline__ uint64_t gl_add_rb(uint64_t a, uint64_t b)
+{
+    uint64_t s, s2;
+    const bool c = __builtin_add_overflow(a, b, &s);
+    const bool c2 = __builtin_add_overflow(s, c ? ZK_EPS : 0ULL, &s2);
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(c2) != 0, 0)) s2 += c2 ? ZK_EPS : 0ULL;
+    return s2;
+}
+
+__device__ __forceinline__ uint64_t gl_sub_rb(uint64_t a, uint64_t b)
+{
+    uint64_t d, d2;
+    const bool br = __builtin_sub_overflow(a, b, &d);
+    const bool br2 = __builtin_sub_overflow(d, br ? ZK_EPS : 0ULL, &d2);
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(br2) != 0, 0)) d2 -= br2 ? ZK_EPS : 0ULL;
+    return d2;
+}
 
 // (hi:lo) mod p, lazy output.  hi*2^64 = hh*2^96 + hl*2^64 == -hh + hl*EPS
 __device__ __forceinline__ uint64_t gl_reduce128(uint64_t lo, uint64_t hi)

@@ -80,16 +80,38 @@ constexpr int GROUPS = 16;
 // twiddle omega_{2h}^i = 2^e with e = 96 i / h in [0, 96) (forward); the
 // inverse twiddle 2^(192 - e) = -2^(96 - e), so the inverse butterfly
 // computes (c - a) * 2^(96 - e) and never needs a negation.
-template <bool INV, int H, int I>
+// RB: the butterflies' add / sub with the rare second carry behind a
+// wave-uniform branch (gl_add_rb / gl_sub_rb, csrc/gl_device.hpp): 5 + 7
+// VALU instead of 7 + 10.  The radix-256 pass kernel uses it (LDE 52.8 ->
+// 56.9 Gelem/s); the 3-pass LDE's 64-register kernels do not (their branchy
+// form ran at half speed: 49.1 -> 26.0 Gelem/s).  ZKGPU_NTT_RB=0 builds the
+// select form everywhere.
+#ifndef ZKGPU_NTT_RB
+#define ZKGPU_NTT_RB 1
+#endif
+template <bool RB>
+__device__ __forceinline__ uint64_t bf_add(uint64_t a, uint64_t b)
+{
+    if constexpr (RB && ZKGPU_NTT_RB) return gl_add_rb(a, b);
+    else return gl_add(a, b);
+}
+template <bool RB>
+__device__ __forceinline__ uint64_t bf_sub(uint64_t a, uint64_t b)
+{
+    if constexpr (RB && ZKGPU_NTT_RB) return gl_sub_rb(a, b);
+    else return gl_sub(a, b);
+}
+
+template <bool INV, int H, int I, bool RB>
 __device__ __forceinline__ uint64_t dif_odd(uint64_t a, uint64_t c)
 {
     constexpr int e = (96 * I) / H;
-    if constexpr (e == 0) return gl_sub(a, c);
-    else if constexpr (!INV) return mul2e<e>(gl_sub(a, c));
-    else return mul2e<96 - e>(gl_sub(c, a));
+    if constexpr (e == 0) return bf_sub<RB>(a, c);
+    else if constexpr (!INV) return mul2e<e>(bf_sub<RB>(a, c));
+    else return mul2e<96 - e>(bf_sub<RB>(c, a));
 }
 
-template <int LOG, bool INV, int H = (1 << LOG) / 2>
+template <int LOG, bool INV, bool RB = false, int H = (1 << LOG) / 2>
 __device__ __forceinline__ void dft_regs(uint64_t *v)
 {
     if constexpr (H >= 1) {
@@ -102,22 +124,22 @@ __device__ __forceinline__ void dft_regs(uint64_t *v)
                             [&]<int I>() {
                                 uint64_t a = v[B * 2 * H + I];
                                 uint64_t c = v[B * 2 * H + I + H];
-                                v[B * 2 * H + I] = gl_add(a, c);
-                                v[B * 2 * H + I + H] = dif_odd<INV, H, I>(a, c);
+                                v[B * 2 * H + I] = bf_add<RB>(a, c);
+                                v[B * 2 * H + I + H] = dif_odd<INV, H, I, RB>(a, c);
                             }.template operator()<Is>(),
                             ...);
                     }(std::make_integer_sequence<int, H>{});
                 }.template operator()<Bs>(),
                 ...);
         }(std::make_integer_sequence<int, R / (2 * H)>{});
-        dft_regs<LOG, INV, H / 2>(v);
+        dft_regs<LOG, INV, RB, H / 2>(v);
     }
 }
 
 // dft_regs when the upper half of v[] is zero (the zero-padded LDE input):
 // the first stage's butterflies are (a, 0) -> (a, a * 2^e), exactly what
 // gl_add(a, 0) / gl_sub(a, 0) return, without the adds
-template <int LOG, bool INV>
+template <int LOG, bool INV, bool RB = false>
 __device__ __forceinline__ void dft_regs_half(uint64_t *v)
 {
     constexpr int R = 1 << LOG, H = R / 2;
@@ -129,7 +151,7 @@ __device__ __forceinline__ void dft_regs_half(uint64_t *v)
             else v[I + H] = mul2e<e>(v[I]);
         }.template operator()<Is>(), ...);
     }(std::make_integer_sequence<int, H>{});
-    dft_regs<LOG, INV, H / 2>(v);
+    dft_regs<LOG, INV, RB, H / 2>(v);
 }
 
 __host__ __device__ constexpr int brev_c(int x, int bits)
@@ -209,11 +231,11 @@ __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
     }
     if constexpr (!INV) {
         if (a.half_zero)
-            dft_regs_half<L1, INV>(v);
+            dft_regs_half<L1, INV, true>(v);
         else
-            dft_regs<L1, INV>(v);
+            dft_regs<L1, INV, true>(v);
     } else {
-        dft_regs<L1, INV>(v);
+        dft_regs<L1, INV, true>(v);
     }
     __syncthreads();  // twR ready
 #pragma unroll
@@ -261,7 +283,7 @@ __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
     // ------------------------------------------------ step 2 (R2-DFT + store)
     g = g2;
     const int k1 = k1s;
-    dft_regs<L2, INV>(v);
+    dft_regs<L2, INV, true>(v);
     if (!a.last && a.otw) {
         // X[k] * omega_m^(j' k) from the table (one coalesced load per element
         // instead of a recurrence product), k = k1 + R1*k2, j' = j0 + g

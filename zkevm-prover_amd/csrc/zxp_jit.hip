@@ -1253,6 +1253,15 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     if ((kas == 1 || kas == 4) && !kchunk && !jit_kl_lds(kl.size()))
         appendf(src, "#define ZK_LIMB_AS __attribute__((address_space(%d)))\n", kas);
     if (cpas == 1 || cpas == 4) appendf(src, "#define ZK_CP_AS __attribute__((address_space(%d)))\n", cpas);
+    {
+        // ZKGPU_ZXP_JIT_RB=1: field add / sub with the rare second correction
+        // behind a wave-uniform branch (gl_device.hpp ZK_RB)
+        static const int rb = [] {
+            const char *e = getenv("ZKGPU_ZXP_JIT_RB");
+            return e ? atoi(e) : 0;
+        }();
+        if (rb) src += "#define ZK_RB 1\n";
+    }
     src += k_gl_device_src;
     appendf(src, "#define ZKJIT_KL_LDS %d\n", !kchunk && jit_kl_lds(kl.size()) ? 1 : 0);
     appendf(src, "#define ZKJIT_SPLIT %d\n", split ? 1 : 0);
