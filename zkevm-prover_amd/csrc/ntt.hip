@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "gl_device.hpp"
+#include "gl_rb.hpp"
 #include "zkgpu_internal.hpp"
 
 namespace zk {
@@ -89,6 +90,9 @@ constexpr int GROUPS = 16;
 #ifndef ZKGPU_NTT_RB
 #define ZKGPU_NTT_RB 1
 #endif
+#ifndef ZKGPU_NTT_RB_SHIFT  // the shift-multiplies' rare corrections too (mul2e_rb)
+#define ZKGPU_NTT_RB_SHIFT 1
+#endif
 template <bool RB>
 __device__ __forceinline__ uint64_t bf_add(uint64_t a, uint64_t b)
 {
@@ -102,13 +106,20 @@ __device__ __forceinline__ uint64_t bf_sub(uint64_t a, uint64_t b)
     else return gl_sub(a, b);
 }
 
+template <int E, bool RB>
+__device__ __forceinline__ uint64_t bf_mul2e(uint64_t x)
+{
+    if constexpr (RB && ZKGPU_NTT_RB && ZKGPU_NTT_RB_SHIFT) return mul2e_rb<E>(x);
+    else return mul2e<E>(x);
+}
+
 template <bool INV, int H, int I, bool RB>
 __device__ __forceinline__ uint64_t dif_odd(uint64_t a, uint64_t c)
 {
     constexpr int e = (96 * I) / H;
     if constexpr (e == 0) return bf_sub<RB>(a, c);
-    else if constexpr (!INV) return mul2e<e>(bf_sub<RB>(a, c));
-    else return mul2e<96 - e>(bf_sub<RB>(c, a));
+    else if constexpr (!INV) return bf_mul2e<e, RB>(bf_sub<RB>(a, c));
+    else return bf_mul2e<96 - e, RB>(bf_sub<RB>(c, a));
 }
 
 template <int LOG, bool INV, bool RB = false, int H = (1 << LOG) / 2>
@@ -241,7 +252,7 @@ __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
 #pragma unroll
     for (int r = 0; r < R1; r++) {
         const int k1 = brev_c(r, L1);
-        if (k1) v[r] = gl_mul(v[r], twR[(j2 * k1) & (R - 1)]);
+        if (k1) v[r] = gl_mul_rb(v[r], twR[(j2 * k1) & (R - 1)]);
     }
     const bool active = tid < GROUPS * R1;  // step-2 threads
     const int g2 = tid & 15, k1s = tid >> 4;
@@ -293,7 +304,7 @@ __global__ void __launch_bounds__(16 * (1 << L2)) k_ntt_pass(PassArgs a)
             const int r = brev_c(k2, L2);
             const uint64_t k = (uint64_t)(k1 + R1 * k2);
             uint64_t x = v[r];
-            if (k1 | k2) x = gl_mul(x, a.otw[(k << logmp) + jp]);
+            if (k1 | k2) x = gl_mul_rb(x, a.otw[(k << logmp) + jp]);
             dst[base + (k << logmp) + g] = x;  // intermediate: lazy
         }
     } else if (!a.last) {

@@ -15,12 +15,17 @@
 // and a reduction per output lane.
 #pragma once
 #include "gl_device.hpp"
+#include "gl_rb.hpp"
 #include "poseidon_gl_constants.h"
 #include "poseidon_gl_sparse.h"
 
 #include <utility>
 
 namespace zk {
+
+#ifndef ZKGPU_POSEIDON_RB
+#define ZKGPU_POSEIDON_RB 1
+#endif
 
 // gl_mul specialised for squaring: 3 partial products instead of 4
 __device__ __forceinline__ uint64_t gl_sqr3(uint64_t a)
@@ -34,15 +39,17 @@ __device__ __forceinline__ uint64_t gl_sqr3(uint64_t a)
     const uint64_t u = p01 + (uint32_t)t;                 // < 2^64
     const uint64_t hi = p11 + (t >> 32) + (u >> 32);
     const uint64_t lo = (u << 32) | (uint32_t)p00;
-    return gl_reduce128(lo, hi);
+    return ZKGPU_POSEIDON_RB ? gl_reduce128_rb(lo, hi) : gl_reduce128(lo, hi);
 }
 
+// S-box products with the reduction's rare correction behind a uniform
+// branch (gl_rb.hpp): 3 fewer VALU per product, 4 products per S-box
 __device__ __forceinline__ uint64_t pow7(uint64_t x)
 {
     const uint64_t x2 = gl_sqr3(x);
-    const uint64_t x3 = gl_mul(x2, x);
+    const uint64_t x3 = ZKGPU_POSEIDON_RB ? gl_mul_rb(x2, x) : gl_mul(x2, x);
     const uint64_t x4 = gl_sqr3(x2);
-    return gl_mul(x3, x4);
+    return ZKGPU_POSEIDON_RB ? gl_mul_rb(x3, x4) : gl_mul(x3, x4);
 }
 
 // M[x][y] = MCIRC[(y - x) mod 12] + (x == y == 0) * 8
