@@ -23,6 +23,28 @@ __device__ __forceinline__ uint64_t gl_reduce128_rb(uint64_t lo, uint64_t hi)
     return r + (c ? ZK_EPS : 0ULL);
 }
 
+// lo + hl 2^64 for a small hl (< 2^20: hl EPS < 2^52, so the carry needs lo
+// >= 2^64 - 2^52, about 2^-12; the Poseidon MDS row sums have hl < 2^11)
+__device__ __forceinline__ uint64_t gl_reduce96_small_rb(uint64_t lo, uint32_t hl)
+{
+    const uint64_t t1 = ((uint64_t)hl << 32) - hl;
+    uint64_t r;
+    const bool c = __builtin_add_overflow(lo, t1, &r);
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(c) != 0, 0)) r += c ? ZK_EPS : 0ULL;
+    return r;
+}
+
+// Dot3::fin with the reduction's rare correction (the sum's high word is
+// < 2^41, so lo - hh borrows with probability < 2^-55)
+__device__ __forceinline__ uint64_t dot3_fin_rb(const Dot3 &d)
+{
+    uint64_t l1, l2;
+    const uint32_t c1 = __builtin_add_overflow(d.A0, d.A1 << 22, &l1) ? 1u : 0u;
+    const uint32_t c2 = __builtin_add_overflow(l1, d.A2 << 43, &l2) ? 1u : 0u;
+    const uint64_t h = (d.A1 >> 42) + (d.A2 >> 21) + c1 + c2;
+    return gl_reduce128_rb(l2, h);
+}
+
 __device__ __forceinline__ uint64_t gl_mul_rb(uint64_t a, uint64_t b)
 {
     const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);

@@ -27,6 +27,9 @@ namespace zk {
 #define ZKGPU_POSEIDON_RB 1
 #endif
 
+// a partial-round dot product's final reduction
+__device__ __forceinline__ uint64_t pfin(const Dot3 &d) { return ZKGPU_POSEIDON_RB ? dot3_fin_rb(d) : d.fin(); }
+
 // gl_mul specialised for squaring: 3 partial products instead of 4
 __device__ __forceinline__ uint64_t gl_sqr3(uint64_t a)
 {
@@ -280,7 +283,8 @@ __device__ __forceinline__ void mds_fold(uint64_t st[12], const uint64_t *K)
         uint32_t c1, c2;
         const uint32_t mid = __builtin_addc((uint32_t)(sl >> 32), (uint32_t)sh, 0u, &c1);
         const uint32_t h = __builtin_addc((uint32_t)(sh >> 32), 0u, c1, &c2);
-        st[x] = gl_reduce96(((uint64_t)mid << 32) | (uint32_t)sl, h);
+        st[x] = ZKGPU_POSEIDON_RB ? gl_reduce96_small_rb(((uint64_t)mid << 32) | (uint32_t)sl, h)
+                                  : gl_reduce96(((uint64_t)mid << 32) | (uint32_t)sl, h);
     }
 }
 
@@ -343,7 +347,8 @@ __device__ __forceinline__ void mds_fft_fold(uint64_t st[12], const uint64_t *K)
         uint32_t c1, c2;
         const uint32_t mid = __builtin_addc((uint32_t)(sl >> 32), (uint32_t)sh, 0u, &c1);
         const uint32_t h = __builtin_addc((uint32_t)(sh >> 32), 0u, c1, &c2);
-        st[x] = gl_reduce96(((uint64_t)mid << 32) | (uint32_t)sl, h);
+        st[x] = ZKGPU_POSEIDON_RB ? gl_reduce96_small_rb(((uint64_t)mid << 32) | (uint32_t)sl, h)
+                                  : gl_reduce96(((uint64_t)mid << 32) | (uint32_t)sl, h);
     }
 }
 
@@ -383,7 +388,7 @@ __device__ __forceinline__ void psb_step(uint64_t &x, uint64_t y[], const uint64
     for (int j = 0; j < 11; j++) d.term(L[j], T + o + 9 + 6 * j);
 #pragma unroll
     for (int i = 0; i < t; i++) d.term(y[i], T + o + 75 + 6 * i);
-    x = d.fin();
+    x = pfin(d);
 }
 
 template <int... ts>
@@ -404,7 +409,7 @@ __device__ __forceinline__ void partial_rounds_blocks(uint64_t st[12])
         Dot3 d(&ZKGPU_PSB_D0[i * 69]);
 #pragma unroll
         for (int j = 0; j < 11; j++) d.term(st[1 + j], &ZKGPU_PSB_D0[i * 69 + 3 + 6 * j]);
-        L[i] = d.fin();
+        L[i] = pfin(d);
     }
     uint64_t x = st[0];
 #pragma unroll 1
@@ -420,7 +425,7 @@ __device__ __forceinline__ void partial_rounds_blocks(uint64_t st[12])
             d.lane(L[j]);
 #pragma unroll
             for (int i = 0; i < ZKGPU_PSB_BLOCK; i++) d.term(y[i], Tj + 3 + 6 * i);
-            L[j] = d.fin();
+            L[j] = pfin(d);
         }
     }
     st[0] = x;
@@ -497,7 +502,7 @@ __device__ __forceinline__ void psb_step_k(uint64_t *x, uint64_t (*y)[ZKGPU_PSB_
 #pragma unroll
             for (int i = 0; i < t; i++) d.term(y[k][i], T + o + 75 + 6 * i);
         }
-        x[k] = d.fin();
+        x[k] = pfin(d);
     }
 }
 
@@ -519,7 +524,7 @@ __device__ __forceinline__ void partial_rounds_blocks_k(uint64_t (*st)[12])
             Dot3 d(&ZKGPU_PSB_D0[i * 69]);
 #pragma unroll
             for (int j = 0; j < 11; j++) d.term(st[k][1 + j], &ZKGPU_PSB_D0[i * 69 + 3 + 6 * j]);
-            L[k][i] = d.fin();
+            L[k][i] = pfin(d);
         }
     uint64_t x[K];
 #pragma unroll
@@ -539,7 +544,7 @@ __device__ __forceinline__ void partial_rounds_blocks_k(uint64_t (*st)[12])
                 d.lane(L[k][j]);
 #pragma unroll
                 for (int i = 0; i < ZKGPU_PSB_BLOCK; i++) d.term(y[k][i], Tj + 3 + 6 * i);
-                L[k][j] = d.fin();
+                L[k][j] = pfin(d);
             }
     }
 #pragma unroll
