@@ -117,7 +117,11 @@ __device__ __forceinline__ uint64_t gl_reduce128(uint64_t lo, uint64_t hi)
     const uint32_t hl = (uint32_t)hi;
     uint64_t t0, r;
     bool br = __builtin_sub_overflow(lo, (uint64_t)hh, &t0);
+#if ZK_RB  // (br needs lo < hh < 2^32: rare)
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(br) != 0, 0)) t0 -= br ? ZK_EPS : 0ULL;
+#else
     t0 -= br ? ZK_EPS : 0ULL;  // br => t0 >= 2^64 - 2^32 + 1 > EPS
+#endif
     const uint64_t t1 = ((uint64_t)hl << 32) - hl;  // hl * EPS, <= 2^64 - 2^33 + 1
     bool c = __builtin_add_overflow(t0, t1, &r);
     return r + (c ? ZK_EPS : 0ULL);  // c => r < t1: no second carry
