@@ -106,7 +106,7 @@ for step in "$@"; do
             out=${pass##*:}
             cd /tmp
             timeout -s KILL 400 rocprofv3 --pmc $ctr --kernel-trace -d "$ROOTDIR/gpurun_out/$out" -o run \
-                --output-format csv -- python3 "$ROOTDIR/bench.py" --workload stark --no-cpu --no-lde --steps 1 --warmup 0 \
+                --output-format csv -- python3 "$ROOTDIR/bench.py" --workload stark --no-cpu --no-lde --no-sharded --no-handoff --no-s42 --steps 1 --warmup 0 \
                 > /dev/null 2> "$ROOTDIR/gpurun_out/$out.err"
             rc=$?
             cd "$ROOTDIR"
