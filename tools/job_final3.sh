@@ -2,7 +2,7 @@
 # round-3 close: GPU suite, smoke, default bench, rocprof kernel stats of the default bench and of the fork-9 2^22 proof
 set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
-O=$R/gpurun_out/final3
+O=$R/gpurun_out/${FINAL_TAG:-final3}
 mkdir -p $O
 cd $R
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
