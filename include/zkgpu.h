@@ -314,6 +314,18 @@ int zkgpu_gl_merkle_open_rows_dev(uint64_t *vals_out, uint64_t *sibs_out, const 
  * tests to pin the arithmetic core against big-integer references. */
 int zkgpu_gl_field_selftest_dev(uint64_t *out, const uint64_t *a, const uint64_t *b, uint64_t n, int op);
 
+/* The same for the helpers whose final correction runs behind a wave-uniform
+ * branch (csrc/gl_rb.hpp; the NTT pass butterflies and the Poseidon S-box,
+ * MDS and dot-product reductions use them), and every shift-multiply:
+ * op 0 gl_add_rb(a, b), 1 gl_sub_rb(a, b), 2 gl_mul_rb(a, b),
+ * 3 gl_reduce128_rb(lo = a, hi = b), 4 gl_reduce96_small_rb(lo = a, hl = b mod 2^32),
+ * 5 dot3_fin_rb(A0 = a, A1 = b, A2 = c), 6 mul2e_rb<e>(a), 7 mul2e<e>(a) (0 <= e < 192),
+ * 8 the Poseidon S-box a^7 (pow7), 9 its squaring gl_sqr3(a),
+ * 10 gl_reduce128(lo = a, hi = b), 11 Dot3::fin(A0 = a, A1 = b, A2 = c).
+ * Canonical results; c is read by ops 5 and 11 only. */
+int zkgpu_gl_field_selftest_rb_dev(uint64_t *out, const uint64_t *a, const uint64_t *b, const uint64_t *c, uint64_t n,
+                                   int op, int e);
+
 /* ---- live kernel profiling --------------------------------------------------
  * With profiling on, every kernel launch is bracketed by HIP events recorded
  * on the launch stream, tagged with the kernel name and its algorithmic bytes

@@ -95,8 +95,11 @@ int zkgpu_steps_parser_eval(uint32_t parser, const uint64_t *ops, uint64_t n_ops
  * copied back).  Host code that writes a section between calls -- in
  * Starks::genProof calculateH1H2 (cm2_n, starks.cpp:104-127), calculateZ
  * (cm3_n, :165-189), every extendPol (cm*_2ns, :53,134,215) and the quotient
- * split (cm4_2ns, :255-296) -- must invalidate it first.  Off by default;
- * turning it off releases the mirrors. */
+ * split (cm4_2ns, :255-296) -- must invalidate it first.  A ZKGPU_STEP2PREV
+ * call starts a proof (starks.cpp:73) and invalidates every mirror itself:
+ * the executor rewrites the witness in the same host map before each proof
+ * (prover.cpp:94-116) without announcing it.  Off by default; turning it off
+ * releases the mirrors. */
 int zkgpu_steps_mirror(int enable);
 int zkgpu_steps_invalidate(const void *host_section); /* NULL: every mirror */
 void zkgpu_steps_release_mirrors(void);

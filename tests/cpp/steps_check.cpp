@@ -267,6 +267,26 @@ int main(int argc, char **argv)
             pols = pols1;
             (steps.*entries[0])(params, dom, 4);
             expect(same(pols, pols2), "second call on mirrors == second call staged");
+            if (parser == ZKGPU_STEP2PREV) {
+                // the next proof: the executor rewrites the witness on the
+                // host and announces nothing (genProof reuses pAddress,
+                // prover.cpp:94-116); step2prev starts a proof, so every
+                // mirror is dropped and the new witness is staged
+                std::vector<Goldilocks::Element> w = pols0;
+                for (const auto &m : map) {  // row 0 of every n-domain section
+                    if (m.section > 4) continue;
+                    for (uint64_t c = 0; c < m.width; c++) w[m.offset + c].fe ^= 3;
+                }
+                pols = w;
+                (steps.*entries[0])(params, dom, 4);
+                const std::vector<Goldilocks::Element> mirrored = pols;
+                gpu.keep_mirrors(false);
+                pols = w;
+                (steps.*entries[0])(params, dom, 4);
+                expect(same(pols, mirrored), "a new witness with mirrors on == staged (no stale mirror)");
+                expect(!same(pols, pols1), "the new witness changes the result");
+                gpu.keep_mirrors(true);
+            }
         }
         gpu.keep_mirrors(false);
         expect(zkgpu_steps_mirror_bytes() == 0, "mirrors released");

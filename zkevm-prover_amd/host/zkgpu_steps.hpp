@@ -32,7 +32,7 @@
 // keep_mirrors(true): sections stay on the device between calls
 // (zkgpu_steps_mirror); the caller invalidates a section its own code writes
 // (invalidate(section pointer), see include/zkgpu_parser.h for the genProof
-// call sites).
+// call sites); step2prev, the first program of a proof, drops every mirror.
 //
 // Errors follow the reference (zklog.error + exitProcess, exit_process.cpp:7)
 // through zkgpu::error_handler() of host/zkgpu_goldilocks.hpp.

@@ -67,6 +67,7 @@ _SIGS = {
     "zkgpu_fri_fold_dev": (ctypes.c_int, [vp, vp, u32, u32, vp, u64]),
     "zkgpu_fri_transpose_dev": (ctypes.c_int, [vp, vp, u64, u32]),
     "zkgpu_gl_field_selftest_dev": (ctypes.c_int, [vp, vp, vp, u64, ctypes.c_int]),
+    "zkgpu_gl_field_selftest_rb_dev": (ctypes.c_int, [vp, vp, vp, vp, u64, ctypes.c_int, ctypes.c_int]),
     "zkgpu_dev_malloc": (ctypes.c_int, [ctypes.POINTER(vp), u64]),
     "zkgpu_dev_free": (ctypes.c_int, [vp]),
     "zkgpu_memcpy_h2d": (ctypes.c_int, [vp, vp, u64]),
@@ -326,6 +327,12 @@ def fri_transpose_dev(aux, pol, degree, transpose_bits):
 
 def field_selftest_dev(out, a, b, n, op):
     _check(lib().zkgpu_gl_field_selftest_dev(_addr(out), _addr(a), _addr(b), n, op), "zkgpu_gl_field_selftest_dev")
+
+
+def field_selftest_rb_dev(out, a, b, c, n, op, e=0):
+    """include/zkgpu.h zkgpu_gl_field_selftest_rb_dev (c may be None)."""
+    _check(lib().zkgpu_gl_field_selftest_rb_dev(_addr(out), _addr(a), _addr(b), _addr(c) if c is not None else None,
+                                                n, op, e), "zkgpu_gl_field_selftest_rb_dev")
 
 
 def calculate_z_dev(z, z_ld, num, num_ld, den, den_ld, n):
