@@ -80,6 +80,10 @@ def parse():
     ap.add_argument("--fork9", action="store_true",
                     help="stark / stark-sharded: the fork-9 widths (751/168/408/6 committed, 234 constants, 389 "
                          "tmpExp; SyntheticStark.fork9) instead of config-4's")
+    ap.add_argument("--zkevm-shaped", action="store_true",
+                    help="stark / stark-sharded: the fork-9 widths with the five zkEVM-shaped expression programs "
+                         "(zkgpu/zkevm_shaped.py: step2prev / step3prev / step3 / step42ns / step52ns in the stage "
+                         "slots, 1,973 evaluations)")
     ap.add_argument("--s42-scale", type=float, default=1.0,
                     help="step42ns workload: fraction of the reference step42ns opcode counts")
     ap.add_argument("--s42-jit", action="store_true", help="step42ns workload: the compiled kernel (else interpreter)")
@@ -98,7 +102,9 @@ def parse():
 def stark_instance(log_n, blow, ncols, n_queries, fork9=False):
     """cm1 = ncols, cm2 = 26, cm3 = 27, cm4 = 6, 30
     constants, qDeg 2, FRI steps [nBitsExt, -4, ..., 5], n_queries queries
-    (synthetic AIR, zkgpu/synthetic.py); fork9: the zkEVM's widths."""
+    (synthetic AIR, zkgpu/synthetic.py); fork9: the zkEVM's widths;
+    fork9 = "zkevm": those widths with the five zkEVM-shaped expression
+    programs (zkgpu/zkevm_shaped.py)."""
     from zkgpu.synthetic import SyntheticStark
     nbe = log_n + blow
     steps = [nbe]
@@ -106,6 +112,9 @@ def stark_instance(log_n, blow, ncols, n_queries, fork9=False):
         steps.append(steps[-1] - 4)
     if steps[-1] > 5:
         steps.append(5)
+    if fork9 == "zkevm":
+        from zkgpu.zkevm_shaped import ZkevmShapedStark
+        return ZkevmShapedStark.create(n_bits=log_n, n_queries=n_queries, fri_steps=steps)
     if fork9:
         return SyntheticStark.fork9(n_bits=log_n, n_queries=n_queries, fri_steps=steps)
     # cm1 = 3t constrained triples + free columns + 3 lookup columns (A, B, C);
@@ -114,6 +123,11 @@ def stark_instance(log_n, blow, ncols, n_queries, fork9=False):
     t = (ncols - 3) // 3
     return SyntheticStark(n_bits=log_n, blowup_bits=blow, t=t, n_free=ncols - 3 - 3 * t, m=6, n_k=26,
                           n_queries=n_queries, fri_steps=steps, n_lookups=2)
+
+
+def _kind(args):
+    """stark_instance's fork9 argument from the command line"""
+    return "zkevm" if getattr(args, "zkevm_shaped", False) else args.fork9
 
 
 def _cpu_model():
@@ -595,7 +609,8 @@ def sharded_children(args, world, rank, local, dist, torch):
     import subprocess
     # fork-9 widths: 2^23 rows from W = 4 (plan 190 GB per rank), 2^22 rows
     # below it (2^23 needs 386 GB on one GPU, 317 GB per rank at W = 2)
-    runs = [("config4", []), ("fork9", ["--fork9"] + (["--log-n", "22"] if world < 4 and args.log_n > 22 else []))]
+    small = ["--log-n", "22"] if world < 4 and args.log_n > 22 else []
+    runs = [("config4", []), ("fork9", ["--fork9"] + small), ("fork9_zkevm_shaped", ["--zkevm-shaped"] + small)]
     out = {}
     failed = False
     for name, extra in runs:
@@ -695,7 +710,7 @@ def main():
                 sc.commit(trace)
         elif args.workload == "stark":
             from zkgpu.stark import GpuStark
-            inst = stark_instance(args.log_n, args.blowup_bits, C, args.queries, args.fork9)
+            inst = stark_instance(args.log_n, args.blowup_bits, C, args.queries, _kind(args))
             gs = GpuStark(inst)  # setup: constants, constant LDE + tree (untimed; files in the reference)
             gs.witness()         # executor stand-in: committed trace cm1 in HBM (untimed)
 
@@ -712,7 +727,7 @@ def main():
         elif args.workload == "stark-sharded":
             # the C++ row-sharded prover (host/sharded_starks.hpp) over RCCL
             from zkgpu.stark import GpuStark, RcclComm
-            inst = stark_instance(args.log_n, args.blowup_bits, C, args.queries, args.fork9)
+            inst = stark_instance(args.log_n, args.blowup_bits, C, args.queries, _kind(args))
             comm = RcclComm()
             gs = GpuStark(inst, comm=comm)
             gs.witness()
@@ -782,7 +797,9 @@ def main():
         elif args.workload == "stark-sharded":
             workload = ("ONE %s STARK proof (2^%d trace, cm1/cm2/cm3/cm4 = %d/%d/%d/%d, %d constants, %d queries) "
                         "row-sharded over %d rank(s): n and 2n domains by rows, NTT-transpose all-to-all per commit"
-                        % ("fork-9-width" if args.fork9 else "config-4", args.log_n, inst.n_cm1, inst.n_cm2,
+                        % ("zkEVM-shaped (fork-9 widths + the five zkEVM-shaped expression programs, "
+                           "zkgpu/zkevm_shaped.py)" if args.zkevm_shaped else
+                           "fork-9-width" if args.fork9 else "config-4", args.log_n, inst.n_cm1, inst.n_cm2,
                            inst.n_cm3, inst.n_cm4, inst.n_const, args.queries, world))
             parallelism = ("one proof, extended domain row-sharded x%d (%s): RCCL exchange column->row blocks + "
                            "halo rows per commit, q/f row gathers" % (world, "C++ prover, host/sharded_starks.hpp"

@@ -22,12 +22,18 @@ INSTANCES = {
     # 389 tmpExp, two plookups; next-row reads and shifted stores in the
     # n-domain stage programs): BASELINE configs[4]'s shape at 2^10 rows
     "fork9": dict(fork9=True, n_bits=10),
+    # the fork-9 widths with the five zkEVM-shaped expression programs in the
+    # stage slots (zkgpu/zkevm_shaped.py): configs[4]'s programs
+    "zkevm": dict(zkevm=True, n_bits=10),
 }
 
 
 def _inst(name):
     from zkgpu.synthetic import SyntheticStark
     a = dict(INSTANCES[name])
+    if a.pop("zkevm", False):
+        from zkgpu.zkevm_shaped import ZkevmShapedStark
+        return ZkevmShapedStark.create(**a)
     if a.pop("fork9", False):
         return SyntheticStark.fork9(**a)
     return SyntheticStark(**a)
@@ -137,7 +143,8 @@ def _free_port():
 
 @pytest.mark.parametrize("world,name,comm", [(2, "lookups", "gloo"), (4, "lookups", "gloo"), (2, "blowup4", "gloo"),
                                              (2, "lookups", "shm"), (4, "blowup4", "shm"), (8, "lookups", "shm"),
-                                             (2, "fork9", "gloo"), (8, "fork9", "shm"), (4, "lookups", "shm-rows")])
+                                             (2, "fork9", "gloo"), (8, "fork9", "shm"), (4, "lookups", "shm-rows"),
+                                             (2, "zkevm", "shm"), (8, "zkevm", "shm")])
 def test_sharded_multiprocess_equals_oracle(oracle_proofs, world, name, comm):
     """gloo = HostStagedComm (Python, torch.distributed); shm = ShmComm
     (host/comm_host.hpp, shared memory + process-shared barriers); -rows: the

@@ -53,16 +53,20 @@ def consts():
             rng.integers(0, P, (2048, 3), dtype=np.uint64))
 
 
-# bench.py's STARK instances at its default size (configs[3] / configs[4])
-STARKS = (("config4", False), ("fork9", True))
+# bench.py's STARK instances at its default size (configs[3] / configs[4]),
+# and the zkEVM-shaped one (zkgpu/zkevm_shaped.py; its stage programs do not
+# depend on the row count, so the tests' 2^10 proof uses these kernels too)
+STARKS = (("config4", False), ("fork9", True), ("zkevm", "zkevm"))
 STARK_PROGS = ("step0", "step1", "step2", "step3prev", "step3", "step42ns", "step52ns")
+_INSTS = {}
 
 
 def stark_program(inst_name, pname):
     sys.path.insert(0, ROOT)
-    import bench
-    inst = bench.stark_instance(23, 1, 100, 128, dict(STARKS)[inst_name])
-    return inst.programs.get(pname)
+    if inst_name not in _INSTS:
+        import bench
+        _INSTS[inst_name] = bench.stark_instance(23, 1, 100, 128, dict(STARKS)[inst_name])
+    return _INSTS[inst_name].programs.get(pname)
 
 
 def get_program(spec):

@@ -1293,8 +1293,16 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             const char *e = getenv("ZKGPU_ZXP_JIT_LCACHE_GAP");
             return e ? atoi(e) : 0;
         }();
-        const bool lc = split && lslots > 0 && lds_column_cache(body, lslots, lgap) > 0;
-        appendf(src, "#define ZKJIT_LCACHE %d\n", lc ? lslots : 0);
+        // LDS budget of one workgroup (64 KB): the limb double buffer (kbuf)
+        // or the whole limb table, then as many cache slots as still fit
+        // (none: the uncached source)
+        const size_t lds_limbs = kchunk ? 2 * JIT_KCHUNK * 4 : (jit_kl_lds(kl.size()) ? kl.size() * 4 : 0);
+        const size_t slot_bytes = (size_t)rows * 256 * 8;
+        const size_t lds_budget = 64 * 1024;
+        const int fit = lds_limbs >= lds_budget ? 0 : (int)((lds_budget - lds_limbs) / slot_bytes);
+        const int slots = std::min(lslots, fit);
+        const bool lc = split && slots > 0 && lds_column_cache(body, slots, lgap) > 0;
+        appendf(src, "#define ZKJIT_LCACHE %d\n", lc ? slots : 0);
     }
     src += k_kernel_head;
     // per-row text carries a ` (-> _r) and ~ (-> r) on its line; expand()

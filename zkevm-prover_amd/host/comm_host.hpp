@@ -26,7 +26,10 @@ struct HostCommHeader {
     uint32_t world;
     uint64_t capacity;
     uint64_t run;                 // this run's tag (run_tag_hash): a stale segment never matches
-    std::atomic<uint32_t> error;  // sticky: a rank failed inside an exchange
+    // error[k % 3]: a rank failed inside exchange k.  One slot per exchange
+    // (cleared two exchanges ahead, see host_exchange): a rank still reading
+    // exchange k's flag never sees a failure a faster rank raised in k + 1
+    std::atomic<uint32_t> error[3];
     pthread_barrier_t barrier;
 };
 
@@ -54,6 +57,7 @@ struct HostCommCtx {
     uint64_t size = 0;
     uint32_t rank = 0, world = 0;
     uint64_t capacity = 0;
+    uint64_t seq = 0;  // exchanges done (the same on every rank: exchanges are collective)
 
     static uint64_t header_bytes() { return (sizeof(HostCommHeader) + 4095) & ~4095ULL; }
     uint64_t box_bytes() const { return 8 + HOST_COMM_MAX_OPS * sizeof(HostCommEntry) + capacity; }
@@ -70,12 +74,20 @@ struct HostCommCtx {
 };
 
 // Every rank reaches both barriers whatever happens: a rank that fails
-// raises the shared (sticky) error flag and still waits, so one rank's error
-// is every rank's non-zero return instead of a hang in the barrier.
+// raises this exchange's error flag and still waits, so one rank's error is
+// every rank's non-zero return for the same exchange instead of a hang in the
+// barrier.  Exchange k uses slot k % 3; after barrier 1 of exchange k every
+// rank has finished exchange k - 1 (its reads included), so slot (k + 1) % 3
+// -- last read in exchange k - 2 -- is cleared there, and no rank can raise it
+// for exchange k + 1 before passing barrier 2 of k, which waits for every
+// rank's clear.
 static int host_exchange(void *vctx, const zkgpu_comm_op *ops, uint32_t n_ops)
 {
     HostCommCtx &c = *(HostCommCtx *)vctx;
     HostCommHeader *h = c.hdr();
+    std::atomic<uint32_t> &err = h->error[c.seq % 3];
+    std::atomic<uint32_t> &next = h->error[(c.seq + 1) % 3];
+    c.seq++;
     int rc = 0;
     uint64_t off = 0, n = 0;
     HostCommEntry *tab = c.entries(c.rank);
@@ -98,9 +110,10 @@ static int host_exchange(void *vctx, const zkgpu_comm_op *ops, uint32_t n_ops)
         off += o.bytes;
     }
     c.n_entries(c.rank) = n;
-    if (rc) h->error.store(1);
+    if (rc) err.store(1);
     if (c.wait()) return -1;
-    if (h->error.load()) {
+    next.store(0);
+    if (err.load()) {
         (void)c.wait();
         return rc ? rc : fail("host comm: another rank failed in this exchange");
     }
@@ -123,9 +136,9 @@ static int host_exchange(void *vctx, const zkgpu_comm_op *ops, uint32_t n_ops)
         }
         i++;
     }
-    if (rc) h->error.store(1);
+    if (rc) err.store(1);
     if (c.wait()) return -1;
-    if (h->error.load()) return rc ? rc : fail("host comm: another rank failed in this exchange");
+    if (err.load()) return rc ? rc : fail("host comm: another rank failed in this exchange");
     return 0;
 }
 

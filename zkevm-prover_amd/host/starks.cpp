@@ -188,6 +188,9 @@ public:
         void *v = nullptr;
         CK(zkgpu_dev_malloc(&v, elems * 8));
         allocs.push_back(v);
+        // zeroed, as the reference's calloc'd memory map (prover.cpp:94-116):
+        // a column no stage writes reads 0, in every proof
+        CK(zkgpu_memset_dev(v, 0, elems * 8));
         *p = (uint64_t *)v;
         return 0;
     }
@@ -965,7 +968,7 @@ int zkgpu_comm_host_create(zkgpu_comm *comm, const char *name, uint32_t world, u
         h->world = world;
         h->capacity = capacity;
         h->run = run;
-        h->error.store(0);
+        for (auto &e : h->error) e.store(0);
         h->ready.store(1, std::memory_order_release);
     } else {
         // wait (up to 60 s) for rank 0's segment of THIS run: a segment left

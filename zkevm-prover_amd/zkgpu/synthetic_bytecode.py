@@ -130,16 +130,20 @@ class _Reuse:
         return k
 
 
-def generate(name="step42ns", seed=1, shape=None, isa=None, scale=1.0):
+def generate(name="step42ns", seed=1, shape=None, isa=None, scale=1.0, reserved=None, readable=None):
     """(ops, args) uint64 arrays of a synthetic program shaped like the
     reference's `name` program: step42ns (constraint quotient), step2prev /
     step3prev / step3 (stage-2/3 column programs with shifted stores) or
     step52ns (FRI polynomial); scale < 1 keeps that fraction of every opcode
-    count (same mix, same map)."""
+    count (same mix, same map).  Stage programs inside a proof
+    (zkgpu/zkevm_shaped.py): reserved = {section name: columns the program
+    must not write}, readable = {section name: the only columns it may read}
+    (sections absent from readable: any column); None = no restriction (the
+    same program as before for the same seed)."""
     if name == "step42ns":
         return _generate_step42ns(seed, shape, isa, scale)
     if name in ("step2prev", "step3prev", "step3"):
-        return _generate_stage(name, seed, shape, isa, scale)
+        return _generate_stage(name, seed, shape, isa, scale, reserved, readable)
     if name == "step52ns":
         return _generate_step52ns(seed, shape, isa, scale)
     raise ValueError("unknown program %r" % name)
@@ -347,7 +351,7 @@ def _find(table, pred):
     return [c for c, (_, mops) in sorted(table.items()) if pred(mops)]
 
 
-def _generate_stage(name, seed=1, shape=None, isa=None, scale=1.0):
+def _generate_stage(name, seed=1, shape=None, isa=None, scale=1.0, reserved=None, readable=None):
     """A stage-2/3 column program (step2prev / step3prev / step3,
     zkevm.chelpers.<step>.parser.cpp): the reference's opcode histogram over
     the n-domain sections, every store opcode (86-120) writing a column of
@@ -362,6 +366,13 @@ def _generate_stage(name, seed=1, shape=None, isa=None, scale=1.0):
     rng = np.random.default_rng(seed)
     g = _Gen(name, shape, rng)
     sh = g.sh
+    reserved = reserved or {}
+    if readable is not None:  # reads only from the readable columns (same subset sizes where they allow)
+        for s_ in g.rsecs:
+            if s_ in readable:
+                ok = np.array(sorted(readable[s_]), np.int64)
+                n = min(sh["reads"][s_]["distinct_cols"], ok.size)
+                g.rcols[s_] = np.sort(rng.choice(ok, size=n, replace=False)) if n else ok[:0]
     hist = {int(k): max(1, int(round(v * scale))) for k, v in sh["opcode_hist"].items()}
     is_store = lambda c: table[c][1][0][1] is not None and table[c][1][0][1][0] in ("P", "PS")
     stores = {c: n for c, n in hist.items() if is_store(c)}
@@ -376,10 +387,11 @@ def _generate_stage(name, seed=1, shape=None, isa=None, scale=1.0):
     written = {}
     for s_ in wsec:
         width = g.map[s_]["width"]
-        want = min(sh["writes"][s_]["distinct_cols"], width)
+        res = reserved.get(s_, ())
+        want = min(sh["writes"][s_]["distinct_cols"], width - len(res))
         share3 = n3 * 3 / max(1, n1 + 3 * n3)
         k3 = int(want * share3 / 3)
-        cols = list(rng.permutation(width))
+        cols = [c for c in rng.permutation(width) if c not in res] if res else list(rng.permutation(width))
         sl, used = [], set()
         for c in cols:
             if len(sl) >= k3:
@@ -399,9 +411,12 @@ def _generate_stage(name, seed=1, shape=None, isa=None, scale=1.0):
     for s_ in g.rsecs:
         if s_ in written:
             width = g.map[s_]["width"]
-            free = np.array(sorted(set(range(width)) - written[s_]), np.int64)
+            ok = set(range(width)) if readable is None or s_ not in readable else set(readable[s_])
+            free = np.array(sorted(ok - written[s_]), np.int64)
             n = min(sh["reads"][s_]["distinct_cols"], free.size)
-            g.rcols[s_] = np.sort(rng.choice(free, size=n, replace=False))
+            g.rcols[s_] = np.sort(rng.choice(free, size=n, replace=False)) if n else free[:0]
+    # columns no read may touch (a dim-3 read covers 3 consecutive columns)
+    unread = {s_: set(range(g.map[s_]["width"])) - set(readable[s_]) for s_ in (readable or {})}
     cells = []  # written (offset, width, dim, shift) cells, for forwarded reads
     copy1 = _find(table, lambda m: len(m) == 1 and m[0][0] == "copy" and m[0][1][0] == "T1" and m[0][2][0] == "P"
                   and m[0][2][1] == 1)[0]
@@ -430,7 +445,7 @@ def _generate_stage(name, seed=1, shape=None, isa=None, scale=1.0):
             if not len(cols):
                 continue
             width = g.map[s2]["width"]
-            bad = written.get(s2, set())
+            bad = written.get(s2, set()) | unread.get(s2, set())
             for _ in range(64):
                 c = int(cols[rng.integers(len(cols))])
                 c = min(c, width - dim)
