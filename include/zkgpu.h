@@ -287,6 +287,11 @@ int zkgpu_scale_by_powers_dev(uint64_t *cols, uint64_t ld, uint32_t ncols, uint6
 /* quotient split (starks.cpp:266-281): qq2 col 3p+d row k = qq1 col d row pN+k * shift_in^p, k < n */
 int zkgpu_qsplit_dev(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t q_deg,
                      uint64_t shift_in);
+/* the same for dim input columns into output columns stride*p + d (d < dim
+ * <= stride): a column owner of the row-sharded prover splits its one
+ * quotient column (dim 1, stride 3) */
+int zkgpu_qsplit_cols_dev(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t q_deg,
+                          uint64_t shift_in, uint32_t dim, uint32_t stride);
 
 /* plookup h1/h2 (Polinomial::calculateH1H2_opt1 / _opt3, polinomial.hpp:349-583,
  * called at starks.cpp:104-127): f, t, h1, h2 are n-row columns of dimension

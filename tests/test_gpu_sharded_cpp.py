@@ -171,3 +171,6 @@ def test_sharded_multiprocess_equals_oracle(oracle_proofs, world, name, comm):
     for _, proof, timers, _ in res:
         _assert_same(proof, oracle_proofs[name])
         assert timers["STARK_STEP_1_EXCHANGE"] >= 0
+        # packed exchanges: one message per peer and direction, whatever the
+        # column count (the commits of fork-9's 751 columns included)
+        assert 0 < timers["COUNT_COMM_MAX_OPS"] <= 2 * (world - 1), timers["COUNT_COMM_MAX_OPS"]

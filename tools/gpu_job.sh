@@ -3,7 +3,7 @@
 # stops at the first fault / abort / segfault / timeout (exit >= 124 or
 # signal), but continues past an ordinary test failure (exit 1).
 # Usage: tools/gpu_job.sh <step>...
-#   steps: tests large smoke bench instbench bwbench parser step42ns prof pmc starkpmc cpufull merkle commit sharded
+#   steps: tests large smoke bench instbench bwbench parser step42ns prof pmc starkpmc cpufull merkle zkevm sharded
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOTDIR=$(pwd)
@@ -124,14 +124,14 @@ for step in "$@"; do
         ok_or_stop $? "bench merkle"
         cat gpurun_out/bench_merkle.json
         ;;
-    commit)
-        timeout -k 10 600 python bench.py --workload commit --steps 3 --warmup 1 \
-            > gpurun_out/bench_commit.json 2> gpurun_out/bench_commit.err
-        ok_or_stop $? "bench commit"
-        cat gpurun_out/bench_commit.json
+    zkevm)
+        timeout -k 10 300 python -u bench.py --workload stark --zkevm-shaped --log-n 22 --steps 3 --warmup 1 --no-cpu \
+            --no-lde --no-handoff --no-s42 --no-sharded > gpurun_out/bench_zkevm.json 2> gpurun_out/bench_zkevm.err
+        ok_or_stop $? "bench zkevm-shaped 2^22"
+        cat gpurun_out/bench_zkevm.json
         ;;
     sharded)
-        timeout -k 10 600 $PYT tests/test_sharded_stark.py -m gpu > gpurun_out/pytest_sharded.log 2>&1
+        timeout -k 10 600 $PYT tests/test_gpu_sharded_cpp.py tests/test_gpu_zkevm_shaped.py > gpurun_out/pytest_sharded.log 2>&1
         ok_or_stop $? "pytest sharded stark gpu"
         tail -3 gpurun_out/pytest_sharded.log
         ;;

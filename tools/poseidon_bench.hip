@@ -141,6 +141,58 @@ __global__ void __launch_bounds__(256) k_perm_clk(uint64_t *st_all, uint64_t n, 
     }
 }
 
+// partial-round tables in memory: scalar loads (constant address space, not
+// foldable) or staged into LDS per workgroup
+__constant__ uint32_t g_psb_d0[759];
+__constant__ uint32_t g_psb_bl[3828];
+
+__global__ void __launch_bounds__(256) k_perm_smem(uint64_t *st_all, uint64_t n, int reps)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t st[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) st[k] = st_all[k * n + i];
+    for (int r = 0; r < reps; r++) perm_fast_tab(st, g_psb_d0, g_psb_bl);
+#pragma unroll
+    for (int k = 0; k < 12; k++) st_all[k * n + i] = gl_canon(st[k]);
+}
+
+// the same with the table addresses opaque per permutation (no loop-invariant
+// hoisting of the scalar loads out of the permutation loop)
+typedef const __attribute__((address_space(4))) uint32_t c4u32;
+__global__ void __launch_bounds__(256) k_perm_smem2(uint64_t *st_all, uint64_t n, int reps)
+{
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t st[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) st[k] = st_all[k * n + i];
+    for (int r = 0; r < reps; r++) {
+        c4u32 *d0 = (c4u32 *)g_psb_d0, *bl = (c4u32 *)g_psb_bl;
+        asm volatile("" : "+s"(d0), "+s"(bl));
+        perm_fast_tab(st, (const uint32_t *)d0, (const uint32_t *)bl);
+    }
+#pragma unroll
+    for (int k = 0; k < 12; k++) st_all[k * n + i] = gl_canon(st[k]);
+}
+
+__global__ void __launch_bounds__(256) k_perm_lds(uint64_t *st_all, uint64_t n, int reps)
+{
+    __shared__ uint32_t d0[760], bl[3828];
+    for (int k = threadIdx.x; k < 759; k += 256) d0[k] = g_psb_d0[k];
+    for (int k = threadIdx.x; k < 3828; k += 256) bl[k] = g_psb_bl[k];
+    __syncthreads();
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t st[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) st[k] = st_all[k * n + i];
+    for (int r = 0; r < reps; r++) perm_fast_tab(st, d0, bl);
+#pragma unroll
+    for (int k = 0; k < 12; k++) st_all[k * n + i] = gl_canon(st[k]);
+}
+
 // occupancy targets: the product leaf kernel runs at 89 VGPRs = 5 waves/SIMD
 template <int W>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) k_perm_w(uint64_t *st_all, uint64_t n,
@@ -168,6 +220,8 @@ int main()
     }
     uint64_t *d;
     (void)hipMalloc(&d, 12 * n * 8);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_psb_d0), ZKGPU_PSB_D0, sizeof ZKGPU_PSB_D0);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_psb_bl), ZKGPU_PSB_BLOCKS, sizeof ZKGPU_PSB_BLOCKS);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
@@ -189,8 +243,11 @@ int main()
         {"fast, 8 waves/SIMD target", k_perm_w<8>},
         {"split: 8 full rounds only", k_perm<7>},
         {"split: 22 partial rounds only", k_perm<8>},
+        {"fast, tables by scalar loads", k_perm_smem},
+        {"fast, tables in LDS", k_perm_lds},
+        {"fast, scalar loads, opaque table", k_perm_smem2},
     };
-    const int nthreads_div[] = {1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 2, 1, 1, 1, 1, 1};
+    const int nthreads_div[] = {1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 2, 1, 1, 1, 1, 1, 1, 1, 1};
     int bad = 0;
     const int nv = sizeof(ks) / sizeof(ks[0]);
     for (int v = 0; v < nv; v++) {
@@ -206,7 +263,7 @@ int main()
             if (ms < best) best = ms;
         }
         (void)hipMemcpy(v ? o : ref, d, 12 * n * 8, hipMemcpyDeviceToHost);
-        bool same = v == 0 || v >= 14 || memcmp(o, ref, 12 * n * 8) == 0;
+        bool same = v == 0 || v == 14 || v == 15 || memcmp(o, ref, 12 * n * 8) == 0;
         bad |= !same;
         printf("%-34s %8.3f ms  %7.2f Gperm/s  %s\n", ks[v].name, best, (double)n * reps / (best * 1e-3) / 1e9,
                same ? "match" : "MISMATCH");

@@ -1330,7 +1330,17 @@ int zkgpu_qsplit_dev(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t 
     int rc;
     if ((rc = require_init())) return rc;
     if (!n) return 0;
-    return qsplit(qq2, ld2, qq1, ld1, n, q_deg, shift_in, g_ctx.stream);
+    return qsplit(qq2, ld2, qq1, ld1, n, q_deg, shift_in, 3, 3, g_ctx.stream);
+}
+
+int zkgpu_qsplit_cols_dev(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t q_deg,
+                          uint64_t shift_in, uint32_t dim, uint32_t stride)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!n || !dim) return 0;
+    if (dim > stride) return set_error(ZKGPU_ERR_ARG, "qsplit_cols: dim %u > stride %u", dim, stride);
+    return qsplit(qq2, ld2, qq1, ld1, n, q_deg, shift_in, dim, stride, g_ctx.stream);
 }
 
 int zkgpu_h1h2_dev(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint64_t *f, uint64_t f_ld,

@@ -400,21 +400,25 @@ __device__ __forceinline__ void psb_steps(uint64_t &x, uint64_t y[], const uint6
 
 // Partial rounds in block dot-product form (gen_poseidon_sparse.py
 // derive_blocks); input: lanes after the first four full rounds (PRE added),
-// output: lanes with the round-26 constants added.
-__device__ __forceinline__ void partial_rounds_blocks(uint64_t st[12])
+// output: lanes with the round-26 constants added.  D0 / BL: the tables
+// ZKGPU_PSB_D0 / ZKGPU_PSB_BLOCKS (compile-time by default; a copy in
+// memory the compiler cannot fold is read with scalar loads instead of one
+// s_mov per coefficient)
+template <typename TP = const uint32_t *>
+__device__ __forceinline__ void partial_rounds_blocks(uint64_t st[12], TP D0 = ZKGPU_PSB_D0, TP BL = ZKGPU_PSB_BLOCKS)
 {
     uint64_t L[11];
 #pragma unroll
     for (int i = 0; i < 11; i++) {
-        Dot3 d(&ZKGPU_PSB_D0[i * 69]);
+        Dot3 d(&D0[i * 69]);
 #pragma unroll
-        for (int j = 0; j < 11; j++) d.term(st[1 + j], &ZKGPU_PSB_D0[i * 69 + 3 + 6 * j]);
+        for (int j = 0; j < 11; j++) d.term(st[1 + j], &D0[i * 69 + 3 + 6 * j]);
         L[i] = pfin(d);
     }
     uint64_t x = st[0];
 #pragma unroll 1
     for (int b = 0; b < ZKGPU_PSB_NBLOCKS; b++) {
-        const uint32_t *T = &ZKGPU_PSB_BLOCKS[b * ZKGPU_PSB_BLOCK_WORDS];
+        const uint32_t *T = &BL[b * ZKGPU_PSB_BLOCK_WORDS];
         uint64_t y[ZKGPU_PSB_BLOCK];
         psb_steps(x, y, L, T, std::make_integer_sequence<int, ZKGPU_PSB_BLOCK>{});
         constexpr int base = psb_xoff(ZKGPU_PSB_BLOCK);
@@ -439,6 +443,17 @@ __device__ __forceinline__ void perm_fast(uint64_t st[12])
     for (int s = 0; s < 12; s++) st[s] = gl_add(st[s], ZKGPU_POSEIDON_RC[s]);
     full_rounds_fold(st, 0);
     partial_rounds_blocks(st);
+    full_rounds_fold(st, 26);
+}
+
+// perm_fast with the partial-round tables read from memory (D0, BL: copies
+// of ZKGPU_PSB_D0 / ZKGPU_PSB_BLOCKS); bit-identical
+__device__ __forceinline__ void perm_fast_tab(uint64_t st[12], const uint32_t *D0, const uint32_t *BL)
+{
+#pragma unroll
+    for (int s = 0; s < 12; s++) st[s] = gl_add(st[s], ZKGPU_POSEIDON_RC[s]);
+    full_rounds_fold(st, 0);
+    partial_rounds_blocks(st, D0, BL);
     full_rounds_fold(st, 26);
 }
 

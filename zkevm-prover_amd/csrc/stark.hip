@@ -622,16 +622,19 @@ __global__ void k_scale_powers(uint64_t *cols, uint64_t ld, uint32_t ncols, uint
     }
 }
 
-// qq2 column 3p+d, row k < N: qq1_d[p N + k] * shiftIn^p   (starks.cpp:266-281)
+// qq2 column stride*p+d, row k < N: qq1_d[p N + k] * shiftIn^p, d < dim
+// (starks.cpp:266-281: dim = stride = 3; the row-sharded prover's column
+// owners split one column, dim 1, into every third output column)
 __global__ void k_qsplit(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t qdeg,
-                         uint64_t shift_in)
+                         uint64_t shift_in, uint32_t dim, uint32_t stride)
 {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     uint64_t f = 1;
     for (uint32_t p = 0; p < qdeg; p++) {
-        for (int d = 0; d < 3; d++)
-            qq2[(uint64_t)(3 * p + d) * ld2 + k] = gl_canon(gl_mul(qq1[(uint64_t)d * ld1 + (uint64_t)p * n + k], f));
+        for (uint32_t d = 0; d < dim; d++)
+            qq2[(uint64_t)(stride * p + d) * ld2 + k] =
+                gl_canon(gl_mul(qq1[(uint64_t)d * ld1 + (uint64_t)p * n + k], f));
         f = gl_mul(f, shift_in);
     }
 }
@@ -804,9 +807,10 @@ int scale_powers(uint64_t *cols, uint64_t ld, uint32_t ncols, uint64_t n, uint64
 }
 
 int qsplit(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t qdeg,
-           uint64_t shift_in, hipStream_t s)
+           uint64_t shift_in, uint32_t dim, uint32_t stride, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_qsplit, dim3(nblk(n, 256)), dim3(256), 0, s, qq2, ld2, qq1, ld1, n, qdeg, shift_in);
+    hipLaunchKernelGGL(k_qsplit, dim3(nblk(n, 256)), dim3(256), 0, s, qq2, ld2, qq1, ld1, n, qdeg, shift_in, dim,
+                       stride);
     return check_launch("k_qsplit");
 }
 

@@ -190,7 +190,7 @@ int xdiv_rows(uint64_t *out0, uint64_t *out1, uint64_t ld, int interleaved, cons
 int ext_powers(uint64_t *out, uint64_t ld, const uint64_t base[3], uint64_t n, hipStream_t s);
 int scale_powers(uint64_t *cols, uint64_t ld, uint32_t ncols, uint64_t n, uint64_t base, hipStream_t s);
 int qsplit(uint64_t *qq2, uint64_t ld2, const uint64_t *qq1, uint64_t ld1, uint64_t n, uint32_t qdeg,
-           uint64_t shift_in, hipStream_t s);
+           uint64_t shift_in, uint32_t dim, uint32_t stride, hipStream_t s);
 int cols3_to_interleaved(uint64_t *out, const uint64_t *cols, uint64_t ld, uint64_t n, hipStream_t s);
 int h1h2(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint64_t *f, uint64_t f_ld,
          const uint64_t *t, uint64_t t_ld, uint64_t n, uint32_t dim, uint64_t *missing_row, hipStream_t s);

@@ -60,6 +60,13 @@ public:
     uint64_t *cm4 = nullptr;    // quotient pieces, whole extended domain (n_cm4 x NE)
     uint64_t *xchg = nullptr;   // all-gather staging, W slots
     uint64_t *hsend = nullptr, *hrecv = nullptr;  // halo / spill / 2n-halo staging (hcap words each)
+    // per-peer packing: every exchange posts at most one send and one receive
+    // per peer (2 (W - 1) operations), whatever the column count -- a rank's
+    // slices for a peer are gathered into its region of pack_s (stride_s
+    // words per peer), a peer's message lands in its region of pack_r
+    uint64_t *pack_s = nullptr, *pack_r = nullptr;
+    uint64_t stride_s = 0, stride_r = 0;
+    uint32_t max_ops = 0;  // largest exchange so far (operations posted by this rank)
     uint64_t *puw = nullptr;    // one plookup's f, t, h1, h2 over the whole n domain (12 x N)
     uint64_t slot = 0, hcap = 0;
     struct Tree {
@@ -195,11 +202,25 @@ public:
             S.ncols[s] = 3;
         }
         const uint64_t ms = max_share();
-        if (dalloc(&gath, 3 * NE) || (W > 1 && (dalloc(&ext, ms * NE) || dalloc(&coln, ms * N)))) return -1;
-        // halo staging: the n-domain halos / spills of every column, or the
-        // 2n-domain halos of a column share for every peer
-        hcap = std::max<uint64_t>((uint64_t)5 * wmax * std::max<uint64_t>(hn, 1), (uint64_t)W * ms * H);
+        // ext: the LDE of the share, and before it the transposes' receive
+        // staging (W slots of ms x ldn words: more than ms x NE only for tiny
+        // domains, where the 64-row halo padding is not small against nb)
+        if (dalloc(&gath, 3 * NE) ||
+            (W > 1 && (dalloc(&ext, std::max<uint64_t>(ms * NE, (uint64_t)W * ms * ldn)) || dalloc(&coln, ms * N))))
+            return -1;
+        // halo staging: the n-domain halos / spills of every column
+        hcap = (uint64_t)5 * wmax * std::max<uint64_t>(hn, 1);
         if (dalloc(&hsend, hcap) || dalloc(&hrecv, hcap)) return -1;
+        if (W > 1) {
+            // send: a commit's column share with its halo, ld BH (the largest);
+            // the quotient's q columns / piece blocks; a plookup's f / t
+            // receive: q columns, piece blocks, f rows, a plookup's f / t (the
+            // n-domain transpose lands in ext, free at that point)
+            const uint64_t piece = 3ULL * info.q_deg * (B + nb);
+            stride_s = std::max<uint64_t>({ms * BH, 3 * B, piece, 6 * nb});
+            stride_r = std::max<uint64_t>({3 * B, piece, 6 * nb});
+            if (dalloc(&pack_s, W * stride_s) || dalloc(&pack_r, W * stride_r)) return -1;
+        }
         if (info.n_pu && dalloc(&puw, 12 * N)) return -1;
         for (auto &t : trees)
             if (dalloc(&t.nodes, zkgpu_gl_merkle_num_elements(B))) return -1;
@@ -228,6 +249,9 @@ public:
     int exchange()
     {
         if (ops.empty()) return 0;
+        max_ops = std::max(max_ops, (uint32_t)ops.size());
+        if (ops.size() > 2ULL * (W - 1))
+            return fail("exchange of %zu operations: more than one send and one receive per peer", ops.size());
         if (comm.exchange(comm.ctx, ops.data(), (uint32_t)ops.size()))
             return fail("zkgpu_comm exchange of %zu operations failed (rank %u of %u)", ops.size(), R, W);
         ops.clear();
@@ -257,17 +281,99 @@ public:
         return 0;
     }
 
-    // the rank's 3 x B block (ld B) of q or f -> full (3 x NE, ld NE) on every rank
+    // the rank's 3 x B block (ld B: one contiguous 3B-word message) of f ->
+    // full (3 x NE, ld NE) on every rank
     int gather_rows(const uint64_t *blk, uint64_t *full)
     {
         for (uint32_t d = 0; d < W; d++)
-            if (d != R)
-                for (int c = 0; c < 3; c++) op(d, 1, blk + c * B, B * 8);
+            if (d != R) op(d, 1, blk, 3 * B * 8);
         for (uint32_t s = 0; s < W; s++)
+            if (s != R) op(s, 0, pack_r + s * stride_r, 3 * B * 8);
+        CK(zkgpu_copy_rows_dev(full, NE, (uint64_t)R * B, nullptr, blk, B, 0, 0, nullptr, 3, B));
+        if (exchange()) return -1;
+        for (uint32_t s = 0; s < W; s++)
+            if (s != R) CK(zkgpu_copy_rows_dev(full, NE, (uint64_t)s * B, nullptr, pack_r + s * stride_r, B, 0, 0, nullptr, 3, B));
+        return 0;
+    }
+
+    // quotient split (starks.cpp:255-296) by column owners: q column j
+    // (j < 3) belongs to rank j mod W.  The q blocks go to the owners (one
+    // message per peer), each owner interpolates its column over the whole
+    // extended domain, splits it into q_deg pieces (output columns 3p + j) and
+    // evaluates them on the extended and the n domain; every rank gets the
+    // row blocks of all pieces back (one message per owner).  Replaces the
+    // transform of all three columns on every rank.
+    std::vector<uint32_t> q_owned(uint32_t r) const
+    {
+        std::vector<uint32_t> j;
+        for (uint32_t c = r; c < 3; c += W) j.push_back(c);
+        return j;
+    }
+    std::vector<uint32_t> pieces_of(const std::vector<uint32_t> &js) const
+    {
+        std::vector<uint32_t> c;
+        for (uint32_t p = 0; p < info.q_deg; p++)
+            for (uint32_t j : js) c.push_back(3 * p + j);
+        return c;
+    }
+    int quotient_sharded()
+    {
+        const std::vector<uint32_t> mine = q_owned(R), my_pieces = pieces_of(mine);
+        const uint64_t *qb = S.sec[SEC_Q_2NS];
+        // 1. q blocks to the column owners; the owned columns whole in gath
+        for (uint32_t d = 0; d < W; d++) {
+            const std::vector<uint32_t> js = q_owned(d);
+            if (d == R || js.empty()) continue;
+            CK(zkgpu_copy_rows_dev(pack_s + d * stride_s, B, 0, nullptr, qb, B, 0, 0, js.data(), (uint32_t)js.size(), B));
+            op(d, 1, pack_s + d * stride_s, js.size() * B * 8);
+        }
+        if (!mine.empty()) {
+            for (uint32_t s = 0; s < W; s++)
+                if (s != R) op(s, 0, pack_r + s * stride_r, mine.size() * B * 8);
+            CK(zkgpu_copy_rows_dev(gath, NE, (uint64_t)R * B, nullptr, qb, B, 0, 0, mine.data(), (uint32_t)mine.size(), B));
+        }
+        if (exchange()) return -1;
+        for (uint32_t s = 0; s < W && !mine.empty(); s++)
             if (s != R)
-                for (int c = 0; c < 3; c++) op(s, 0, full + c * NE + s * B, B * 8);
-        for (int c = 0; c < 3; c++) CK(zkgpu_memcpy_d2d(full + c * NE + R * B, blk + c * B, B * 8));
-        return exchange();
+                CK(zkgpu_copy_rows_dev(gath, NE, (uint64_t)s * B, nullptr, pack_r + s * stride_r, B, 0, 0, nullptr,
+                                       (uint32_t)mine.size(), B));
+        // 2. the owner's pieces (quotient_pieces for its columns)
+        const uint64_t shift_in = pw(inv(7), N);
+        for (size_t k = 0; k < mine.size(); k++) {
+            const uint32_t j = mine[k];
+            CK(zkgpu_gl_ntt_dev(qq1 + k * NE, NE, gath + k * NE, NE, NE, 1, 1));
+            for (uint32_t p = 0; p < info.q_deg; p++) CK(zkgpu_memset_dev(qq2 + (uint64_t)(3 * p + j) * NE, 0, NE * 8));
+            CK(zkgpu_qsplit_cols_dev(qq2 + (uint64_t)j * NE, NE, qq1 + k * NE, NE, N, info.q_deg, shift_in, 1, 3));
+            CK(zkgpu_gl_ntt_dev(cm4 + (uint64_t)j * NE, 3 * NE, qq2 + (uint64_t)j * NE, 3 * NE, NE, info.q_deg, 0));
+            for (uint32_t p = 0; p < info.q_deg; p++)
+                CK(zkgpu_memcpy_d2d(cm4_n + (uint64_t)(3 * p + j) * N, qq2 + (uint64_t)(3 * p + j) * NE, N * 8));
+            CK(zkgpu_scale_by_powers_dev(cm4_n + (uint64_t)j * N, 3 * N, info.q_deg, N, inv(7)));
+            CK(zkgpu_gl_ntt_dev(cm4_n + (uint64_t)j * N, 3 * N, cm4_n + (uint64_t)j * N, 3 * N, N, info.q_deg, 0));
+        }
+        // 3. every rank its row blocks of every piece (extended and n domain)
+        const uint32_t np = (uint32_t)my_pieces.size();
+        for (uint32_t d = 0; d < W && np; d++) {
+            if (d == R) continue;
+            uint64_t *m = pack_s + d * stride_s;
+            CK(zkgpu_copy_rows_dev(m, B, 0, nullptr, cm4, NE, (uint64_t)d * B, 0, my_pieces.data(), np, B));
+            CK(zkgpu_copy_rows_dev(m + (uint64_t)np * B, nb, 0, nullptr, cm4_n, N, (uint64_t)d * nb, 0, my_pieces.data(),
+                                   np, nb));
+            op(d, 1, m, (uint64_t)np * (B + nb) * 8);
+        }
+        for (uint32_t s = 0; s < W; s++) {
+            const uint32_t ns = (uint32_t)pieces_of(q_owned(s)).size();
+            if (s != R && ns) op(s, 0, pack_r + s * stride_r, (uint64_t)ns * (B + nb) * 8);
+        }
+        if (exchange()) return -1;
+        for (uint32_t s = 0; s < W; s++) {
+            const std::vector<uint32_t> ps = pieces_of(q_owned(s));
+            if (s == R || ps.empty()) continue;
+            const uint32_t ns = (uint32_t)ps.size();
+            CK(zkgpu_copy_rows_dev(cm4, NE, (uint64_t)R * B, ps.data(), pack_r + s * stride_r, B, 0, 0, nullptr, ns, B));
+            CK(zkgpu_copy_rows_dev(cm4_n, N, r0(), ps.data(), pack_r + s * stride_r + (uint64_t)ns * B, nb, 0, 0,
+                                   nullptr, ns, nb));
+        }
+        return 0;
     }
 
     static void hash_node(uint64_t out[4], const uint64_t *l, const uint64_t *r)
@@ -310,25 +416,29 @@ public:
     // the NTT transpose: rows [0, nb) of every column of n-domain section sec
     // to the rank owning the column; the rank's share [lo, hi) arrives in
     // coln (ld N) at rows [s nb, (s+1) nb) from rank s
+    // One message per peer: the peer's columns [dlo, dhi) of the block are
+    // contiguous (ld ldn; their halo / padding rows travel along, ~64 / nb of
+    // the bytes); received into ext (free until the LDE), then placed.
     int rows_to_share(uint32_t sec, uint32_t ncols)
     {
         uint32_t lo, hi;
         share(ncols, R, lo, hi);
+        const uint64_t slot = (uint64_t)max_share() * ldn;
         for (uint32_t d = 0; d < W; d++) {
             uint32_t dlo, dhi;
             share(ncols, d, dlo, dhi);
-            for (uint32_t c = dlo; c < dhi; c++) {
-                const uint64_t *src = S.sec[sec] + (uint64_t)c * ldn;
-                if (d == R)
-                    CK(zkgpu_memcpy_d2d(coln + (uint64_t)(c - lo) * N + r0(), src, nb * 8));
-                else
-                    op(d, 1, src, nb * 8);
-            }
+            if (d == R || dhi == dlo) continue;
+            op(d, 1, S.sec[sec] + (uint64_t)dlo * ldn, (uint64_t)(dhi - dlo) * ldn * 8);
         }
-        for (uint32_t s = 0; s < W; s++)
+        for (uint32_t s = 0; s < W && hi > lo; s++)
+            if (s != R) op(s, 0, ext + s * slot, (uint64_t)(hi - lo) * ldn * 8);
+        if (hi > lo)
+            CK(zkgpu_copy_rows_dev(coln, N, r0(), nullptr, S.sec[sec] + (uint64_t)lo * ldn, ldn, 0, 0, nullptr, hi - lo, nb));
+        if (exchange()) return -1;
+        for (uint32_t s = 0; s < W && hi > lo; s++)
             if (s != R)
-                for (uint32_t c = lo; c < hi; c++) op(s, 0, coln + (uint64_t)(c - lo) * N + (uint64_t)s * nb, nb * 8);
-        return exchange();
+                CK(zkgpu_copy_rows_dev(coln, N, (uint64_t)s * nb, nullptr, ext + s * slot, ldn, 0, 0, nullptr, hi - lo, nb));
+        return 0;
     }
 
     // rows [0, hn) of every written column -> the previous rank's halo rows
@@ -500,7 +610,6 @@ public:
     {
         uint32_t lo, hi;
         share(ncols, R, lo, hi);
-        const uint32_t ms = max_share();
         uint64_t *blk = S.sec[sec_e];
         if (W == 1) {  // one rank: the LDE straight into the block, then its halo (the first rows)
             tstart();
@@ -516,34 +625,27 @@ public:
         if (hi > lo) CK(zkgpu_gl_extend_pol_dev(ext, NE, src, src_ld, NE, N, hi - lo));
         if (lde_name && tstop(lde_name)) return -1;
         tstart();
+        // peer d's rows [d B, d B + B + H) (mod NE: the halo of the last
+        // block wraps) of the share, packed with the block's own ld BH: the
+        // message lands as whole block columns [lo, hi) on the peer
+        uint32_t log_ne = 0;
+        while ((1ULL << log_ne) < NE) log_ne++;
         for (uint32_t d = 0; d < W; d++) {
             if (d == R || hi == lo) continue;
-            for (uint32_t c = 0; c < hi - lo; c++) op(d, 1, ext + c * NE + (uint64_t)d * B, B * 8);
-            // the halo: the next block's first H rows, packed per peer
-            CK(zkgpu_copy_rows_dev(hsend + (uint64_t)d * ms * H, H, 0, nullptr, ext, NE, (uint64_t)((d + 1) % W) * B, 0,
-                                   nullptr, hi - lo, H));
-            op(d, 1, hsend + (uint64_t)d * ms * H, (uint64_t)(hi - lo) * H * 8);
+            CK(zkgpu_copy_rows_dev(pack_s + d * stride_s, BH, 0, nullptr, ext, NE, (uint64_t)d * B, log_ne, nullptr,
+                                   hi - lo, B + H));
+            op(d, 1, pack_s + d * stride_s, (uint64_t)(hi - lo) * BH * 8);
         }
         for (uint32_t s = 0; s < W; s++) {
             uint32_t slo, shi;
             share(ncols, s, slo, shi);
             if (s == R || shi == slo) continue;
-            for (uint32_t c = slo; c < shi; c++) op(s, 0, blk + (uint64_t)c * BH, B * 8);
-            op(s, 0, hrecv + (uint64_t)s * ms * H, (uint64_t)(shi - slo) * H * 8);
+            op(s, 0, blk + (uint64_t)slo * BH, (uint64_t)(shi - slo) * BH * 8);
         }
-        for (uint32_t c = lo; c < hi; c++)
-            CK(zkgpu_memcpy_d2d(blk + (uint64_t)c * BH, ext + (c - lo) * NE + (uint64_t)R * B, B * 8));
         if (hi > lo)
-            CK(zkgpu_copy_rows_dev(blk + (uint64_t)lo * BH, BH, B, nullptr, ext, NE, (uint64_t)((R + 1) % W) * B, 0,
-                                   nullptr, hi - lo, H));
+            CK(zkgpu_copy_rows_dev(blk + (uint64_t)lo * BH, BH, 0, nullptr, ext, NE, (uint64_t)R * B, log_ne, nullptr,
+                                   hi - lo, B + H));
         if (exchange()) return -1;
-        for (uint32_t s = 0; s < W; s++) {
-            uint32_t slo, shi;
-            share(ncols, s, slo, shi);
-            if (s == R || shi == slo) continue;
-            CK(zkgpu_copy_rows_dev(blk + (uint64_t)slo * BH, BH, B, nullptr, hrecv + (uint64_t)s * ms * H, H, 0, 0,
-                                   nullptr, shi - slo, H));
-        }
         if (xchg_name && tstop(xchg_name)) return -1;
         tstart();
         if (merkelize(t, blk, BH, ncols, root)) return -1;
@@ -668,20 +770,27 @@ public:
             const uint32_t *q = &pu[5 * k];
             const uint32_t d = q[4];
             uint64_t *fw = puw, *tw = puw + 3 * N, *h1w = puw + 6 * N, *h2w = puw + 9 * N;
-            for (uint32_t part = 0; part < 2; part++) {
-                uint64_t *whole = part ? tw : fw;
-                const uint32_t c0 = q[part];
-                for (uint32_t c = 0; c < d; c++) {
-                    const uint64_t *mine = S.sec[SEC_TMP_N] + (uint64_t)(c0 + c) * ldn;
-                    CK(zkgpu_memcpy_d2d(whole + (uint64_t)c * N + r0(), mine, nb * 8));
-                    for (uint32_t p = 0; p < W; p++) {
-                        if (p == R) continue;
-                        op(p, 1, mine, nb * 8);
-                        op(p, 0, whole + (uint64_t)c * N + (uint64_t)p * nb, nb * 8);
-                    }
+            // the rank's f and t rows as one message (2d columns, ld nb) to every peer
+            std::vector<uint32_t> ft;
+            for (uint32_t part = 0; part < 2; part++)
+                for (uint32_t c = 0; c < d; c++) ft.push_back(q[part] + c);
+            std::vector<uint32_t> dst;  // f columns 0..d-1 of fw, t columns of tw (= fw + 3N)
+            for (uint32_t part = 0; part < 2; part++)
+                for (uint32_t c = 0; c < d; c++) dst.push_back(3 * part + c);
+            CK(zkgpu_copy_rows_dev(fw, N, r0(), dst.data(), S.sec[SEC_TMP_N], ldn, 0, 0, ft.data(), 2 * d, nb));
+            if (W > 1) {
+                CK(zkgpu_copy_rows_dev(pack_s, nb, 0, nullptr, S.sec[SEC_TMP_N], ldn, 0, 0, ft.data(), 2 * d, nb));
+                for (uint32_t p = 0; p < W; p++) {
+                    if (p == R) continue;
+                    op(p, 1, pack_s, 2ULL * d * nb * 8);
+                    op(p, 0, pack_r + p * stride_r, 2ULL * d * nb * 8);
                 }
+                if (exchange()) return -1;
+                for (uint32_t p = 0; p < W; p++)
+                    if (p != R)
+                        CK(zkgpu_copy_rows_dev(fw, N, (uint64_t)p * nb, dst.data(), pack_r + p * stride_r, nb, 0, 0,
+                                               nullptr, 2 * d, nb));
             }
-            if (exchange()) return -1;
             uint64_t miss = 0;
             const int rc = zkgpu_h1h2_dev(h1w, N, h2w, N, fw, N, tw, N, N, d, &miss);
             if (rc) {
@@ -765,7 +874,7 @@ public:
         if (run_block(step42ns, ch, evals.data(), 0, nullptr, nullptr)) return -1;
         if (tstop("STARK_STEP_4_CALCULATE_EXPS_2NS")) return -1;
         tstart();
-        if (gather_rows(S.sec[SEC_Q_2NS], gath) || quotient_pieces(gath, cm4)) return -1;
+        if (quotient_sharded()) return -1;
         if (tstop("STARK_STEP_4_CALCULATE_EXPS_2NS_INTT_NTT")) return -1;
         tstart();
         if (merkelize(trees[3], cm4 + (uint64_t)R * B, NE, info.n_cm4, roots[3])) return -1;
@@ -800,7 +909,11 @@ public:
         if (gather_rows(S.sec[SEC_F_2NS], gath)) return -1;
         CK(zkgpu_cols3_to_interleaved_dev(fri_pol[0], gath, NE, NE));
         if (tstop("STARK_STEP_5_CALCULATE_EXPS")) return -1;
-        return fri_and_queries(tr, &roots[0][0], evals, out, tall);
+        const int rc = fri_and_queries(tr, &roots[0][0], evals, out, tall);
+        // a count, not a time: the largest exchange this rank posted (every
+        // exchange is at most one send and one receive per peer, 2 (W - 1))
+        if (W > 1) timers.emplace_back("COUNT_COMM_MAX_OPS", (double)max_ops);
+        return rc;
     }
 
     // each query row is opened by the rank owning it, the records all-gathered

@@ -929,99 +929,10 @@ int zkgpu_comm_rccl_create(zkgpu_comm *comm, const uint8_t id[128], uint32_t wor
 
 int zkgpu_comm_host_create(zkgpu_comm *comm, const char *name, uint32_t world, uint32_t rank, uint64_t capacity)
 {
-    using zkgpu_host::HostCommCtx;
-    using zkgpu_host::HostCommHeader;
-    using zkgpu_host::fail;
-    memset(comm, 0, sizeof *comm);
-    if (!world || rank >= world || !name || name[0] != '/')
-        return fail("zkgpu_comm_host_create: need rank < world and a name starting with '/'");
-    auto *c = new HostCommCtx();
-    c->rank = rank;
-    c->world = world;
-    c->capacity = capacity;
-    c->size = HostCommCtx::header_bytes() + (uint64_t)world * c->box_bytes();
-    const uint64_t run = zkgpu_host::run_tag_hash();
-    void *m = MAP_FAILED;
-    if (rank == 0) {
-        shm_unlink(name);
-        int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
-        if (fd >= 0 && ftruncate(fd, (off_t)c->size)) {
-            close(fd);
-            fd = -1;
-        }
-        if (fd >= 0) {
-            m = mmap(nullptr, c->size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-            close(fd);
-        }
-        if (m == MAP_FAILED) {
-            delete c;
-            return fail("zkgpu_comm_host_create: shared memory %s of %llu bytes not available", name,
-                        (unsigned long long)c->size);
-        }
-        c->base = (uint8_t *)m;
-        HostCommHeader *h = c->hdr();
-        pthread_barrierattr_t a;
-        pthread_barrierattr_init(&a);
-        pthread_barrierattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
-        pthread_barrier_init(&h->barrier, &a, world);
-        pthread_barrierattr_destroy(&a);
-        h->world = world;
-        h->capacity = capacity;
-        h->run = run;
-        for (auto &e : h->error) e.store(0);
-        h->ready.store(1, std::memory_order_release);
-    } else {
-        // wait (up to 60 s) for rank 0's segment of THIS run: a segment left
-        // under the name by an earlier run (other tag, or not yet unlinked by
-        // rank 0) is unmapped and looked up again
-        for (int t = 0; t < 6000 && m == MAP_FAILED; t++) {
-            const int fd = shm_open(name, O_RDWR, 0600);
-            struct stat st;
-            if (fd >= 0 && !fstat(fd, &st) && (uint64_t)st.st_size >= c->size)
-                m = mmap(nullptr, c->size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-            if (fd >= 0) close(fd);
-            if (m != MAP_FAILED) {
-                const HostCommHeader *h = (const HostCommHeader *)m;
-                if (h->ready.load(std::memory_order_acquire) != 1 || h->run != run) {
-                    munmap(m, c->size);
-                    m = MAP_FAILED;
-                } else if (h->world != world || h->capacity != capacity) {
-                    munmap(m, c->size);
-                    delete c;
-                    return fail("zkgpu_comm_host_create: segment %s belongs to another world", name);
-                }
-            }
-            if (m == MAP_FAILED) std::this_thread::sleep_for(std::chrono::milliseconds(10));
-        }
-        if (m == MAP_FAILED) {
-            delete c;
-            return fail("zkgpu_comm_host_create: shared memory %s of this run not available", name);
-        }
-        c->base = (uint8_t *)m;
-    }
-    // every rank has mapped the segment: its name is no longer needed
-    if (c->wait()) {
-        munmap(m, c->size);
-        delete c;
-        return -1;
-    }
-    if (rank == 0) shm_unlink(name);
-    comm->rank = rank;
-    comm->world = world;
-    comm->ctx = c;
-    comm->exchange = zkgpu_host::host_exchange;
-    return 0;
+    return zkgpu_host::host_comm_create(comm, name, world, rank, capacity);
 }
 
-void zkgpu_comm_host_destroy(zkgpu_comm *comm)
-{
-    if (!comm || !comm->ctx) return;
-    auto *c = (zkgpu_host::HostCommCtx *)comm->ctx;
-    munmap(c->base, c->size);
-    delete c;
-    comm->ctx = nullptr;
-    comm->exchange = nullptr;
-}
+void zkgpu_comm_host_destroy(zkgpu_comm *comm) { zkgpu_host::host_comm_destroy(comm); }
 
 void zkgpu_comm_rccl_destroy(zkgpu_comm *comm)
 {

@@ -92,6 +92,7 @@ _SIGS = {
     "zkgpu_lagrange_xi_rows_dev": (ctypes.c_int, [vp, vp, u64, vp, u32, u64, u64]),
     "zkgpu_ext_powers_dev": (ctypes.c_int, [vp, u64, vp, u64]),
     "zkgpu_qsplit_dev": (ctypes.c_int, [vp, u64, vp, u64, u64, u32, u64]),
+    "zkgpu_qsplit_cols_dev": (ctypes.c_int, [vp, u64, vp, u64, u64, u32, u64, u32, u32]),
     "zkgpu_scale_by_powers_dev": (ctypes.c_int, [vp, u64, u32, u64, u64]),
     "zkgpu_cols3_to_interleaved_dev": (ctypes.c_int, [vp, vp, u64, u64]),
     "zkgpu_h1h2_dev": (ctypes.c_int, [vp, u64, vp, u64, vp, u64, vp, u64, u64, u32, pu64]),
@@ -545,6 +546,11 @@ def h1h2_dev(h1, h1_ld, h2, h2_ld, f, f_ld, t, t_ld, n, dim):
 
 def qsplit_dev(qq2, ld2, qq1, ld1, n, q_deg, shift_in):
     _check(lib().zkgpu_qsplit_dev(_addr(qq2), ld2, _addr(qq1), ld1, n, q_deg, shift_in), "zkgpu_qsplit_dev")
+
+
+def qsplit_cols_dev(qq2, ld2, qq1, ld1, n, q_deg, shift_in, dim, stride):
+    _check(lib().zkgpu_qsplit_cols_dev(_addr(qq2), ld2, _addr(qq1), ld1, n, q_deg, shift_in, dim, stride),
+           "zkgpu_qsplit_cols_dev")
 
 
 def evmap_dev(cols, lds, dims, primes, lev, lpev, l_ld, n, extend_bits):
