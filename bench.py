@@ -233,14 +233,27 @@ def _newest(pattern, load=True):
     return None, None
 
 
-def valu_peak(kernel):
+def _stamped(pattern, family):
+    """(path, doc, note) of the newest profile matching pattern whose source
+    stamp (zkgpu/stamp.py) matches the current sources of `family`; when the
+    newest one is stale or unstamped: (path, None, why) -- its counters describe
+    other kernels and are not used."""
+    from zkgpu.stamp import check
+    f, d = _newest(pattern)
+    if not d:
+        return None, None, "no committed %s profile" % pattern
+    ok, why = check(d, family)
+    return (f, d, why) if ok else (f, None, "stale: %s (%s)" % (why, os.path.basename(f)))
+
+
+def valu_peak(kernel, family):
     """Issue peak of `kernel` in wave64 VALU instructions / s: the measured
-    per-instruction issue cost at >= 2 waves per SIMD (profiles/*_instbench.json,
-    tools/instbench.hip) weighted by the kernel's VALU instruction mix
-    (profiles/*_valu_mix.json, tools/valu_mix.py over the shipped code object).
-    Returns (peak, note) or (None, reason)."""
+    per-instruction issue cost at 8 waves per SIMD (profiles/*_instbench.json,
+    tools/instbench.hip) weighted by the kernel's static VALU instruction mix
+    (profiles/*_valu_mix.json, tools/valu_mix.py over the shipped code object,
+    stamped).  Returns (peak, note) or (None, reason)."""
     fi, ib = _newest("*_instbench.json")
-    fm, mix = _newest("*_valu_mix.json")
+    fm, mix, why = _stamped("*_valu_mix.json", family)
     if not ib:
         return None, "no committed instbench profile"
     cost = {}
@@ -250,7 +263,8 @@ def valu_peak(kernel):
     base = cost.get("v_add_u32")
     km = (mix or {}).get("kernels", {}).get(kernel)
     if not km:
-        return N_SIMDS * CLOCK_HZ / base, "v_add_u32 issue cost %.2f clk (8 waves/SIMD); no mix for %s" % (base, kernel)
+        return N_SIMDS * CLOCK_HZ / base, "v_add_u32 issue cost %.2f clk (8 waves/SIMD); no current mix for %s (%s)" % (
+            base, kernel, why)
     tot, cyc = 0, 0.0
     for ins, n in km["histogram"].items():
         c = cost.get(ins, base)  # instructions not measured separately: the v_add_u32 rate
@@ -264,48 +278,64 @@ def valu_peak(kernel):
 def lde_traffic_per_lde(labels_launches):
     """PMC HBM bytes of one LDE: sum over its pass kernels of the per-launch
     traffic in the newest profiles/*_lde_pmc.json (separate FETCH_SIZE /
-    WRITE_SIZE passes of `bench.py --workload lde`, gfx950 corrections)."""
-    f, d = _newest("*_lde_pmc.json")
+    WRITE_SIZE passes of `bench.py --workload lde`, gfx950 corrections) --
+    only when its stamp matches the current NTT sources.  Returns (bytes,
+    source, note)."""
+    f, d, why = _stamped("*_lde_pmc.json", "lde")
     if not d:
-        return None, None
+        return None, None, why
     labs = d.get("bench_labels", {})
     tot = 0.0
     for lab, n in labels_launches.items():
         if lab not in labs or "hbm_bytes_per_launch" not in labs[lab]:
-            return None, None
+            return None, None, "the profile has no %s" % lab
         tot += labs[lab]["hbm_bytes_per_launch"] * n
-    return tot, os.path.basename(f)
+    return tot, os.path.basename(f), why
 
 
-def stark_valu(kernel, avg_ms):
-    """VALU wave-instructions per launch of `kernel` in a 2^23 proof from the
-    newest profiles/*_stark_pmc.json; returns the valu dict or None."""
-    f, d = _newest("*_stark_pmc.json")
+def kernel_counters(kernel, family, launches_per_proof):
+    """VALU wave-instructions and HBM bytes of one proof's launches of
+    `kernel` in the newest stamped profiles/*_stark_pmc.json (the last
+    launches_per_proof launches of its one-proof run: the earlier ones are
+    setup) and the kernel's clock there.  Returns (dict, note) or (None, why)."""
+    f, d, why = _stamped("*_stark_pmc.json", family)
     if not d:
-        return None
+        return None, why
     k = d.get("kernels", {}).get(kernel)
-    if not k or not k.get("valu_wave_instr_per_launch"):
-        return None
-    peak, note = valu_peak(kernel)
+    if not k or "launch_valu" not in k:
+        return None, "the profile has no per-launch record of %s" % kernel
+    lv, lm = k["launch_valu"][-launches_per_proof:], k["launch_ms"][-launches_per_proof:]
+    return {"valu_per_proof": sum(lv), "pmc_ms_per_proof": sum(lm), "launches": len(lv),
+            "hbm_bytes_per_launch": k.get("hbm_bytes_per_launch"),
+            "clock_GHz": k.get("clock_GHz") if k.get("clock_valid") else None,
+            "source": os.path.basename(f)}, why
+
+
+def stark_valu(kernel, ms_per_proof, launches_per_proof, family="poseidon"):
+    """VALU issue rate of `kernel` in this run: its stamped per-proof
+    SQ_INSTS_VALU over its device time per proof here, against the
+    mix-weighted issue peak; the clock the kernel runs at (GRBM busy cycles /
+    kernel time, kept only when <= the 2.4 GHz maximum)."""
+    kc, why = kernel_counters(kernel, family, launches_per_proof)
+    if kc is None:
+        return {"kernel": kernel, "stale": True, "note": why}
+    peak, note = valu_peak(kernel, family)
     if peak is None:
         return None
-    rate = k["valu_wave_instr_per_launch"] / (avg_ms * 1e-3)
+    rate = kc["valu_per_proof"] / (ms_per_proof * 1e-3)
     frac = rate / peak
     if frac > 1.0:
         raise SystemExit("valu.frac %.3f > 1 for %s: the peak model (%s) is wrong" % (frac, kernel, note))
-    res = {"kernel": kernel, "wave_instr_per_launch": k["valu_wave_instr_per_launch"], "avg_launch_ms": round(avg_ms, 4),
-           "achieved": round(rate / 1e9, 1), "peak": round(peak / 1e9, 1), "unit": "G wave-instr/s",
-           "frac": round(frac, 4), "peak_model": note + " at the nominal %.1f GHz" % (CLOCK_HZ / 1e9),
-           "source": os.path.basename(f)}
-    # the clock the kernel actually runs at (power-limited below the nominal
-    # 2.4 GHz; GRBM busy cycles / duration, tools/pmc_clock.sh)
-    fc, clk = _newest("*_clock.json")
-    ghz = (clk or {}).get("labels", {}).get(kernel)
-    if ghz:
+    res = {"kernel": kernel, "wave_instr_per_proof": kc["valu_per_proof"], "launches_per_proof": launches_per_proof,
+           "ms_per_proof": round(ms_per_proof, 3), "achieved": round(rate / 1e9, 1), "peak": round(peak / 1e9, 1),
+           "unit": "G wave-instr/s", "frac": round(frac, 4),
+           "peak_model": note + " at the nominal %.1f GHz" % (CLOCK_HZ / 1e9), "source": kc["source"],
+           "stamp": why}
+    ghz = kc["clock_GHz"]
+    if ghz and ghz <= CLOCK_HZ / 1e9:
         res["clock_GHz"] = ghz
         res["peak_at_clock"] = round(peak * ghz * 1e9 / CLOCK_HZ / 1e9, 1)
         res["frac_at_clock"] = round(frac * CLOCK_HZ / (ghz * 1e9), 4)
-        res["clock_source"] = os.path.basename(fc)
     return res
 
 
@@ -369,15 +399,15 @@ def lde_measure(args, dev, torch, world, dist):
     alg = 24.0 * n * C if args.blowup_bits == 1 else 8.0 * (n + ne) * C
     achieved = alg / (dev_ms * 1e-3) / 1e9
     launches = {k: v[0] / steps for k, v in passes.items()}
-    traffic, src = (None, None)
+    traffic, src, tnote = None, None, "counters exist for configs[1] only (2^23 -> 2^24 x 100)"
     if args.log_n == 23 and C == 100 and args.blowup_bits == 1:
-        traffic, src = lde_traffic_per_lde(launches)
+        traffic, src, tnote = lde_traffic_per_lde(launches)
     roof = {"kernel": "extendPol = NTT pass chain (%s per LDE)"
                       % ", ".join("%g x %s" % (launches[k], k) for k in sorted(launches)),
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic, "traffic_ratio": round(traffic / alg, 2) if traffic else None,
-            "traffic_source": src, "alg_bytes_per_launch": alg,
+            "traffic_source": src, "traffic_stamp": tnote, "alg_bytes_per_launch": alg,
             "alg_bytes_note": "SURVEY.md 8(d): LDE N -> 2N x C reads 8NC, writes 16NC = 24NC bytes; 'launch' = "
                               "one LDE (its NTT pass kernels), device time from HIP events on the launch stream",
             "avg_launch_ms": round(dev_ms, 4)}
@@ -475,16 +505,35 @@ def leaves_line(inst, args, v):
            "hbm_frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "perms_per_proof": perms, "Gperm_s": round(perms / (ms * 1e-3) / 1e9, 3),
            "bound": "VALU (~20 K VALU per 64 B absorbed; the valu block prices it against the issue peak)"}
-    f, _ = _newest("*_poseidon_bench.txt", load=False)
-    if f:
-        import re
-        m = re.search(r"^fast \(FFT MDS \+ block dots\)\s+[\d.]+ ms\s+([\d.]+) Gperm/s", open(f).read(), re.M)
-        if m:
-            iso = float(m.group(1))
-            res["isolated_Gperm_s"] = iso
-            res["ratio_to_isolated"] = round(res["Gperm_s"] / iso, 3)
-            res["isolated_source"] = os.path.basename(f) + " (the shipped permutation, 8 waves/SIMD at 2.02 GHz; " \
-                "the leaf kernel runs at 2.33 GHz, profiles/r02_clock.json)"
+    f, d, why = _stamped("*_poseidon_bench.json", "poseidon")
+    if d and d.get("fast_Gperm_s"):
+        res["isolated_Gperm_s"] = d["fast_Gperm_s"]
+        res["ratio_to_isolated"] = round(res["Gperm_s"] / d["fast_Gperm_s"], 3)
+        res["isolated_source"] = "%s (the shipped permutation, one state per thread, %s GHz under load; %s)" % (
+            os.path.basename(f), d.get("clock_GHz"), why)
+    else:
+        res["isolated_note"] = why
+    return res
+
+
+def dominant_roofline(inst, args, v, valu):
+    """k_leaves_cols, the proof's dominant kernel, on both of its bounds from
+    this run's timing: HBM (SURVEY.md 8(d) leaves bytes: 8 B x rows x cols +
+    32 B digest per row, per proof) and VALU issue (the stamped per-proof
+    SQ_INSTS_VALU of the same build, the valu block)."""
+    ne = 1 << (args.log_n + args.blowup_bits)
+    widths = [inst.n_cm1, inst.n_cm2, inst.n_cm3, inst.n_cm4]
+    ms = v[1] / args.steps
+    alg = sum(8.0 * ne * w + 32.0 * ne for w in widths)
+    hbm = alg / (ms * 1e-3) / 1e9
+    res = {"kernel": "k_leaves_cols", "ms_per_proof": round(ms, 3), "bound": "valu",
+           "hbm": {"achieved": round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(hbm / HBM_PEAK_GBS, 4),
+                   "alg_bytes_per_proof": alg}}
+    if valu and not valu.get("stale"):
+        res["valu"] = {k: valu[k] for k in ("achieved", "peak", "unit", "frac", "frac_at_clock", "clock_GHz", "source")
+                       if k in valu}
+    else:
+        res["valu"] = {"stale": True, "note": (valu or {}).get("note")}
     return res
 
 
@@ -513,7 +562,9 @@ def quotient_measure(args, dev, torch, world, dist):
                    "opcode histogram / temporaries / fork-9 map, tests/golden/zkevm_bytecode_shape.json) -> product "
                    "converter -> ZXP compile -> segment kernels; 2^24-row extended domain, sections resident in HBM; "
                    "parity: tests/test_gpu_parser.py (full size, 2^16 rows, vs the oracle parser)"}
-    f, d = _newest("*_s42_pmc.json")
+    f, d, why = _stamped("*_s42_pmc.json", "zxp")
+    if roof is not None:
+        roof["traffic_stamp"] = why
     if roof is not None and d and d.get("hbm_bytes_per_step"):
         roof["traffic"] = d["hbm_bytes_per_step"]
         roof["traffic_ratio"] = round(d["hbm_bytes_per_step"] / roof["alg_bytes_per_launch"], 2)
@@ -530,7 +581,7 @@ def quotient_measure(args, dev, torch, world, dist):
             res["valu"] = {"wave_instr_per_pass": valu, "achieved": round(rate / 1e9, 1), "peak": 978.0,
                            "unit": "G wave-instr/s", "frac": round(rate / 978e9, 4),
                            "peak_model": "mix-weighted issue peak of the field-arithmetic kernels (DESIGN.md 3)",
-                           "source": os.path.basename(f)}
+                           "source": os.path.basename(f), "stamp": why}
     res["roofline"] = roof
     for t in s42["tensors"].values():
         del t
@@ -842,8 +893,9 @@ def main():
                     kernels[dom][1] / sum(v[1] for v in kernels.values()), 3)}
                 if "k_leaves_cols" in kernels:
                     v = kernels["k_leaves_cols"]
-                    res["valu"] = stark_valu("k_leaves_cols", v[1] / v[0])
+                    res["valu"] = stark_valu("k_leaves_cols", v[1] / args.steps, int(round(v[0] / args.steps)))
                     res["leaves"] = leaves_line(inst, args, v)
+                    res["roofline_dominant"] = dominant_roofline(inst, args, v, res["valu"])
             if args.workload in ("stark", "stark-sharded") and stages:
                 res["stages_ms"] = {k: round(v, 3) for k, v in stages.items()}
         res["cpu_baseline"] = cpu

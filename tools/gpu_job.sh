@@ -3,7 +3,7 @@
 # stops at the first fault / abort / segfault / timeout (exit >= 124 or
 # signal), but continues past an ordinary test failure (exit 1).
 # Usage: tools/gpu_job.sh <step>...
-#   steps: tests large smoke bench instbench bwbench parser step42ns prof pmc starkpmc cpufull merkle zkevm sharded
+#   steps: tests large smoke bench instbench bwbench parser step42ns prof pmc cpufull merkle zkevm sharded
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOTDIR=$(pwd)
@@ -85,33 +85,10 @@ for step in "$@"; do
         ok_or_stop $rc "rocprofv3 kernel-trace (one proof)"
         ;;
     pmc)
-        # LDE (configs[1]): HBM traffic per pass kernel, separate FETCH / WRITE / SQ passes
-        for pass in "FETCH_SIZE:pmc_fetch" "WRITE_SIZE:pmc_write" "SQ_INSTS_VALU SQ_WAVES:pmc_sqb"; do
-            ctr=${pass%%:*}
-            out=${pass##*:}
-            cd /tmp
-            timeout -s KILL 300 rocprofv3 --pmc $ctr --kernel-trace -d "$ROOTDIR/gpurun_out/$out" -o run \
-                --output-format csv -- python3 "$ROOTDIR/bench.py" --workload lde --no-cpu --steps 2 --warmup 1 \
-                > /dev/null 2> "$ROOTDIR/gpurun_out/$out.err"
-            rc=$?
-            cd "$ROOTDIR"
-            ok_or_stop $rc "rocprofv3 lde pmc $out"
-        done
-        ;;
-    starkpmc)
-        # 2^23 STARK proof: HBM traffic (separate FETCH / WRITE passes) and VALU issue per kernel
-        for pass in "FETCH_SIZE:pmc_sfetch" "WRITE_SIZE:pmc_swrite" \
-                    "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE:pmc_ssq"; do
-            ctr=${pass%%:*}
-            out=${pass##*:}
-            cd /tmp
-            timeout -s KILL 400 rocprofv3 --pmc $ctr --kernel-trace -d "$ROOTDIR/gpurun_out/$out" -o run \
-                --output-format csv -- python3 "$ROOTDIR/bench.py" --workload stark --no-cpu --no-lde --no-sharded --no-handoff --no-s42 --steps 1 --warmup 0 \
-                > /dev/null 2> "$ROOTDIR/gpurun_out/$out.err"
-            rc=$?
-            cd "$ROOTDIR"
-            ok_or_stop $rc "rocprofv3 stark pmc $out"
-        done
+        # every counter bench.py's ratios read, stamped (tools/pmc_round.sh -> profiles/${PMC_TAG}_*)
+        bash tools/pmc_round.sh ${PMC_TAG:-r04} > gpurun_out/pmc_round.log 2>&1
+        ok_or_stop $? "pmc round"
+        tail -3 gpurun_out/pmc_round.log
         ;;
     step42ns)
         timeout -k 10 600 python bench.py --workload step42ns --no-cpu --steps 3 --warmup 1 \

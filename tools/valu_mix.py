@@ -80,9 +80,11 @@ def main():
     for r in res.values():
         r["histogram"] = dict(r["histogram"].most_common())
         r["valu_total"] = sum(r["histogram"].values())
+    sys.path.insert(0, os.path.join(ROOT, "zkevm-prover_amd"))
+    from zkgpu.stamp import all_stamps
     doc = {"_doc": "static VALU instruction histogram per kernel label of lib/libzkgpu.so (tools/valu_mix.py); "
                    "bench.py weights the measured issue costs (profiles/*_instbench.json) with it",
-           "kernels": res}
+           "kernels": res, "stamps": all_stamps()}
     path = os.path.join(ROOT, "profiles", "%s_valu_mix.json" % tag)
     json.dump(doc, open(path, "w"), indent=1)
     for lab, r in res.items():
