@@ -59,7 +59,9 @@ def taken_dotfin(a0, a1, a2):
 
 
 def taken_mul2e(e, x):
-    """mul2e_rb<e>'s rare correction (gl_rb.hpp); e = 0, 32 and >= 96 have none."""
+    """mul2e_rb<e>'s rare correction (gl_rb.hpp; e = 0, 32, >= 96 and
+    20 < e < 32 take mul2e's select form instead: the same condition, no
+    branch)."""
     if e == 0 or e == 32 or e >= 96:
         return False
     if e < 32:

@@ -88,3 +88,24 @@ def test_merkle_2p23_x100_openings(oracle, zkgpu):
     assert np.array_equal(vals, zkgpu.from_device(srcT).T)
     for q, i in enumerate(idx):
         assert np.array_equal(oracle.merkle_root_from_proof(vals[q], sibs[q], int(i)), root)
+
+
+def test_merkle_2p23_x100_tree_bit_exact(oracle, zkgpu):
+    """BASELINE.md config 3 as written: the whole Poseidon Merkle tree over
+    2^23 rows x 100 columns (leaves, every node level, root) equals the
+    oracle's merkletree (oracle/merkle.c, OpenMP) bit for bit."""
+    import os
+    import torch
+    nrows, C = 1 << 23, 100
+    src = rand_cols(torch, C, nrows, 6)
+    nodes = torch.empty(zkgpu.merkle_num_elements(nrows), dtype=torch.int64, device="cuda:0")
+    zkgpu.merkletree_dev(nodes, src, nrows, C, nrows)
+    torch.cuda.synchronize()
+    got = zkgpu.from_device(nodes)
+    rows = np.ascontiguousarray(zkgpu.from_device(src).T)  # the reference's row-major source
+    del src
+    oracle.lib().oc_set_num_threads(min(16, os.cpu_count() or 1))
+    ref = oracle.merkletree(rows)
+    assert got.shape == ref.shape
+    assert np.array_equal(got[-4:], ref[-4:]), "root"
+    assert np.array_equal(got, ref)

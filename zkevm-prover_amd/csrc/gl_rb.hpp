@@ -60,13 +60,18 @@ __device__ __forceinline__ uint64_t gl_mul_rb(uint64_t a, uint64_t b)
 // mul2e with its final correction behind a wave-uniform branch where that
 // correction is rare (the radix-256 NTT pass; same values as mul2e): for
 // 0 < E < 32 the carry of lo + hl EPS needs lo >= 2^64 - 2^(E+32) (about
-// 2^(E-32)), for 32 < E < 96 the borrow needs the shifted high word below
-// 2^2 (about 2^-30).  E = 32 and E >= 96 keep mul2e.
+// 2^(E-32) per lane, so a 64-lane wave takes it with probability ~2^(E-26):
+// the branch pays only for E <= ZK_RB_SHIFT_MAX_E), for 32 < E < 96 the
+// borrow needs the shifted high word below 2^2 (about 2^-30).  E = 32,
+// E >= 96 and the larger E < 32 keep mul2e.
+#ifndef ZK_RB_SHIFT_MAX_E
+#define ZK_RB_SHIFT_MAX_E 20
+#endif
 template <int E>
 __device__ __forceinline__ uint64_t mul2e_rb(uint64_t x)
 {
     static_assert(E >= 0 && E < 192, "exponent range");
-    if constexpr (E == 0 || E == 32 || E >= 96) {
+    if constexpr (E == 0 || E == 32 || E >= 96 || (E < 32 && E > ZK_RB_SHIFT_MAX_E)) {
         return mul2e<E>(x);
     } else if constexpr (E < 32) {
         const uint32_t hl = (uint32_t)(x >> (64 - E));
