@@ -802,19 +802,33 @@ constexpr int MID_LDS = 16 * 272;  // u64 per block
 // (pads 272 / 257: conflict-free ds_write_b64 16-lane and ds_read_b64 32-lane groups)
 // TA: tw16 is a per-element stage-A table [k2 * 256 + t] (the LDE's
 // F_p^(RA t) coset factor folded into omega_4096^(t k2)), else omega_4096^e.
+// ZKGPU_LDE_MID_RB=1: P2's butterflies, shift-multiplies and twiddle
+// products with the rare corrections behind wave-uniform branches
+// (gl_rb.hpp), as the radix-256 pass.  Measured (round 4, A/B twice on one
+// box, 3-pass LDE 2^23 -> 2^24 x 100): 42.3 against 49.8 Gelem/s with the
+// select form -- the branches split the 200-VGPR kernel's blocks.  Off.
+#ifndef ZKGPU_LDE_MID_RB
+#define ZKGPU_LDE_MID_RB 0
+#endif
+__device__ __forceinline__ uint64_t mid_mul(uint64_t a, uint64_t b)
+{
+    if constexpr (ZKGPU_LDE_MID_RB) return gl_mul_rb(a, b);
+    else return gl_mul(a, b);
+}
+
 template <bool INV, bool TA>
 __device__ __forceinline__ void dft4096_block(uint64_t *v, uint64_t *L, int t, const uint64_t *tw16,
                                               const uint64_t *tw256)
 {
     // sched_barrier: keeps the compiler from hoisting the next stage's
     // twiddle loads over the current stage (register pressure)
-    dft_regs<4, INV>(v);
+    dft_regs<4, INV, ZKGPU_LDE_MID_RB>(v);
     if constexpr (TA) {
 #pragma unroll
-        for (int r = 0; r < 16; r++) v[r] = gl_mul(v[r], tw16[(brev_c(r, 4) << 8) + t]);
+        for (int r = 0; r < 16; r++) v[r] = mid_mul(v[r], tw16[(brev_c(r, 4) << 8) + t]);
     } else {
 #pragma unroll
-        for (int r = 1; r < 16; r++) v[r] = gl_mul(v[r], tw16[t * brev_c(r, 4)]);
+        for (int r = 1; r < 16; r++) v[r] = mid_mul(v[r], tw16[t * brev_c(r, 4)]);
     }
 #pragma unroll
     for (int r = 0; r < 16; r++) L[brev_c(r, 4) * 272 + t] = v[r];
@@ -825,9 +839,9 @@ __device__ __forceinline__ void dft4096_block(uint64_t *v, uint64_t *L, int t, c
     for (int j1 = 0; j1 < 16; j1++) v[j1] = L[hi * 272 + lo + 16 * j1];
     __syncthreads();
     __builtin_amdgcn_sched_barrier(0);
-    dft_regs<4, INV>(v);
+    dft_regs<4, INV, ZKGPU_LDE_MID_RB>(v);
 #pragma unroll
-    for (int r = 1; r < 16; r++) v[r] = gl_mul(v[r], tw256[lo * brev_c(r, 4)]);
+    for (int r = 1; r < 16; r++) v[r] = mid_mul(v[r], tw256[lo * brev_c(r, 4)]);
 #pragma unroll
     for (int r = 0; r < 16; r++) L[lo * 257 + brev_c(r, 4) * 16 + hi] = v[r];
     __syncthreads();
@@ -836,7 +850,7 @@ __device__ __forceinline__ void dft4096_block(uint64_t *v, uint64_t *L, int t, c
     for (int j0 = 0; j0 < 16; j0++) v[j0] = L[j0 * 257 + hi * 16 + lo];
     __syncthreads();
     __builtin_amdgcn_sched_barrier(0);
-    dft_regs<4, INV>(v);
+    dft_regs<4, INV, ZKGPU_LDE_MID_RB>(v);
 }
 
 // P2: one block (kA, column) per workgroup, columns fastest (VGPRs: 16
@@ -867,7 +881,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         // scalar loads) * F_p^(RA t) (folded into the stage-A table)
         const uint64_t *S = a.fs + ((uint64_t)p * RA + kA) * 16;
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = gl_mul(c[k], S[k]);
+        for (int k = 0; k < 16; k++) v[k] = mid_mul(c[k], S[k]);
         dft4096_block<false, true>(v, L, t, a.twa[p], a.tw256[0]);
         __builtin_amdgcn_sched_barrier(0);
         if (p == 0) {
@@ -881,8 +895,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     for (int k = 0; k < 16; k++) {
         const uint64_t w = otw[256 * k];
         HIP_vector_type<unsigned long long, 2> pr;
-        pr.x = gl_mul(z0[brev_c(k, 4)], w);
-        pr.y = gl_mul(v[brev_c(k, 4)], w);
+        pr.x = mid_mul(z0[brev_c(k, 4)], w);
+        pr.y = mid_mul(v[brev_c(k, 4)], w);
         *reinterpret_cast<HIP_vector_type<unsigned long long, 2> *>(dst + 512 * k) = pr;
     }
 }
