@@ -90,6 +90,8 @@ def parse():
     ap.add_argument("--no-s42", action="store_true",
                     help="stark workload: skip the zkEVM-shaped quotient block (quotient_zkevm_shaped)")
     ap.add_argument("--s42-steps", type=int, default=3)
+    ap.add_argument("--no-cpu-zkevm", action="store_true",
+                    help="stark workload: skip the oracle's zkEVM-shaped sample (cpu_baseline.zkevm_shaped, ~20 s)")
     ap.add_argument("--cpu-sample-bits", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_BITS", "18")))
     ap.add_argument("--cpu-sample-cols", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_COLS", "4")))
     ap.add_argument("--cpu-full", action="store_true",
@@ -163,6 +165,28 @@ def cpu_baseline_stark(sample_bits, blow, ncols, n_queries):
             "sample": "oracle genProof (oracle/stark_prover.py over oracle/*.c) of the config-4 instance shape at "
                       "2^%d rows (%d cm1 cols, %d queries), %.1f s, %d threads (%s)"
                       % (sample_bits, ncols, n_queries, dt, threads, _cpu_model())}
+
+
+def cpu_baseline_zkevm(sample_bits, n_queries):
+    """The oracle prover on the zkEVM-shaped instance (fork-9 widths + the
+    five zkEVM-shaped programs, zkgpu/zkevm_shaped.py) at 2^sample_bits rows:
+    the CPU path of the same proof the GPU's sharded_one_proof.fork9_zkevm_shaped
+    line times at 2^22-2^23."""
+    from oracle import oracle as oc
+    from oracle.stark_prover import OracleStark
+    oc.lib()
+    threads = _threads()
+    oc.lib().oc_set_num_threads(threads)
+    inst = stark_instance(sample_bits, 1, 100, n_queries, "zkevm")
+    o = OracleStark(inst)
+    o.witness()
+    t0 = time.perf_counter()
+    o.prove()
+    dt = time.perf_counter() - t0
+    return {"value": round(dt, 3), "unit": "s/proof", "cores": threads, "kind": "port", "rows": 1 << sample_bits,
+            "sample": "oracle genProof of the zkEVM-shaped instance (751/168/408/6 committed, 234 constants, the five "
+                      "zkEVM-shaped programs, 1,973 evaluations) at 2^%d rows, %d queries, %.1f s, %d threads (%s)"
+                      % (sample_bits, n_queries, dt, threads, _cpu_model())}
 
 
 def cpu_full_size_record():
@@ -815,6 +839,19 @@ def main():
                 if full and full.get("value"):
                     cpu["full_size"] = full
                     cpu["full_size_vs_gpu"] = round(full["value"] / value, 1)
+                if not args.no_cpu_zkevm:
+                    z = cpu_baseline_zkevm(14, args.queries)
+                    g = ((sharded or {}).get("fork9_zkevm_shaped") or {})
+                    if g.get("value"):
+                        rows = 1 << (args.log_n - 1 if args.log_n > 22 else args.log_n)
+                        z["gpu_same_instance"] = {"s_per_proof": g["value"], "rows": rows,
+                                                  "source": "sharded_one_proof.fork9_zkevm_shaped (1 GPU)"}
+                        z["per_row_ratio"] = round((z["value"] / z["rows"]) / (g["value"] / rows), 1)
+                        z["per_row_ratio_note"] = ("CPU seconds per trace row at 2^14 / GPU seconds per row at 2^%d: a "
+                                                   "throughput ratio of the same proof, not an extrapolated full-size "
+                                                   "time (the CPU's per-row cost still falls with size: FRI and queries "
+                                                   "are a fixed cost)" % (args.log_n - 1 if args.log_n > 22 else args.log_n))
+                    cpu["zkevm_shaped"] = z
             elif args.workload == "lde":
                 cpu = cpu_baseline_lde(args.log_n, args.blowup_bits, args.cpu_sample_cols)
             elif args.workload == "merkle":
