@@ -91,7 +91,7 @@ def parse():
                     help="stark workload: skip the zkEVM-shaped quotient block (quotient_zkevm_shaped)")
     ap.add_argument("--s42-steps", type=int, default=3)
     ap.add_argument("--no-cpu-zkevm", action="store_true",
-                    help="stark workload: skip the oracle's zkEVM-shaped sample (cpu_baseline.zkevm_shaped, ~20 s)")
+                    help="stark workload: skip the oracle's zkEVM-shaped sample (cpu_baseline.zkevm_shaped, 2^16 rows, ~20 s)")
     ap.add_argument("--cpu-sample-bits", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_BITS", "18")))
     ap.add_argument("--cpu-sample-cols", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_COLS", "4")))
     ap.add_argument("--cpu-full", action="store_true",
@@ -840,14 +840,14 @@ def main():
                     cpu["full_size"] = full
                     cpu["full_size_vs_gpu"] = round(full["value"] / value, 1)
                 if not args.no_cpu_zkevm:
-                    z = cpu_baseline_zkevm(14, args.queries)
+                    z = cpu_baseline_zkevm(16, args.queries)
                     g = ((sharded or {}).get("fork9_zkevm_shaped") or {})
                     if g.get("value"):
                         rows = 1 << (args.log_n - 1 if args.log_n > 22 else args.log_n)
                         z["gpu_same_instance"] = {"s_per_proof": g["value"], "rows": rows,
                                                   "source": "sharded_one_proof.fork9_zkevm_shaped (1 GPU)"}
                         z["per_row_ratio"] = round((z["value"] / z["rows"]) / (g["value"] / rows), 1)
-                        z["per_row_ratio_note"] = ("CPU seconds per trace row at 2^14 / GPU seconds per row at 2^%d: a "
+                        z["per_row_ratio_note"] = ("CPU seconds per trace row at 2^16 / GPU seconds per row at 2^%d: a "
                                                    "throughput ratio of the same proof, not an extrapolated full-size "
                                                    "time (the CPU's per-row cost still falls with size: FRI and queries "
                                                    "are a fixed cost)" % (args.log_n - 1 if args.log_n > 22 else args.log_n))

@@ -28,7 +28,9 @@ FAMILIES = {
 ENV = {
     "lde": ["ZKGPU_LDE3", "ZKGPU_NTT_RB"],
     "poseidon": [],
-    "zxp": ["ZKGPU_ZXP_JIT", "ZKGPU_ZXP_JIT_LCACHE", "ZKGPU_ZXP_JIT_LCACHE_GAP", "ZKGPU_ZXP_JIT_KCHUNK",
+    # (ZKGPU_ZXP_JIT, interpreter vs compiled, is not one: the profiled
+    # workloads pick the compiled kernels themselves, bench.py --s42-jit)
+    "zxp": ["ZKGPU_ZXP_JIT_LCACHE", "ZKGPU_ZXP_JIT_LCACHE_GAP", "ZKGPU_ZXP_JIT_KCHUNK",
             "ZKGPU_ZXP_JIT_KLDS", "ZKGPU_ZXP_JIT_ROWS", "ZKGPU_ZXP_JIT_RB", "ZKGPU_ZXP_JIT_UNROLL"],
 }
 
