@@ -305,8 +305,17 @@ struct Dot3 {
         const LimbQ q{qv.x, qv.y, qv.z, qv.w};
         const LimbP r{rv.x, rv.y};
 #else
-        const LimbQ q = *(const LimbQ *)c;
-        const LimbP r = *(const LimbP *)(c + 4);
+        // explicit vector types: a struct copy is split into dword loads at
+        // -O1, which the LDS chunks of the split programs then read as
+        // ds_read2_b32 pairs, each behind a v_add_u32 of its base (the pair's
+        // 8-bit offsets do not reach across a 4 KB chunk); one 16-byte and one
+        // 8-byte read take the 16-bit offset field instead
+        typedef uint32_t u32x4_ __attribute__((ext_vector_type(4)));
+        typedef uint32_t u32x2_ __attribute__((ext_vector_type(2)));
+        const u32x4_ qv = *(const u32x4_ *)c;
+        const u32x2_ rv = *(const u32x2_ *)(c + 4);
+        const LimbQ q{qv.x, qv.y, qv.z, qv.w};
+        const LimbP r{rv.x, rv.y};
 #endif
         const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);
         A0 += (uint64_t)a0 * q.x;
