@@ -171,6 +171,7 @@ extern "C" __global__ void __launch_bounds__(256) ZKJIT_WAVES zxp_jit(const JitP
     const bool live_ = i_ < S_;
     const uint64_t ib_ = live_ ? i_ : 0;
     __shared__ __attribute__((aligned(16))) uint32_t kbuf[2 * ZKJIT_KL_CHUNK];
+    uint4 pf_;  // the next chunk, in flight (zxp_jit_source chunk_head)
     kput(kbuf, kpre(p.kl, 0));
     __syncthreads();
 #else
@@ -1035,21 +1036,33 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         const char *e = getenv("ZKGPU_ZXP_JIT_SYNC");
         return e ? atoi(e) : 0;
     }();
+    // ZKGPU_ZXP_JIT_KSYNC=1: a new limb chunk (and so a workgroup barrier)
+    // at every code block, the round-3 form; default 0: a chunk spans as many
+    // code blocks as its limbs fill (a barrier every ~3-4 blocks instead of
+    // every block)
+    static const int ksync = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_KSYNC");
+        return e ? atoi(e) : 0;
+    }();
     size_t block_start = 0, n_blocks = 0;
-    auto chunk_head = [&] {  // LDS base of this block's chunk; next block's chunk start patched in at the end
-        appendf(body, "const uint32_t *K = kbuf + %d - %zu; const uint4 pf_ = kpre(p.kl, @KLO%zu@);\n",
+    auto chunk_head = [&] {  // LDS base of this chunk; the next chunk's start patched in at the end
+        appendf(body, "const uint32_t *K = kbuf + %d - %zu; pf_ = kpre(p.kl, @KLO%zu@);\n",
                 (int)(blk_no & 1) * JIT_KCHUNK, blk_lo, blk_no + 1);
     };
-    std::vector<size_t> klo_of;  // chunk start of block b
+    std::vector<size_t> klo_of;  // chunk start of chunk b
     auto maybe_split = [&] {
-        if (split && (body.size() - block_start >= block || (kchunk && kl2.size() - blk_lo > JIT_KCHUNK - 512))) {
-            if (kchunk) {
+        const bool full = kchunk && kl2.size() - blk_lo > JIT_KCHUNK - (ksync ? 512 : 256);
+        if (split && (body.size() - block_start >= block || full)) {
+            if (kchunk && (ksync || full)) {
                 appendf(body, "kput(kbuf + %d, pf_);\n}\n__syncthreads();\n", (int)((blk_no + 1) & 1) * JIT_KCHUNK);
                 blk_lo = kl2.size();
                 blk_no++;
                 klo_of.push_back(blk_lo);
                 body += "if (zk_one()) {\n";
                 chunk_head();
+            } else if (kchunk) {  // same chunk, new code block
+                appendf(body, "}\nif (zk_one()) {\nconst uint32_t *K = kbuf + %d - %zu;\n", (int)(blk_no & 1) * JIT_KCHUNK,
+                        blk_lo);
             } else {
                 body += "}\n";
                 if (sync_every > 0 && ++n_blocks % sync_every == 0) body += "__syncthreads();\n";
