@@ -889,7 +889,9 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
     // domains use the interpreter.  ZKGPU_ZXP_JIT=0 never, =2 always.
     const char *env_jit = getenv("ZKGPU_ZXP_JIT");
     const int jit_mode = env_jit ? atoi(env_jit) : 1;
-    const bool use_jit = !force_interp && fuse && (jit_mode == 2 || (jit_mode == 1 && log_dom >= 16));
+    // (the compiled kernels address a column with a 32-bit byte offset:
+    // domains up to 2^28 rows plus their halo)
+    const bool use_jit = !force_interp && fuse && log_dom <= 28 && (jit_mode == 2 || (jit_mode == 1 && log_dom >= 16));
     std::vector<zxp_operand> opv;
     const zxp_instr *pin = in;
     const zxp_term *terms = nullptr;

@@ -137,6 +137,10 @@ __device__ __forceinline__ uint4 kpre(const uint32_t *kl, size_t lo)
     return *(const __attribute__((address_space(1))) uint4 *)(kl + lo + 4 * threadIdx.x);
 }
 __device__ __forceinline__ void kput(uint32_t *dst, uint4 v) { *(uint4 *)(dst + 4 * threadIdx.x) = v; }
+__device__ __forceinline__ uint64_t gload_o(const uint64_t *base, uint32_t byte_off)
+{
+    return *(const gu64_t *)((const char *)base + byte_off);
+}
 __device__ __forceinline__ uint64_t zk_cs(uint64_t *slot, uint64_t v)
 {
     *slot = v;
@@ -184,7 +188,16 @@ extern "C" __global__ void __launch_bounds__(256) ZKJIT_WAVES zxp_jit(const JitP
 #else
 #define CPTR(j) (const_cast<uint64_t *>(p.cp[j]))
 #endif
+// a column read: 32-bit byte offset from the column's (scalar) base, so the
+// load takes the global_load saddr form -- one offset register per row shift
+// shared by every column, no 64-bit address per load (domains <= 2^28 rows,
+// api.hip use_jit)
+#if ZKJIT_SADDR
+const uint32_t m32_ = (uint32_t)m;
+#define C(j, sh, ii) gload_o(CPTR(j), (((uint32_t)(ii) + (uint32_t)(sh)) & m32_) << 3)
+#else
 #define C(j, sh, ii) gload(CPTR(j) + ((ii + (uint64_t)(sh)) & m))
+#endif
 #if ZKJIT_LCACHE
     // compiler-managed column cache (lds_column_cache): slot s of this lane
     // (ZKJIT_ROWS rows per thread: slot s of row r at (s ROWS + r))
@@ -1293,6 +1306,14 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         src += "#define ZKJIT_WAVES\n";
     const uint32_t rows = jit_rows(split);
     appendf(src, "#define ZKJIT_ROWS %u\n", rows);
+    {
+        // ZKGPU_ZXP_JIT_SADDR=0: 64-bit column addresses (the round-3 form)
+        static const int saddr = [] {
+            const char *e = getenv("ZKGPU_ZXP_JIT_SADDR");
+            return e ? atoi(e) : 1;
+        }();
+        appendf(src, "#define ZKJIT_SADDR %d\n", saddr ? 1 : 0);
+    }
     {
         // LDS column cache (lds_column_cache): block-split programs;
         // ZKGPU_ZXP_JIT_LCACHE slots per lane and row (LDS: 2 KB per slot, row
