@@ -259,15 +259,23 @@ def _newest(pattern, load=True):
 
 def _stamped(pattern, family):
     """(path, doc, note) of the newest profile matching pattern whose source
-    stamp (zkgpu/stamp.py) matches the current sources of `family`; when the
-    newest one is stale or unstamped: (path, None, why) -- its counters describe
-    other kernels and are not used."""
+    stamp (zkgpu/stamp.py) matches the current sources of `family`; when none
+    does: (newest path, None, why) -- the counters describe other kernels and
+    are not used."""
     from zkgpu.stamp import check
-    f, d = _newest(pattern)
-    if not d:
-        return None, None, "no committed %s profile" % pattern
-    ok, why = check(d, family)
-    return (f, d, why) if ok else (f, None, "stale: %s (%s)" % (why, os.path.basename(f)))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), key=_profile_order)
+    stale = None
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        ok, why = check(d, family)
+        if ok:
+            return f, d, why
+        if stale is None:
+            stale = (f, None, "stale: %s (%s)" % (why, os.path.basename(f)))
+    return stale or (None, None, "no committed %s profile" % pattern)
 
 
 def valu_peak(kernel, family):
