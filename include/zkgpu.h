@@ -130,6 +130,18 @@ int zkgpu_build_const_tree(uint64_t *tree_out, const uint64_t *const_pols, uint6
  * duration of the call (hipHostRegister). */
 int zkgpu_load_rows_dev(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint64_t nrows, uint64_t ncols,
                         uint64_t block_rows, int register_host);
+/* The same load in the background: a host thread of the library runs the
+ * block loop on streams of its own (stage: caller-owned device buffer of at
+ * least zkgpu_load_rows_stage_bytes bytes), so kernels on the library stream
+ * -- the previous proof -- run while the trace crosses PCIe.  `rows`, `cols`
+ * and `stage` stay untouched by the caller until zkgpu_load_wait(ticket)
+ * returns (the load's status; the ticket is freed).  No reference
+ * counterpart: the reference's batch prover loads each trace before its
+ * genProof (prover.cpp:94-116). */
+uint64_t zkgpu_load_rows_stage_bytes(uint64_t nrows, uint64_t ncols, uint64_t block_rows);
+int zkgpu_load_rows_async(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint64_t nrows, uint64_t ncols,
+                          uint64_t block_rows, uint64_t *stage, uint64_t stage_bytes, void **ticket);
+int zkgpu_load_wait(void *ticket);
 
 /* MerkleTreeGL::getGroupProof(Element *proof, uint64_t idx) for nq queries at
  * once -- merkleTreeGL.cpp:12-35, friProve.cpp:195-232.

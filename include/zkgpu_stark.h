@@ -68,6 +68,16 @@ int zkgpu_stark_witness(void *handle);
 /* load cm1_n from a host row-major buffer (n rows x n_cm1), the reference's
  * commit-pols layout (commit_pols.hpp:18) */
 int zkgpu_stark_set_cm1(void *handle, const uint64_t *rows);
+/* queue the trace of the proof AFTER the next one: returns at once, the
+ * trace crosses PCIe into a second cm1_n buffer (zkgpu_load_rows_async)
+ * while the next zkgpu_stark_prove runs on the current cm1_n, and becomes
+ * cm1_n when that prove returns.  `rows` must stay valid until then; a later
+ * set_cm1 / set_cm1_async supersedes it.  Costs one more cm1_n (n x n_cm1
+ * u64) of HBM.  Single-GPU prover only. */
+int zkgpu_stark_set_cm1_async(void *handle, const uint64_t *rows);
+/* cm1_n back into a host row-major buffer (n rows x n_cm1; the inverse of
+ * set_cm1).  Single-GPU prover only. */
+int zkgpu_stark_get_cm1(void *handle, uint64_t *rows);
 /* load the constant polynomials from a host row-major buffer (n rows x
  * n_const), the reference's .const file (ConstantPolsStarks, starks.hpp:94-116);
  * recomputes their LDE, tree and verkey */

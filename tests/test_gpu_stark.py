@@ -97,6 +97,43 @@ def test_set_cm1_row_major_boundary(oracle, zkgpu):
     g.close()
 
 
+def test_set_cm1_async_pipelined_proofs(oracle, zkgpu):
+    """Back-to-back proofs with the next trace handed over in the background
+    (zkgpu_stark_set_cm1_async during the current prove): each proof equals the
+    oracle's proof of its own trace.  The two traces differ in the free
+    (unconstrained) columns."""
+    from oracle.stark_prover import OracleStark
+    from zkgpu.synthetic import SyntheticStark
+    from zkgpu.stark import GpuStark
+    inst = SyntheticStark(n_bits=10, t=3, m=1, n_free=5, n_queries=8)
+    free = list(range(3 * inst.t, 3 * inst.t + inst.n_free))
+    traces, refs = [], []
+    for k in range(3):
+        o = OracleStark(inst)
+        o.witness()
+        if k:
+            rng = np.random.default_rng(k)
+            o.S[0][:, free] = rand_gl(rng, (o.N, len(free)))
+        traces.append(o.S[0].copy())
+        refs.append(o.prove())
+    assert refs[0] != refs[1]
+    g = GpuStark(inst)
+    g.set_cm1(traces[0])
+    assert np.array_equal(g.get_cm1(), traces[0])
+    g.set_cm1_async(traces[1])  # loads while proof 0 runs, taken when it returns
+    assert g.prove() == refs[0]
+    assert np.array_equal(g.get_cm1(), traces[1])
+    g.set_cm1_async(traces[2])
+    assert g.prove() == refs[1]
+    assert g.prove() == refs[2]
+    assert g.prove() == refs[2]  # nothing queued: the trace stays
+    # a queued load superseded by a synchronous one
+    g.set_cm1_async(traces[1])
+    g.set_cm1(traces[0])
+    assert g.prove() == refs[0]
+    g.close()
+
+
 def test_lookup_value_not_in_table_fails_loudly(oracle, zkgpu):
     """An f value outside the table stops the GPU prover with the reference's
     "Number not included" error (polinomial.hpp:409-413)."""

@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <thread>
 #include <vector>
 
 #include "gl_device.hpp"
@@ -610,19 +611,45 @@ int zkgpu_build_const_tree(uint64_t *tree_out, const uint64_t *const_pols, uint6
 }
 
 // ---------------------------------------------------------------- executor hand-off
-int zkgpu_load_rows_dev(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint64_t nrows, uint64_t ncols,
-                        uint64_t block_rows, int register_host)
+// block loop of the loaders: block b's H2D copy into stage half b & 1 on a copy
+// stream, its transpose into the columns on stream ts once copied; a half is
+// refilled only after its transpose has read it.  Returns with the work queued
+// (ts, the copy stream), not finished.
+static int load_rows_blocks(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint64_t nrows, uint64_t ncols,
+                            uint64_t block_rows, uint64_t *stage, hipStream_t cs, hipStream_t ts, hipEvent_t copied[2],
+                            hipEvent_t freed[2])
 {
-    int rc;
-    if ((rc = require_init())) return rc;
-    if (!nrows || !ncols) return 0;
-    if (ld < nrows) return set_error(ZKGPU_ERR_ARG, "load_rows: ld %llu < nrows", (unsigned long long)ld);
-    Ctx &c = g_ctx;
+    int rc = 0;
+    const uint64_t nblocks = (nrows + block_rows - 1) / block_rows;
+    for (uint64_t b = 0; b < nblocks && !rc; b++) {
+        const int k = (int)(b & 1);
+        const uint64_t r0 = b * block_rows, nr = std::min(block_rows, nrows - r0);
+        uint64_t *buf = stage + (size_t)k * block_rows * ncols;
+        if (b >= 2 && (rc = check_hip(hipStreamWaitEvent(cs, freed[k], 0), "wait"))) break;
+        if ((rc = check_hip(hipMemcpyAsync(buf, rows + r0 * ncols, nr * ncols * sizeof(uint64_t),
+                                           hipMemcpyHostToDevice, cs),
+                            "H2D")))
+            break;
+        if ((rc = check_hip(hipEventRecord(copied[k], cs), "record"))) break;
+        if ((rc = check_hip(hipStreamWaitEvent(ts, copied[k], 0), "wait"))) break;
+        rows_to_cols(buf, cols + r0, nr, ncols, ld, ts);
+        if ((rc = check_hip(hipEventRecord(freed[k], ts), "record"))) break;
+    }
+    return rc;
+}
+
+static uint64_t load_block_rows(uint64_t block_rows, uint64_t nrows, uint64_t ncols)
+{
     if (!block_rows) block_rows = std::max<uint64_t>(1, (64ULL << 20) / (ncols * sizeof(uint64_t)));  // ~64 MB
-    block_rows = std::min(block_rows, nrows);
-    const size_t blk_bytes = block_rows * ncols * sizeof(uint64_t);
-    uint64_t *stage = workspace(2, 2 * blk_bytes);
-    if (!stage) return ZKGPU_ERR_OOM;
+    return std::min(block_rows, nrows);
+}
+
+// one load on its own streams (transposes on ts): the shared body of the
+// synchronous and the background loader
+static int load_rows_streams(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint64_t nrows, uint64_t ncols,
+                             uint64_t block_rows, uint64_t *stage, hipStream_t ts, bool register_host)
+{
+    int rc = 0;
     const size_t total = nrows * ncols * sizeof(uint64_t);
     bool registered = false;
     if (register_host) {
@@ -637,23 +664,9 @@ int zkgpu_load_rows_dev(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint6
         rc = check_hip(hipEventCreateWithFlags(&copied[k], hipEventDisableTiming), "event");
         if (!rc) rc = check_hip(hipEventCreateWithFlags(&freed[k], hipEventDisableTiming), "event");
     }
-    const uint64_t nblocks = (nrows + block_rows - 1) / block_rows;
-    for (uint64_t b = 0; b < nblocks && !rc; b++) {
-        const int k = (int)(b & 1);
-        const uint64_t r0 = b * block_rows, nr = std::min(block_rows, nrows - r0);
-        uint64_t *buf = stage + (size_t)k * block_rows * ncols;
-        if (b >= 2 && (rc = check_hip(hipStreamWaitEvent(cs, freed[k], 0), "wait"))) break;
-        if ((rc = check_hip(hipMemcpyAsync(buf, rows + r0 * ncols, nr * ncols * sizeof(uint64_t),
-                                           hipMemcpyHostToDevice, cs),
-                            "H2D")))
-            break;
-        if ((rc = check_hip(hipEventRecord(copied[k], cs), "record"))) break;
-        if ((rc = check_hip(hipStreamWaitEvent(c.stream, copied[k], 0), "wait"))) break;
-        rows_to_cols(buf, cols + r0, nr, ncols, ld, c.stream);
-        if ((rc = check_hip(hipEventRecord(freed[k], c.stream), "record"))) break;
-    }
-    if (!rc) rc = check_hip(hipStreamSynchronize(c.stream), "load_rows sync");
-    (void)hipStreamSynchronize(cs);
+    if (!rc) rc = load_rows_blocks(cols, ld, rows, nrows, ncols, block_rows, stage, cs, ts, copied, freed);
+    if (!rc) rc = check_hip(hipStreamSynchronize(ts), "load_rows sync");
+    if (cs) (void)hipStreamSynchronize(cs);
     for (int k = 0; k < 2; k++) {
         if (copied[k]) (void)hipEventDestroy(copied[k]);
         if (freed[k]) (void)hipEventDestroy(freed[k]);
@@ -661,6 +674,71 @@ int zkgpu_load_rows_dev(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint6
     if (cs) (void)hipStreamDestroy(cs);
     if (registered) (void)hipHostUnregister((void *)rows);
     return rc ? rc : check_launch("rows_to_cols");
+}
+
+int zkgpu_load_rows_dev(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint64_t nrows, uint64_t ncols,
+                        uint64_t block_rows, int register_host)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!nrows || !ncols) return 0;
+    if (ld < nrows) return set_error(ZKGPU_ERR_ARG, "load_rows: ld %llu < nrows", (unsigned long long)ld);
+    block_rows = load_block_rows(block_rows, nrows, ncols);
+    uint64_t *stage = workspace(2, 2 * block_rows * ncols * sizeof(uint64_t));
+    if (!stage) return ZKGPU_ERR_OOM;
+    return load_rows_streams(cols, ld, rows, nrows, ncols, block_rows, stage, g_ctx.stream, register_host != 0);
+}
+
+// Background loader (zkgpu_load_rows_async): the same block loop in a host
+// thread of its own, on streams of its own, so a proof's kernels on the
+// library stream run while the next trace crosses PCIe.  A pageable source
+// is staged through the driver by the calling thread of the copy, which is
+// why the copies need a thread and not only a stream.
+struct LoadTicket {
+    std::thread th;
+    int rc = 0;
+};
+
+uint64_t zkgpu_load_rows_stage_bytes(uint64_t nrows, uint64_t ncols, uint64_t block_rows)
+{
+    if (!nrows || !ncols) return 0;
+    return 2 * load_block_rows(block_rows, nrows, ncols) * ncols * sizeof(uint64_t);
+}
+
+int zkgpu_load_rows_async(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint64_t nrows, uint64_t ncols,
+                          uint64_t block_rows, uint64_t *stage, uint64_t stage_bytes, void **ticket)
+{
+    int rc;
+    *ticket = nullptr;
+    if ((rc = require_init())) return rc;
+    if (ld < nrows) return set_error(ZKGPU_ERR_ARG, "load_rows_async: ld %llu < nrows", (unsigned long long)ld);
+    block_rows = load_block_rows(block_rows, nrows, ncols);
+    if (nrows && ncols && (!stage || stage_bytes < 2 * block_rows * ncols * sizeof(uint64_t)))
+        return set_error(ZKGPU_ERR_ARG, "load_rows_async: stage of %llu bytes < 2 blocks (%llu)",
+                         (unsigned long long)stage_bytes, (unsigned long long)(2 * block_rows * ncols * 8));
+    LoadTicket *t = new LoadTicket();
+    const int device = g_ctx.device;
+    t->th = std::thread([=] {
+        if (!nrows || !ncols) return;
+        int r = check_hip(hipSetDevice(device), "hipSetDevice (loader)");
+        hipStream_t ts = nullptr;
+        if (!r) r = check_hip(hipStreamCreateWithFlags(&ts, hipStreamNonBlocking), "loader stream");
+        if (!r) r = load_rows_streams(cols, ld, rows, nrows, ncols, block_rows, stage, ts, false);
+        if (ts) (void)hipStreamDestroy(ts);
+        t->rc = r;
+    });
+    *ticket = t;
+    return 0;
+}
+
+int zkgpu_load_wait(void *ticket)
+{
+    if (!ticket) return 0;
+    LoadTicket *t = (LoadTicket *)ticket;
+    if (t->th.joinable()) t->th.join();
+    const int rc = t->rc;
+    delete t;
+    return rc;
 }
 
 // ---------------------------------------------------------------- device memory

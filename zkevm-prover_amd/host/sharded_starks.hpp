@@ -575,6 +575,8 @@ public:
     }
 
     int commit_const() override { return fail("stark (sharded): constants are committed from their whole copy"); }
+    int set_cm1_async(const uint64_t *) override { return fail("stark (sharded): set_cm1_async is single-GPU only"); }
+    int get_cm1(uint64_t *) override { return fail("stark (sharded): get_cm1 is single-GPU only"); }
 
     // the executor's row-major buffer: the rank takes rows [r0, r0 + ldn) mod N
     int set_cm1(const uint64_t *rows) override

@@ -173,8 +173,15 @@ public:
     bool dry = false;
     uint64_t planned = 0;
 
+    // background hand-off of the next proof's cm1_n (set_cm1_async)
+    uint64_t *cm1_next = nullptr, *cm1_xfer = nullptr;
+    uint64_t xfer_bytes = 0;
+    void *cm1_ticket = nullptr;
+    bool cm1_pending = false;
+
     virtual ~Starks()
     {
+        (void)zkgpu_load_wait(cm1_ticket);
         for (void *p : allocs) zkgpu_dev_free(p);
     }
 
@@ -399,15 +406,54 @@ public:
         return 0;
     }
 
+    // the executor's row-major buffer, streamed in row blocks (no full-size
+    // staging copy: at the fork-9 widths cm1_n is 25-50 GB)
     virtual int set_cm1(const uint64_t *rows)
     {
+        if (take_cm1_async(false)) return -1;  // a pending background load is superseded
+        if (zkgpu_load_rows_dev(S.sec[SEC_CM1_N], N, rows, N, info.n_cm1, 0, 0))
+            return fail("set_cm1: %s", zkgpu_last_error());
+        return 0;
+    }
+
+    // cm1_n back as the executor's row-major layout (n rows x n_cm1)
+    virtual int get_cm1(uint64_t *rows)
+    {
         void *tmp = nullptr;
-        CK(zkgpu_dev_malloc(&tmp, (uint64_t)info.n_cm1 * N * 8));
-        int rc = zkgpu_memcpy_h2d(tmp, rows, (uint64_t)info.n_cm1 * N * 8);
-        if (!rc) rc = zkgpu_rows_to_cols_dev(S.sec[SEC_CM1_N], N, (const uint64_t *)tmp, N, info.n_cm1);
-        if (!rc) rc = zkgpu_synchronize();
+        const uint64_t bytes = (uint64_t)info.n_cm1 * N * 8;
+        CK(zkgpu_dev_malloc(&tmp, bytes ? bytes : 8));
+        int rc = zkgpu_cols_to_rows_dev((uint64_t *)tmp, S.sec[SEC_CM1_N], N, N, info.n_cm1);
+        if (!rc) rc = zkgpu_memcpy_d2h(rows, tmp, bytes);
         zkgpu_dev_free(tmp);
-        if (rc) return fail("set_cm1: %s", zkgpu_last_error());
+        if (rc) return fail("get_cm1: %s", zkgpu_last_error());
+        return 0;
+    }
+
+    virtual int set_cm1_async(const uint64_t *rows)
+    {
+        if (take_cm1_async(false)) return -1;
+        if (!cm1_next) {
+            xfer_bytes = zkgpu_load_rows_stage_bytes(N, info.n_cm1, 0);
+            if (dalloc(&cm1_next, (uint64_t)(info.n_cm1 ? info.n_cm1 : 1) * N) ||
+                dalloc(&cm1_xfer, std::max<uint64_t>(1, xfer_bytes / 8)))
+                return -1;
+        }
+        if (zkgpu_load_rows_async(cm1_next, N, rows, N, info.n_cm1, 0, cm1_xfer, xfer_bytes, &cm1_ticket))
+            return fail("set_cm1_async: %s", zkgpu_last_error());
+        cm1_pending = true;
+        return 0;
+    }
+
+    // wait for a queued background load; with `use`, swap its buffer in as
+    // cm1_n (every consumer reads S.sec at call time), else drop it
+    int take_cm1_async(bool use)
+    {
+        if (!cm1_pending) return 0;
+        cm1_pending = false;
+        const int rc = zkgpu_load_wait(cm1_ticket);
+        cm1_ticket = nullptr;
+        if (rc) return fail("set_cm1_async: %s", zkgpu_last_error());
+        if (use) std::swap(S.sec[SEC_CM1_N], cm1_next);
         return 0;
     }
 
@@ -477,7 +523,16 @@ public:
         return 0;
     }
 
+    // the proof of the current cm1_n; a trace queued by set_cm1_async (loaded
+    // meanwhile) becomes cm1_n when it returns
     virtual int prove(uint64_t *out)
+    {
+        const int rc = prove_body(out);
+        const int rc2 = take_cm1_async(true);
+        return rc ? rc : rc2;
+    }
+
+    int prove_body(uint64_t *out)
     {
         timers.clear();
         auto tall = clk::now();
@@ -800,6 +855,8 @@ int zkgpu_stark_create(void **handle, const zkgpu_stark_info *info)
 
 int zkgpu_stark_witness(void *h) { return ((Starks *)h)->witness(); }
 int zkgpu_stark_set_cm1(void *h, const uint64_t *rows) { return ((Starks *)h)->set_cm1(rows); }
+int zkgpu_stark_set_cm1_async(void *h, const uint64_t *rows) { return ((Starks *)h)->set_cm1_async(rows); }
+int zkgpu_stark_get_cm1(void *h, uint64_t *rows) { return ((Starks *)h)->get_cm1(rows); }
 int zkgpu_stark_set_const(void *h, const uint64_t *rows) { return ((Starks *)h)->set_const(rows); }
 int zkgpu_stark_set_publics(void *h, const uint64_t *publics) { return ((Starks *)h)->set_publics(publics); }
 uint64_t zkgpu_stark_proof_len(void *h) { return ((Starks *)h)->proof_len(); }

@@ -61,6 +61,9 @@ _SIGS = {
     "zkgpu_const_tree_num_elements": (u64, [u64, u32]),
     "zkgpu_build_const_tree": (ctypes.c_int, [vp, vp, u64, u32, u32]),
     "zkgpu_load_rows_dev": (ctypes.c_int, [vp, u64, vp, u64, u64, u64, ctypes.c_int]),
+    "zkgpu_load_rows_stage_bytes": (u64, [u64, u64, u64]),
+    "zkgpu_load_rows_async": (ctypes.c_int, [vp, u64, vp, u64, u64, u64, vp, u64, ctypes.POINTER(vp)]),
+    "zkgpu_load_wait": (ctypes.c_int, [vp]),
     "zkgpu_gl_merkletree_dev": (ctypes.c_int, [vp, vp, u64, u64, u64]),
     "zkgpu_gl_merkletree_rows_dev": (ctypes.c_int, [vp, vp, u64, u64]),
     "zkgpu_gl_merkle_open_dev": (ctypes.c_int, [vp, vp, vp, vp, u64, u64, u64, vp, u64]),
@@ -273,6 +276,36 @@ def load_rows_dev(cols, ld, rows, block_rows=0, register_host=False):
     nrows, ncols = rows.shape
     _check(lib().zkgpu_load_rows_dev(_addr(cols), ld, rows.ctypes.data, nrows, ncols, block_rows,
                                      int(register_host)), "zkgpu_load_rows_dev")
+
+
+class RowsLoad:
+    """Background hand-off (zkgpu_load_rows_async): wait() returns once the
+    columns hold the rows.  Keeps the host rows and the staging buffer alive
+    until then."""
+
+    def __init__(self, cols, ld, rows, stage, ticket):
+        self.cols, self.rows, self.stage, self.ticket = cols, rows, stage, ticket
+
+    def wait(self):
+        if self.ticket is not None:
+            t, self.ticket = self.ticket, None
+            _check(lib().zkgpu_load_wait(t), "zkgpu_load_wait")
+
+
+def load_rows_async(cols, ld, rows, stage, block_rows=0):
+    """Start the load of host row-major rows into device column-major cols on
+    the library's loader thread; stage: device buffer of at least
+    load_rows_stage_bytes(nrows, ncols) bytes.  Returns a RowsLoad."""
+    rows = np.ascontiguousarray(rows, dtype=np.uint64)
+    nrows, ncols = rows.shape
+    t = ctypes.c_void_p()
+    _check(lib().zkgpu_load_rows_async(_addr(cols), ld, rows.ctypes.data, nrows, ncols, block_rows, _addr(stage),
+                                       stage.numel() * stage.element_size(), ctypes.byref(t)), "zkgpu_load_rows_async")
+    return RowsLoad(cols, ld, rows, stage, t)
+
+
+def load_rows_stage_bytes(nrows, ncols, block_rows=0):
+    return int(lib().zkgpu_load_rows_stage_bytes(nrows, ncols, block_rows))
 
 
 def ntt_dev(dst, ld_dst, src, ld_src, n, ncols, inverse=False):

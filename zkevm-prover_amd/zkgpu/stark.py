@@ -68,6 +68,8 @@ def slib():
             ("zkgpu_stark_create", ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(_Info)]),
             ("zkgpu_stark_witness", ctypes.c_int, [vp]),
             ("zkgpu_stark_set_cm1", ctypes.c_int, [vp, vp]),
+            ("zkgpu_stark_set_cm1_async", ctypes.c_int, [vp, vp]),
+            ("zkgpu_stark_get_cm1", ctypes.c_int, [vp, vp]),
             ("zkgpu_stark_proof_len", u64, [vp]),
             ("zkgpu_stark_prove", ctypes.c_int, [vp, vp]),
             ("zkgpu_stark_verkey", ctypes.c_int, [vp, vp]),
@@ -292,6 +294,20 @@ class GpuStark:
         rows = np.ascontiguousarray(rows, np.uint64)
         _check(slib().zkgpu_stark_set_cm1(self.h, rows.ctypes.data), "zkgpu_stark_set_cm1")
 
+    def get_cm1(self):
+        """cm1_n as the executor's row-major buffer (n x n_cm1)"""
+        rows = np.empty((1 << self.inst.n_bits, self.inst.n_cm1), np.uint64)
+        _check(slib().zkgpu_stark_get_cm1(self.h, rows.ctypes.data), "zkgpu_stark_get_cm1")
+        return rows
+
+    def set_cm1_async(self, rows):
+        """queue the trace of the proof after the next one: it loads while the
+        next prove() runs and is cm1_n when that returns (`rows` is kept
+        referenced until then)"""
+        rows = np.ascontiguousarray(rows, np.uint64)
+        self._cm1_next = rows
+        _check(slib().zkgpu_stark_set_cm1_async(self.h, rows.ctypes.data), "zkgpu_stark_set_cm1_async")
+
     def verkey(self):
         v = np.zeros(4, np.uint64)
         slib().zkgpu_stark_verkey(self.h, v.ctypes.data)
@@ -306,6 +322,7 @@ class GpuStark:
         n = slib().zkgpu_stark_proof_len(self.h)
         buf = np.zeros(n, np.uint64)
         _check(slib().zkgpu_stark_prove(self.h, buf.ctypes.data), "zkgpu_stark_prove")
+        self._cm1_next = None  # a background cm1 load was taken by this prove
         return buf
 
     def prove(self):
