@@ -297,13 +297,19 @@ struct Dot3 {
     // table through, csrc/zxp_jit.hip)
     __device__ __forceinline__ void term_al(uint64_t a, const uint32_t *c)
     {
-#ifdef ZK_LIMB_AS
+#if defined(ZK_LIMB_AS)
         typedef uint32_t u32x4_ __attribute__((ext_vector_type(4)));
         typedef uint32_t u32x2_ __attribute__((ext_vector_type(2)));
         const u32x4_ qv = *(const ZK_LIMB_AS u32x4_ *)c;
         const u32x2_ rv = *(const ZK_LIMB_AS u32x2_ *)(c + 4);
         const LimbQ q{qv.x, qv.y, qv.z, qv.w};
         const LimbP r{rv.x, rv.y};
+#elif defined(ZK_LIMB_STRUCT)
+        // a whole-table LDS copy read by an -O2 kernel (zxp_jit.hip): the
+        // load/store vectorizer merges the struct copy itself; explicit vector
+        // loads there cost the config-4 quotient 13.3 -> 16.3 ms
+        const LimbQ q = *(const LimbQ *)c;
+        const LimbP r = *(const LimbP *)(c + 4);
 #else
         // explicit vector types: a struct copy is split into dword loads at
         // -O1, which the LDS chunks of the split programs then read as

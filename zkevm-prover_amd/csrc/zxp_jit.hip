@@ -1288,6 +1288,14 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         }();
         if (rb) src += "#define ZK_RB 1\n";
     }
+    {
+        // DOT limb reads (gl_device.hpp Dot3::term_al): explicit 16 + 8-byte
+        // loads for the split programs' LDS chunks (-O1), the struct copy the
+        // -O2 vectorizer merges for the others; ZKGPU_ZXP_JIT_LIMB_STRUCT
+        // forces one form (1 struct, 0 vector) for A/B
+        const char *e = getenv("ZKGPU_ZXP_JIT_LIMB_STRUCT");
+        if (e ? atoi(e) != 0 : !kchunk) src += "#define ZK_LIMB_STRUCT 1\n";
+    }
     src += k_gl_device_src;
     appendf(src, "#define ZKJIT_KL_LDS %d\n", !kchunk && jit_kl_lds(kl.size()) ? 1 : 0);
     appendf(src, "#define ZKJIT_SPLIT %d\n", split ? 1 : 0);
