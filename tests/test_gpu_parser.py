@@ -205,6 +205,8 @@ def test_zkevm_shaped_programs_gpu_equal_oracle(oracle, zkgpu, monkeypatch, name
     ran = zkgpu.prof_kernels()
     if jit == "2":
         assert any(k.startswith("k_zxp_jit") for k in ran), ("the compiled kernels did not run", ran)
+        if name == "step52ns":  # its three opening-point chains run fused (zxp_jit.hip "fused column chains")
+            assert "for (int q_" in zkgpu.zxp_jit_source(prog, chal, pub, evals)
     # oracle on the same inputs (x_i = 7 w^i on the 2n coset, w^i on the n domain)
     x = np.zeros(dom, np.uint64)
     oracle.lib().oc_powers(oracle._p(x), 7 if ext else 1, oracle.gl_w(log_dom), dom)

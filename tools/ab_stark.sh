@@ -3,6 +3,7 @@
 # --workload stark, no side measurements): one bench process per variant,
 # baseline first and last; prints s/proof and the expression-stage timers.
 # The variants' code objects must be in the JIT cache (prebuilt on the CPU).
+# AB_BENCH_ARGS: extra bench.py arguments (e.g. "--zkevm-shaped --log-n 22").
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -10,7 +11,7 @@ run() {
     local tag=$1
     shift
     env "$@" timeout -k 10 300 python bench.py --workload stark --no-lde --no-s42 --no-sharded --no-cpu --no-handoff \
-        --steps 3 --warmup 1 > gpurun_out/ab_stark.json 2> gpurun_out/ab_stark.err
+        --steps 3 --warmup 1 ${AB_BENCH_ARGS:-} > gpurun_out/ab_stark.json 2> gpurun_out/ab_stark.err
     local rc=$?
     [ $rc -eq 0 ] || { echo "[ab_stark] $tag rc=$rc"; tail -3 gpurun_out/ab_stark.err; exit $rc; }
     python3 -c "

@@ -29,6 +29,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <array>
 #include <map>
 #include <set>
 #include <mutex>
@@ -896,12 +897,211 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             if (I.op != ZXP_COPY && I.b < last_read.size()) last_read[I.b] = k;
         }
     }
+    // Only programs of ZKGPU_ZXP_JIT_SPLIT_MIN (1000) compiled instructions or
+    // more are split: the opaque branch costs registers (config-4 FRI
+    // polynomial: 74 -> 200 VGPRs, 9 -> 57 ms), and small programs compile in
+    // seconds as one block.
+    static const uint32_t split_min = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_SPLIT_MIN");
+        return (uint32_t)(e ? atol(e) : 1000);
+    }();
+    const bool split = in.n_instr >= split_min || in.force_split;
+    // ---- fused column chains (the FRI polynomial, step52ns) -------------
+    // A Horner chain over committed columns compiles to a chain of DOTs of at
+    // most max_terms terms, each carrying the previous one as an F_p^3 term;
+    // the FRI polynomial has one chain per opening point and most columns sit
+    // in several of them (zkEVM-shaped step52ns: 3 chains, 3,778 column terms
+    // over 1,497 columns; config-4: 397 over 189), each read again from HBM
+    // at a distance no cache holds.  A non-split program evaluates up to
+    // FUSE_MAX such chains together where the first link stood: each chain is
+    // unrolled on the host (a link's column coefficient mapped through the
+    // later links' carry maps, exact arithmetic mod p), the columns are
+    // grouped by the set of chains they appear in, and each group is one loop
+    // that reads a column once and accumulates it into all of its chains.
+    // Same values (the chain sum is linear; accumulators are reduced every
+    // FUSE_PIECE columns).  Measured (A/B on one box): zkEVM-shaped FRI
+    // polynomial at 2^23 rows 69.4 -> 38.4 ms (proof 1.134 -> 1.104 s); the
+    // config-4 one (397 column terms, its re-reads close enough to hit the
+    // caches) 9.3 -> 10.4 ms, so only chains of ZKGPU_ZXP_JIT_FUSE_MIN (1024)
+    // column terms or more are fused.  ZKGPU_ZXP_JIT_FUSE=0 disables.
+    constexpr int FUSE_MAX = 4;
+    constexpr uint32_t FUSE_PIECE = 224;
+    static const int fuse_env = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_FUSE");
+        return e ? atoi(e) : 1;
+    }();
+    static const size_t fuse_min = [] {
+        const char *e = getenv("ZKGPU_ZXP_JIT_FUSE_MIN");
+        return (size_t)(e ? atol(e) : 1024);
+    }();
+    std::vector<int32_t> fused(in.n_instr, -1);  // chain of a fused link
+    std::vector<std::vector<uint32_t>> fchains;   // links in order, per fused chain
+    uint32_t fuse_at = UINT32_MAX;                // where the fused chains are evaluated
+    if (!split && fuse_env) {
+        // a link: DOT3 whose terms are column reads (columns the program never
+        // writes), constants, and the whole previous link (its only reader)
+        std::map<uint32_t, uint32_t> def_at;  // SSA operand -> defining instruction
+        for (uint32_t k = 0; k < in.n_instr; k++) def_at[in.ins[k].dst] = k;
+        std::vector<int64_t> prev(in.n_instr, -2);  // -2 not a link, -1 first link, else previous link
+        std::vector<uint32_t> readers(in.n_opnd ? in.n_opnd : 1, 0);
+        for (uint32_t k = 0; k < in.n_instr; k++) {
+            const zxp_instr &I = in.ins[k];
+            if (I.op == ZXP_DOT1 || I.op == ZXP_DOT3) {
+                std::set<uint32_t> srcs;
+                for (uint32_t t = I.a; t < I.a + I.b; t++)
+                    if (in.terms[t].src != ZXP_TERM_ONE && in.terms[t].src < in.n_opnd) srcs.insert(in.terms[t].src);
+                for (uint32_t x : srcs) readers[x]++;
+            } else {
+                if (I.a < in.n_opnd) readers[I.a]++;
+                if (I.op != ZXP_COPY && I.b < in.n_opnd && I.b != I.a) readers[I.b]++;
+            }
+        }
+        for (uint32_t k = 0; k < in.n_instr; k++) {
+            const zxp_instr &I = in.ins[k];
+            if (I.op != ZXP_DOT3 || in.opnd[I.dst].kind != ZXP_TMP3) continue;
+            int64_t pv = -1;
+            bool ok = true;
+            uint32_t ncol = 0;
+            for (uint32_t t = I.a; t < I.a + I.b && ok; t++) {
+                const zxp_term &tm = in.terms[t];
+                if (tm.src == ZXP_TERM_ONE) continue;
+                const zxp_operand &o = in.opnd[tm.src];
+                if (o.kind == ZXP_COL) {
+                    ok = !is_written(col_slot(o.a, o.b));
+                    ncol++;
+                } else if (o.kind == ZXP_TMP3 && def_at.count(tm.src) && prev[def_at[tm.src]] != -2 &&
+                           readers[tm.src] == 1 && (pv < 0 || pv == (int64_t)def_at[tm.src])) {
+                    pv = def_at[tm.src];
+                } else {
+                    ok = false;
+                }
+            }
+            if (ok && (ncol > 0 || pv >= 0)) prev[k] = pv;
+        }
+        // chains: from links nobody continues, walk back
+        std::vector<uint8_t> continued(in.n_instr, 0);
+        for (uint32_t k = 0; k < in.n_instr; k++)
+            if (prev[k] >= 0) continued[prev[k]] = 1;
+        std::vector<std::vector<uint32_t>> cand;
+        for (uint32_t k = 0; k < in.n_instr; k++) {
+            if (prev[k] == -2 || continued[k]) continue;
+            std::vector<uint32_t> ch;
+            for (int64_t x = k; x >= 0; x = prev[x]) ch.push_back((uint32_t)x);
+            std::reverse(ch.begin(), ch.end());
+            cand.push_back(ch);
+        }
+        // the largest chains (by column terms), if at least two share columns
+        auto ncols_of = [&](const std::vector<uint32_t> &ch) {
+            size_t n = 0;
+            for (uint32_t x : ch) n += in.ins[x].b;
+            return n;
+        };
+        std::stable_sort(cand.begin(), cand.end(),
+                         [&](const std::vector<uint32_t> &a, const std::vector<uint32_t> &b) { return ncols_of(a) > ncols_of(b); });
+        if (cand.size() > (size_t)FUSE_MAX) cand.resize(FUSE_MAX);
+        std::map<std::pair<uint32_t, int32_t>, uint32_t> in_chains;  // (slot, shift) -> chain mask
+        for (size_t g = 0; g < cand.size(); g++)
+            for (uint32_t x : cand[g])
+                for (uint32_t t = in.ins[x].a; t < in.ins[x].a + in.ins[x].b; t++) {
+                    const zxp_term &tm = in.terms[t];
+                    if (tm.src == ZXP_TERM_ONE || in.opnd[tm.src].kind != ZXP_COL) continue;
+                    const zxp_operand &o = in.opnd[tm.src];
+                    in_chains[{col_slot(o.a, o.b), (int32_t)o.c}] |= 1u << g;
+                }
+        size_t shared = 0, terms = 0;
+        for (auto &kv : in_chains) {
+            shared += __builtin_popcount(kv.second) > 1;
+            terms += __builtin_popcount(kv.second);
+        }
+        if (cand.size() >= 2 && shared > 0 && terms >= fuse_min) {
+            fchains = cand;
+            for (size_t g = 0; g < fchains.size(); g++)
+                for (uint32_t x : fchains[g]) {
+                    fused[x] = (int32_t)g;
+                    fuse_at = std::min(fuse_at, x);
+                }
+        }
+    }
+    // unrolled chains: per chain, the coefficient (F_p^3) of every column and
+    // the constant, mapped through the later links' carry maps
+    struct FusedCol {
+        uint32_t slot;
+        int32_t sh;
+        uint32_t mask;  // chains the column appears in (structure, not values)
+        uint64_t c[FUSE_MAX][3];
+    };
+    std::vector<FusedCol> fcols;  // in order of first appearance
+    std::vector<std::array<uint64_t, 3>> fconst(fchains.size(), std::array<uint64_t, 3>{0, 0, 0});
+    if (!fchains.empty()) {
+        constexpr uint64_t P = 0xFFFFFFFF00000001ULL;
+        auto fadd = [](uint64_t a, uint64_t b) {
+            const uint64_t s = a + b;
+            return (s < a || s >= P) ? s - P : s;
+        };
+        auto fmul = [](uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) % P); };
+        std::map<std::pair<uint32_t, int32_t>, size_t> fidx;
+        for (size_t g = 0; g < fchains.size(); g++)
+            for (uint32_t x : fchains[g])
+                for (uint32_t t = in.ins[x].a; t < in.ins[x].a + in.ins[x].b; t++) {
+                    const zxp_term &tm = in.terms[t];
+                    if (tm.src == ZXP_TERM_ONE || in.opnd[tm.src].kind != ZXP_COL) continue;
+                    const zxp_operand &o = in.opnd[tm.src];
+                    const std::pair<uint32_t, int32_t> key{col_slot(o.a, o.b), (int32_t)o.c};
+                    if (!fidx.count(key)) {
+                        fidx[key] = fcols.size();
+                        FusedCol fc;
+                        memset(&fc, 0, sizeof(fc));
+                        fc.slot = key.first;
+                        fc.sh = key.second;
+                        fcols.push_back(fc);
+                    }
+                }
+        for (size_t g = 0; g < fchains.size(); g++) {
+            // M: the map from a link's value to the chain's final value (3x3 over F_p)
+            uint64_t M[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+            for (size_t li = fchains[g].size(); li-- > 0;) {
+                const zxp_instr &I = in.ins[fchains[g][li]];
+                uint64_t L[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};  // previous link -> this link
+                for (uint32_t t = I.a; t < I.a + I.b; t++) {
+                    const zxp_term &tm = in.terms[t];
+                    uint64_t a[3], v[3];
+                    for (int j = 0; j < 3; j++) a[j] = tm.coef[j] % P;
+                    for (int r = 0; r < 3; r++) {
+                        v[r] = 0;
+                        for (int j = 0; j < 3; j++) v[r] = fadd(v[r], fmul(M[r][j], a[j]));
+                    }
+                    if (tm.src == ZXP_TERM_ONE) {
+                        for (int r = 0; r < 3; r++) fconst[g][r] = fadd(fconst[g][r], v[r]);
+                    } else if (in.opnd[tm.src].kind == ZXP_COL) {
+                        const zxp_operand &o = in.opnd[tm.src];
+                        FusedCol &fc = fcols[fidx[{col_slot(o.a, o.b), (int32_t)o.c}]];
+                        fc.mask |= 1u << g;
+                        for (int r = 0; r < 3; r++) fc.c[g][r] = fadd(fc.c[g][r], v[r]);
+                    } else {  // the previous link, component tm.comp
+                        for (int r = 0; r < 3; r++) L[r][tm.comp] = fadd(L[r][tm.comp], a[r]);
+                    }
+                }
+                uint64_t M2[3][3];
+                for (int r = 0; r < 3; r++)
+                    for (int c = 0; c < 3; c++) {
+                        M2[r][c] = 0;
+                        for (int j = 0; j < 3; j++) M2[r][c] = fadd(M2[r][c], fmul(M[r][j], L[j][c]));
+                    }
+                memcpy(M, M2, sizeof(M));
+            }
+        }
+    }
     std::vector<size_t> dot_k0(in.n_instr, 0);
     std::vector<uint32_t> first_use(in.n_instr, UINT32_MAX);  // declaration point of DOT k's accumulators
     {
         std::vector<int64_t> last1(in.n_tmp1 + 1, -1), last3(in.n_tmp3 + 1, -1);
         for (uint32_t k = 0; k < in.n_instr; k++) {
             const zxp_instr &I = in.ins[k];
+            if (fused[k] >= 0) {  // evaluated with its chain at fuse_at
+                const zxp_operand &D = in.opnd[I.dst];
+                if (D.kind == ZXP_TMP3) last3[D.a] = (k == fchains[fused[k]].back()) ? (int64_t)fuse_at : (int64_t)k;
+                continue;
+            }
             if (I.op == ZXP_DOT1 || I.op == ZXP_DOT3) {
                 const bool three = I.op == ZXP_DOT3;
                 uint64_t c0[3] = {0, 0, 0};
@@ -991,15 +1191,6 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         const long b = e ? atol(e) : 1024;
         return (size_t)(b > 0 ? b : 1L << 40);
     }();
-    // Only programs of ZKGPU_ZXP_JIT_SPLIT_MIN (1000) compiled instructions or
-    // more are split: the opaque branch costs registers (config-4 FRI
-    // polynomial: 74 -> 200 VGPRs, 9 -> 57 ms), and small programs compile in
-    // seconds as one block.
-    static const uint32_t split_min = [] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_SPLIT_MIN");
-        return (uint32_t)(e ? atol(e) : 1000);
-    }();
-    const bool split = in.n_instr >= split_min || in.force_split;
     // Limb chunks in LDS (ZKGPU_ZXP_JIT_KCHUNK): a split program whose limb
     // table is too large for LDS reads it from global memory, one wave-uniform
     // 16 + 8-byte vector load pair per term, each taking the texture
@@ -1102,10 +1293,83 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                 appendf(body, "D%u_0`.term_al(%s, K + %zu);\n", st.dot, st.val.c_str(), kt);
         }
     };
+    // the fused chains (above), where their first link stood
+    auto emit_fused = [&]() -> int {
+        const size_t G = fchains.size();
+        body += "{\n";
+        for (size_t g = 0; g < G; g++) {
+            align_kl(4);
+            const size_t o = kl.size();
+            for (int j = 0; j < 3; j++) limbs3(fconst[g][j]);
+            appendf(body, "Dot3 F%zu_0` = Dot3(K + %zu), F%zu_1` = Dot3(K + %zu), F%zu_2` = Dot3(K + %zu);\n", g, o, g, o + 4,
+                    g, o + 8);
+        }
+        std::vector<uint32_t> fill(G, 0);  // terms since the chain's last reduction
+        for (uint32_t mask = 1; mask < (1u << G); mask++) {
+            std::vector<const FusedCol *> cols;
+            for (const FusedCol &fc : fcols)
+                if (fc.mask == mask) cols.push_back(&fc);
+            if (cols.empty()) continue;
+            std::vector<int> mem;
+            for (size_t g = 0; g < G; g++)
+                if (mask >> g & 1) mem.push_back((int)g);
+            const size_t R = mem.size();
+            for (size_t p0 = 0; p0 < cols.size(); p0 += FUSE_PIECE) {
+                const size_t n = std::min<size_t>(FUSE_PIECE, cols.size() - p0);
+                const size_t np = (n + 3) & ~(size_t)3;
+                const size_t off = zt.size();
+                for (size_t e = 0; e < np; e++) {
+                    const FusedCol &fc = *cols[p0 + std::min(e, n - 1)];
+                    for (size_t r = 0; r < R; r++) {
+                        JitTerm jt;
+                        memset(&jt, 0, sizeof(jt));
+                        jt.ptr = cp[fc.slot];
+                        jt.sh = fc.sh;
+                        if (e < n)  // padding entries: zero limbs
+                            for (int j = 0; j < 3; j++) zxp_limbs6(fc.c[mem[r]][j] % 0xFFFFFFFF00000001ULL, jt.c[j]);
+                        zt.push_back(jt);
+                    }
+                }
+                for (int g : mem)
+                    if (fill[g] + np > 240) {  // Dot3 accumulators: reduce before 2^63 (gl_device.hpp)
+                        appendf(body, "{ const uint64_t x0_ = F%d_0`.fin(), x1_ = F%d_1`.fin(), x2_ = F%d_2`.fin(); "
+                                      "F%d_0` = Dot3(); F%d_0`.lane(x0_); F%d_1` = Dot3(); F%d_1`.lane(x1_); "
+                                      "F%d_2` = Dot3(); F%d_2`.lane(x2_); }\n",
+                                g, g, g, g, g, g, g, g, g);
+                        fill[g] = 1;
+                    }
+                for (int g : mem) fill[g] += (uint32_t)np;
+                appendf(body, "for (int q_ = 0; q_ < %zu; q_ += 4) {\nconst JitTerm *t_ = ZT + %zu + (size_t)q_ * %zu;\n"
+                              "uint64_t fv`[4];\n", np, off, R);
+                appendf(body, "_Pragma(\"unroll\") for (int u_ = 0; u_ < 4; u_++) fv`[u_] = gload(t_[u_ * %zu].ptr + "
+                              "((i` + (uint64_t)t_[u_ * %zu].sh) & m));\n", R, R);
+                body += "_Pragma(\"unroll\") for (int u_ = 0; u_ < 4; u_++) {\n";
+                for (size_t r = 0; r < R; r++)
+                    appendf(body, "F%d_0`.term(fv`[u_], t_[u_ * %zu + %zu].c[0]); F%d_1`.term(fv`[u_], t_[u_ * %zu + %zu].c[1]); "
+                                  "F%d_2`.term(fv`[u_], t_[u_ * %zu + %zu].c[2]);\n",
+                            mem[r], R, r, mem[r], R, r, mem[r], R, r);
+                body += "}\n}\n";
+            }
+        }
+        for (size_t g = 0; g < G; g++) {
+            char fin[128];
+            snprintf(fin, sizeof(fin), "gl3{{F%zu_0`.fin(), F%zu_1`.fin(), F%zu_2`.fin()}}", g, g, g);
+            if (assign(in.ins[fchains[g].back()].dst, Expr{fin, 3})) return 1;
+        }
+        body += "}\n";
+        return 0;
+    };
     for (uint32_t k = 0; k < in.n_instr; k++) {
         const zxp_instr &I = in.ins[k];
         maybe_split();
         emit_declarations(k);
+        if (fused[k] >= 0) {
+            if (k == fuse_at) {
+                if (emit_fused()) return 1;
+                emit_streams(k);
+            }
+            continue;
+        }
         if (I.op == ZXP_DOT1 || I.op == ZXP_DOT3) {
             const bool three = I.op == ZXP_DOT3;
             // column terms read from memory: looped from the term table when
