@@ -835,7 +835,7 @@ def main():
         if args.workload == "stark" and not args.no_lde:
             lde, roof = lde_measure(args, dev, torch, world, dist)
         if args.workload == "stark" and world == 1 and not args.no_handoff:
-            handoff = handoff_measure(n, C, dev, torch, zkgpu, value)
+            handoff = handoff_measure(n, inst.n_cm1, dev, torch, zkgpu, value)
             handoff["pipelined"] = handoff_pipelined(gs, value)
         if args.workload == "stark" and world == 1 and args.log_n == 23 and not args.no_s42:
             gs = None  # the config-4 instance's HBM back before the 200 GB of fork-9-width sections
