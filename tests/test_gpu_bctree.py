@@ -58,3 +58,26 @@ def test_load_rows_dev(zkgpu, nrows, ncols, block, register):
     torch.cuda.synchronize()
     got = zkgpu.from_device(cols).reshape(ncols, ld)[:, :nrows]
     assert np.array_equal(got, rows.T)
+
+
+@pytest.mark.parametrize("nrows,ncols,block", [(1000, 13, 96), (4096, 751, 0), (64, 1, 7)])
+def test_load_rows_async(zkgpu, nrows, ncols, block):
+    """The background loader (zkgpu_load_rows_async on the library's loader
+    thread and streams) lands the same columns as the synchronous one, while
+    kernels on the library stream run beside it; a too-small stage is refused."""
+    import torch
+    rng = np.random.default_rng(7 * nrows + ncols)
+    rows = rng.integers(0, 2**64 - 1, size=(nrows, ncols), dtype=np.uint64)
+    ld = nrows + 8
+    cols = torch.zeros(ncols * ld, dtype=torch.int64, device="cuda:0")
+    stage_bytes = zkgpu.load_rows_stage_bytes(nrows, ncols, block)
+    stage = torch.empty((stage_bytes + 7) // 8, dtype=torch.int64, device="cuda:0")
+    job = zkgpu.load_rows_async(cols, ld, rows, stage, block_rows=block)
+    busy = zkgpu.merkletree(rng.integers(0, 2**63, size=(1 << 12, 8), dtype=np.uint64))  # library-stream work meanwhile
+    job.wait()
+    torch.cuda.synchronize()
+    got = zkgpu.from_device(cols).reshape(ncols, ld)[:, :nrows]
+    assert np.array_equal(got, rows.T) and busy.size
+    small = torch.empty(max(1, stage_bytes // 16), dtype=torch.int64, device="cuda:0")
+    with pytest.raises(zkgpu.ZkgpuError, match="stage"):
+        zkgpu.load_rows_async(cols, ld, rows, small, block_rows=block)
