@@ -920,10 +920,13 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     // that reads a column once and accumulates it into all of its chains.
     // Same values (the chain sum is linear; accumulators are reduced every
     // FUSE_PIECE columns).  Measured (A/B on one box): zkEVM-shaped FRI
-    // polynomial at 2^23 rows 69.4 -> 38.4 ms (proof 1.134 -> 1.104 s); the
-    // config-4 one (397 column terms, its re-reads close enough to hit the
-    // caches) 9.3 -> 10.4 ms, so only chains of ZKGPU_ZXP_JIT_FUSE_MIN (1024)
-    // column terms or more are fused.  ZKGPU_ZXP_JIT_FUSE=0 disables.
+    // polynomial at 2^23 rows 69.4 -> 38.4 ms with 4 column loads in flight
+    // per iteration, 33.5 ms with 8 (ZKGPU_ZXP_JIT_FUSE_U); the config-4 one
+    // (397 column terms) 9.3 -> 10.4 ms with 4, 8.1 ms with 8.  Small chains
+    // inside other programs (config-4 quotient, step3prev: 20-24 columns)
+    // ran slower fused, so a program is fused only when its chains hold at
+    // least half of its column terms and ZKGPU_ZXP_JIT_FUSE_MIN (128) or more
+    // -- the FRI polynomials.  ZKGPU_ZXP_JIT_FUSE=0 disables.
     constexpr int FUSE_MAX = 4;
     constexpr uint32_t FUSE_PIECE = 224;
     static const int fuse_env = [] {
@@ -932,7 +935,12 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     }();
     static const size_t fuse_min = [] {
         const char *e = getenv("ZKGPU_ZXP_JIT_FUSE_MIN");
-        return (size_t)(e ? atol(e) : 1024);
+        return (size_t)(e ? atol(e) : 128);
+    }();
+    static const size_t fuse_u = [] {  // column loads in flight per fused-loop iteration
+        const char *e = getenv("ZKGPU_ZXP_JIT_FUSE_U");
+        const long u = e ? atol(e) : 8;
+        return (size_t)(u == 2 || u == 8 || u == 16 ? u : 4);
     }();
     std::vector<int32_t> fused(in.n_instr, -1);  // chain of a fused link
     std::vector<std::vector<uint32_t>> fchains;   // links in order, per fused chain
@@ -1008,12 +1016,16 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                     const zxp_operand &o = in.opnd[tm.src];
                     in_chains[{col_slot(o.a, o.b), (int32_t)o.c}] |= 1u << g;
                 }
-        size_t shared = 0, terms = 0;
+        size_t shared = 0, terms = 0, all_terms = 0;
         for (auto &kv : in_chains) {
             shared += __builtin_popcount(kv.second) > 1;
             terms += __builtin_popcount(kv.second);
         }
-        if (cand.size() >= 2 && shared > 0 && terms >= fuse_min) {
+        for (uint32_t k = 0; k < in.n_instr; k++)  // the program's column terms
+            if (in.ins[k].op == ZXP_DOT1 || in.ins[k].op == ZXP_DOT3)
+                for (uint32_t t = in.ins[k].a; t < in.ins[k].a + in.ins[k].b; t++)
+                    all_terms += in.terms[t].src != ZXP_TERM_ONE && in.opnd[in.terms[t].src].kind == ZXP_COL;
+        if (cand.size() >= 2 && shared > 0 && terms >= fuse_min && 2 * terms >= all_terms) {
             fchains = cand;
             for (size_t g = 0; g < fchains.size(); g++)
                 for (uint32_t x : fchains[g]) {
@@ -1316,7 +1328,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             const size_t R = mem.size();
             for (size_t p0 = 0; p0 < cols.size(); p0 += FUSE_PIECE) {
                 const size_t n = std::min<size_t>(FUSE_PIECE, cols.size() - p0);
-                const size_t np = (n + 3) & ~(size_t)3;
+                const size_t np = (n + fuse_u - 1) / fuse_u * fuse_u;
                 const size_t off = zt.size();
                 for (size_t e = 0; e < np; e++) {
                     const FusedCol &fc = *cols[p0 + std::min(e, n - 1)];
@@ -1339,11 +1351,11 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                         fill[g] = 1;
                     }
                 for (int g : mem) fill[g] += (uint32_t)np;
-                appendf(body, "for (int q_ = 0; q_ < %zu; q_ += 4) {\nconst JitTerm *t_ = ZT + %zu + (size_t)q_ * %zu;\n"
-                              "uint64_t fv`[4];\n", np, off, R);
-                appendf(body, "_Pragma(\"unroll\") for (int u_ = 0; u_ < 4; u_++) fv`[u_] = gload(t_[u_ * %zu].ptr + "
-                              "((i` + (uint64_t)t_[u_ * %zu].sh) & m));\n", R, R);
-                body += "_Pragma(\"unroll\") for (int u_ = 0; u_ < 4; u_++) {\n";
+                appendf(body, "for (int q_ = 0; q_ < %zu; q_ += %zu) {\nconst JitTerm *t_ = ZT + %zu + (size_t)q_ * %zu;\n"
+                              "uint64_t fv`[%zu];\n", np, fuse_u, off, R, fuse_u);
+                appendf(body, "_Pragma(\"unroll\") for (int u_ = 0; u_ < %zu; u_++) fv`[u_] = gload(t_[u_ * %zu].ptr + "
+                              "((i` + (uint64_t)t_[u_ * %zu].sh) & m));\n", fuse_u, R, R);
+                appendf(body, "_Pragma(\"unroll\") for (int u_ = 0; u_ < %zu; u_++) {\n", fuse_u);
                 for (size_t r = 0; r < R; r++)
                     appendf(body, "F%d_0`.term(fv`[u_], t_[u_ * %zu + %zu].c[0]); F%d_1`.term(fv`[u_], t_[u_ * %zu + %zu].c[1]); "
                                   "F%d_2`.term(fv`[u_], t_[u_ * %zu + %zu].c[2]);\n",
