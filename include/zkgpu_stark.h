@@ -73,7 +73,9 @@ int zkgpu_stark_set_cm1(void *handle, const uint64_t *rows);
  * while the next zkgpu_stark_prove runs on the current cm1_n, and becomes
  * cm1_n when that prove returns.  `rows` must stay valid until then; a later
  * set_cm1 / set_cm1_async supersedes it.  Costs one more cm1_n (n x n_cm1
- * u64) of HBM.  Single-GPU prover only. */
+ * u64; a shard's rows on a sharded prover) of HBM.  On a sharded prover each
+ * rank passes the whole row-major buffer and loads its own rows, as with
+ * set_cm1. */
 int zkgpu_stark_set_cm1_async(void *handle, const uint64_t *rows);
 /* cm1_n back into a host row-major buffer (n rows x n_cm1; the inverse of
  * set_cm1).  Single-GPU prover only. */

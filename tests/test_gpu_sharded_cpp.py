@@ -115,14 +115,20 @@ def _worker(rank, world, port, q, name, shm, rows=False):
         zkgpu.init(0)
         comm = ShmComm(shm, world, rank) if shm else HostStagedComm()
         g = GpuStark(_inst(name), comm=comm)
-        if rows:  # the executor's row-major cm1 (each rank takes its rows + halo)
+        if rows == "async":  # trace A, then B queued in the background during A's proof
+            a, b = _two_traces(name)
+            g.set_cm1(a)
+            g.set_cm1_async(b)
+            proof = (g.prove(), g.prove())
+        elif rows:  # the executor's row-major cm1 (each rank takes its rows + halo)
             from oracle.stark_prover import OracleStark
             o = OracleStark(_inst(name))
             o.witness()
             g.set_cm1(o.S[0])
+            proof = g.prove()
         else:
             g.witness()
-        proof = g.prove()
+            proof = g.prove()
         q.put((rank, proof, g.timers(), None))
         g.close()
         comm.close()
@@ -131,6 +137,21 @@ def _worker(rank, world, port, q, name, shm, rows=False):
         q.put((rank, None, None, traceback.format_exc()))
     finally:
         dist.destroy_process_group()
+
+
+def _two_traces(name):
+    """the instance's witness and a second trace differing in its free
+    (unconstrained) cm1 columns"""
+    import numpy as np
+    from oracle.stark_prover import OracleStark
+    inst = _inst(name)
+    o = OracleStark(inst)
+    o.witness()
+    a = o.S[0].copy()
+    free = list(range(3 * inst.t, 3 * inst.t + inst.n_free))
+    b = a.copy()
+    b[:, free] = np.random.default_rng(1).integers(0, 2**63, size=(b.shape[0], len(free)), dtype=np.uint64)
+    return a, b
 
 
 def _free_port():
@@ -174,3 +195,41 @@ def test_sharded_multiprocess_equals_oracle(oracle_proofs, world, name, comm):
         # packed exchanges: one message per peer and direction, whatever the
         # column count (the commits of fork-9's 751 columns included)
         assert 0 < timers["COUNT_COMM_MAX_OPS"] <= 2 * (world - 1), timers["COUNT_COMM_MAX_OPS"]
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_sharded_set_cm1_async(oracle, world):
+    """Back-to-back sharded proofs with the next trace queued in the
+    background (set_cm1_async: each rank loads its rows [r0, r0 + ldn) mod N,
+    the last rank's in two pieces across the domain end): both proofs equal
+    the oracle's proofs of their traces."""
+    import multiprocessing as mp
+    import uuid
+    from oracle.stark_prover import OracleStark
+    a, b = _two_traces("lookups")
+    want = []
+    for t in (a, b):
+        o = OracleStark(_inst("lookups"))
+        o.witness()
+        o.S[0][:] = t
+        want.append(o.prove())
+    assert want[0] != want[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    shm = "/zkgpu_t_%s" % uuid.uuid4().hex[:12]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, "lookups", shm, "async")) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=240) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    errs = [e for *_, e in res if e]
+    assert not errs, errs[0]
+    for _, (pa, pb), _, _ in res:
+        _assert_same(pa, want[0])
+        _assert_same(pb, want[1])

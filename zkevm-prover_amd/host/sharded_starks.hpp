@@ -575,7 +575,23 @@ public:
     }
 
     int commit_const() override { return fail("stark (sharded): constants are committed from their whole copy"); }
-    int set_cm1_async(const uint64_t *) override { return fail("stark (sharded): set_cm1_async is single-GPU only"); }
+    // the rank's rows of the next proof's trace, loaded during this prove (as
+    // set_cm1: rows [r0, r0 + ldn) mod N, so up to two host pieces)
+    int set_cm1_async(const uint64_t *rows) override
+    {
+        if (take_cm1_async(false)) return -1;
+        const uint64_t w = info.n_cm1, first = std::min(ldn, N - r0());
+        if (cm1_next_alloc(ldn, 2)) return -1;
+        if (zkgpu_load_rows_async(cm1_next, ldn, rows + r0() * w, first, w, 0, cm1_xfer[0], xfer_bytes, &cm1_ticket[0]) ||
+            (ldn > first && zkgpu_load_rows_async(cm1_next + first, ldn, rows, ldn - first, w, 0, cm1_xfer[1], xfer_bytes,
+                                                  &cm1_ticket[1]))) {
+            cm1_pending = true;  // wait for whatever started
+            (void)take_cm1_async(false);
+            return fail("set_cm1_async: %s", zkgpu_last_error());
+        }
+        cm1_pending = true;
+        return 0;
+    }
     int get_cm1(uint64_t *) override { return fail("stark (sharded): get_cm1 is single-GPU only"); }
 
     // the executor's row-major buffer: the rank takes rows [r0, r0 + ldn) mod N
@@ -823,6 +839,13 @@ public:
     }
 
     int prove(uint64_t *out) override
+    {
+        const int rc = prove_sharded(out);
+        const int rc2 = take_cm1_async(true);  // a queued trace becomes cm1_n (set_cm1_async)
+        return rc ? rc : rc2;
+    }
+
+    int prove_sharded(uint64_t *out)
     {
         timers.clear();
         auto tall = clk::now();

@@ -174,14 +174,15 @@ public:
     uint64_t planned = 0;
 
     // background hand-off of the next proof's cm1_n (set_cm1_async)
-    uint64_t *cm1_next = nullptr, *cm1_xfer = nullptr;
+    // (up to two row pieces: a shard's rows wrap around the domain end)
+    uint64_t *cm1_next = nullptr, *cm1_xfer[2] = {nullptr, nullptr};
     uint64_t xfer_bytes = 0;
-    void *cm1_ticket = nullptr;
+    void *cm1_ticket[2] = {nullptr, nullptr};
     bool cm1_pending = false;
 
     virtual ~Starks()
     {
-        (void)zkgpu_load_wait(cm1_ticket);
+        for (void *t : cm1_ticket) (void)zkgpu_load_wait(t);
         for (void *p : allocs) zkgpu_dev_free(p);
     }
 
@@ -432,15 +433,21 @@ public:
     virtual int set_cm1_async(const uint64_t *rows)
     {
         if (take_cm1_async(false)) return -1;
-        if (!cm1_next) {
-            xfer_bytes = zkgpu_load_rows_stage_bytes(N, info.n_cm1, 0);
-            if (dalloc(&cm1_next, (uint64_t)(info.n_cm1 ? info.n_cm1 : 1) * N) ||
-                dalloc(&cm1_xfer, std::max<uint64_t>(1, xfer_bytes / 8)))
-                return -1;
-        }
-        if (zkgpu_load_rows_async(cm1_next, N, rows, N, info.n_cm1, 0, cm1_xfer, xfer_bytes, &cm1_ticket))
+        if (cm1_next_alloc(N, 1)) return -1;
+        if (zkgpu_load_rows_async(cm1_next, N, rows, N, info.n_cm1, 0, cm1_xfer[0], xfer_bytes, &cm1_ticket[0]))
             return fail("set_cm1_async: %s", zkgpu_last_error());
         cm1_pending = true;
+        return 0;
+    }
+
+    // the second cm1_n buffer (ld rows per column) and `pieces` loader stages
+    int cm1_next_alloc(uint64_t ld, int pieces)
+    {
+        if (cm1_next) return 0;
+        xfer_bytes = zkgpu_load_rows_stage_bytes(ld, info.n_cm1, 0);
+        if (dalloc(&cm1_next, (uint64_t)(info.n_cm1 ? info.n_cm1 : 1) * ld)) return -1;
+        for (int k = 0; k < pieces; k++)
+            if (dalloc(&cm1_xfer[k], std::max<uint64_t>(1, xfer_bytes / 8))) return -1;
         return 0;
     }
 
@@ -450,8 +457,12 @@ public:
     {
         if (!cm1_pending) return 0;
         cm1_pending = false;
-        const int rc = zkgpu_load_wait(cm1_ticket);
-        cm1_ticket = nullptr;
+        int rc = 0;
+        for (void *&t : cm1_ticket) {
+            const int r = zkgpu_load_wait(t);
+            t = nullptr;
+            rc = rc ? rc : r;
+        }
         if (rc) return fail("set_cm1_async: %s", zkgpu_last_error());
         if (use) std::swap(S.sec[SEC_CM1_N], cm1_next);
         return 0;
