@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <new>
 #include <thread>
 #include <vector>
 
@@ -716,9 +717,11 @@ int zkgpu_load_rows_async(uint64_t *cols, uint64_t ld, const uint64_t *rows, uin
     if (nrows && ncols && (!stage || stage_bytes < 2 * block_rows * ncols * sizeof(uint64_t)))
         return set_error(ZKGPU_ERR_ARG, "load_rows_async: stage of %llu bytes < 2 blocks (%llu)",
                          (unsigned long long)stage_bytes, (unsigned long long)(2 * block_rows * ncols * 8));
-    LoadTicket *t = new LoadTicket();
+    LoadTicket *t = new (std::nothrow) LoadTicket();
+    if (!t) return set_error(ZKGPU_ERR_OOM, "load_rows_async: ticket");
     const int device = g_ctx.device;
-    t->th = std::thread([=] {
+    try {
+        t->th = std::thread([=] {
         if (!nrows || !ncols) return;
         int r = check_hip(hipSetDevice(device), "hipSetDevice (loader)");
         hipStream_t ts = nullptr;
@@ -726,7 +729,11 @@ int zkgpu_load_rows_async(uint64_t *cols, uint64_t ld, const uint64_t *rows, uin
         if (!r) r = load_rows_streams(cols, ld, rows, nrows, ncols, block_rows, stage, ts, false);
         if (ts) (void)hipStreamDestroy(ts);
         t->rc = r;
-    });
+        });
+    } catch (...) {  // no thread: nothing started
+        delete t;
+        return set_error(ZKGPU_ERR_ARG, "load_rows_async: cannot start the loader thread");
+    }
     *ticket = t;
     return 0;
 }
