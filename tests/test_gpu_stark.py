@@ -131,6 +131,12 @@ def test_set_cm1_async_pipelined_proofs(oracle, zkgpu):
     g.set_cm1_async(traces[1])
     g.set_cm1(traces[0])
     assert g.prove() == refs[0]
+    # a queued load superseded by another queued one
+    g.set_cm1_async(traces[1])
+    g.set_cm1_async(traces[2])
+    assert g.prove() == refs[0] and g.prove() == refs[2]
+    # destroyed with a load still queued: the destructor waits for it
+    g.set_cm1_async(traces[1])
     g.close()
 
 
