@@ -215,3 +215,22 @@ def test_jit_source_compiles_for_gfx950(zkgpu_host, name):
     assert "zxp_jit" in src
     src2 = zkgpu_host.zxp_jit_source(prog, _rand(rng, (8, 3)), np.zeros(8, np.uint64), _rand(rng, ev.shape))
     assert src == src2  # same structure -> same kernel (cached per process)
+
+
+def test_fused_chains_only_for_fri_polynomials(zkgpu_host):
+    """Fused column chains (csrc/zxp_jit.hip): the zkEVM-shaped FRI polynomial
+    (three opening-point chains over 1,497 columns) prints its chains as loops
+    reading each column once; the zkEVM-shaped quotient and the stage-3
+    program (chains holding a small share of their column terms) are left
+    alone; the kernel text does not depend on the challenges."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import jit_prebuild as jp
+    ch, pub, ev = jp.consts()
+    rng = np.random.default_rng(3)
+    p52 = jp.program(1.0, "step52ns")
+    src = zkgpu_host.zxp_jit_source(p52, ch, pub, ev)
+    assert src.count("for (int q_") >= 3
+    assert src == zkgpu_host.zxp_jit_source(p52, _rand(rng, ch.shape), pub, _rand(rng, ev.shape))
+    for name in ("step3prev", "step42ns"):
+        assert "for (int q_" not in zkgpu_host.zxp_jit_source(jp.program(0.25 if name == "step42ns" else 1.0, name),
+                                                             ch, pub, ev)
