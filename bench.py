@@ -94,6 +94,7 @@ def parse():
                     help="stark workload: skip the oracle's zkEVM-shaped sample (cpu_baseline.zkevm_shaped, 2^16 rows, ~20 s)")
     ap.add_argument("--cpu-sample-bits", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_BITS", "18")))
     ap.add_argument("--cpu-sample-cols", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_COLS", "4")))
+    ap.add_argument("--rank-probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-full", action="store_true",
                     help="only time the oracle STARK prover at the full size (minutes of CPU); prints one JSON line "
                          "for profiles/*_cpu_full_stark.json")
@@ -719,7 +720,8 @@ def sharded_children(args, world, rank, local, dist, torch):
             port = int(t.item())
         env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(local), WORLD_SIZE=str(world),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        cmd = [sys.executable, os.path.abspath(__file__), "--workload", "stark-sharded", "--steps", "3", "--warmup",
+        cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--workload", "stark-sharded",
+               "--steps", "3", "--warmup",
                "1", "--no-cpu", "--log-n", str(args.log_n), "--blowup-bits", str(args.blowup_bits), "--ncols",
                str(args.ncols), "--queries", str(args.queries)] + extra  # (a later --log-n wins)
         t0 = time.time()
@@ -750,8 +752,88 @@ def sharded_children(args, world, rank, local, dist, torch):
                      "scaling": "strong", "workload": d["config"]["workload"],
                      "exchange_ms": round(sum(v for k, v in st.items() if "EXCHANGE" in k and not k.startswith("COUNT_")),
                                           3),
-                     "stages_ms": st, "wall_s": round(time.time() - t0, 1)}
+                     "stages_ms": {k: v for k, v in st.items() if not k.startswith("COUNT_COMM")},
+                     "wall_s": round(time.time() - t0, 1)}
+        if d.get("comm"):
+            out[name]["comm"] = d["comm"]
     return out if rank == 0 else None
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) started without a launcher (no WORLD_SIZE):
+    start N rank processes of this same command line -- RANK = LOCAL_RANK = i,
+    WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a free MASTER_PORT, as
+    torch.distributed.run would -- and return the exit status.  Runs before
+    anything here touches a GPU (no torch import in this process).  Rank 0's
+    stdout is this process's stdout, so its JSON line is the line.  If a rank
+    fails, the others get 60 s to finish and are then killed (a rank waiting in
+    a collective for a dead peer never returns); the first failure's status is
+    the result."""
+    import signal
+    import subprocess
+    n = args.gpus
+    port = int(os.environ.get("MASTER_PORT") or _free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+
+    def forward(sig, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(sig)
+        raise SystemExit(128 + sig)
+
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
+    status, deadline = 0, None
+    while any(p.poll() is None for p in procs):
+        for p in procs:
+            rc = p.poll()
+            if rc not in (None, 0) and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                deadline = time.time() + 60
+                sys.stderr.write("bench.py: rank %d exited with %s\n" % (procs.index(p), rc))
+        if deadline is not None and time.time() > deadline:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(0.2)
+    for i, p in enumerate(procs):
+        if p.returncode and status == 0:
+            status = p.returncode if p.returncode > 0 else 128 - p.returncode
+            sys.stderr.write("bench.py: rank %d exited with %s\n" % (i, p.returncode))
+    return status
+
+
+def world_of(args):
+    """(world, rank, local rank) this process runs as.  --gpus N must agree
+    with the world a launcher (torch.distributed.run) put it in: a driver
+    that asks for N GPUs never gets a line measured on another number."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d, but this process joined a world of %d ranks (WORLD_SIZE)"
+                         % (args.gpus, world))
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def comm_summary(stages, world):
+    """The C++ sharded prover's own account of its exchanges in the last proof
+    (COUNT_COMM_* beside its stage timers): the world its communicator was
+    created with and the bytes this rank (rank 0) sent."""
+    if "COUNT_COMM_WORLD" not in stages:
+        return None
+    n = int(stages.get("COUNT_COMM_EXCHANGES", 0))
+    sent = stages.get("COUNT_COMM_BYTES_SENT", 0.0)
+    res = {"comm_world": int(stages["COUNT_COMM_WORLD"]), "exchanges_per_proof": n,
+           "rank0_bytes_sent_per_proof": int(sent),
+           "rank0_bytes_sent_per_exchange": int(sent / n) if n else 0,
+           "rank0_largest_exchange_bytes": int(stages.get("COUNT_COMM_MAX_BYTES_SENT", 0)),
+           "max_ops_per_exchange": int(stages.get("COUNT_COMM_MAX_OPS", 0))}
+    if res["comm_world"] != world:
+        raise SystemExit("bench.py: the prover's communicator has world %d, the job %d" % (res["comm_world"], world))
+    return res
 
 
 def cpu_full_main(args):
@@ -765,13 +847,21 @@ def main():
     args = parse()
     if args.cpu_full:
         return cpu_full_main(args)
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world, rank, local = world_of(args)
+    if args.rank_probe:  # launcher check (tests/test_bench_launch.py): no GPU, no torch
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                        "MASTER_PORT")}), flush=True)
+        if os.environ.get("ZKGPU_BENCH_PROBE_FAIL") == str(rank):
+            sys.exit(3)  # the launcher's failure path
+        return
     import torch
     import torch.distributed as dist
     import zkgpu
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("nccl", init_method="env://")
     torch.cuda.set_device(local)
@@ -959,6 +1049,9 @@ def main():
             res["sharded_one_proof"] = sharded
         if replicas is not None:
             res["replicas"] = replicas
+            one = (sharded or {}).get("config4") or {}
+            if one.get("comm") and scaling == "strong":
+                res["comm"] = one["comm"]  # the headline proof's exchanges (C++ prover's count)
         if kernels is not None:
             res["kernels"] = kernel_table(kernels)
             if args.workload == "stark" and args.log_n == 23 and C == 100:
@@ -972,6 +1065,9 @@ def main():
                     res["roofline_dominant"] = dominant_roofline(inst, args, v, res["valu"])
             if args.workload in ("stark", "stark-sharded") and stages:
                 res["stages_ms"] = {k: round(v, 3) for k, v in stages.items()}
+                comm = comm_summary(stages, world)
+                if comm:
+                    res["comm"] = comm
         res["cpu_baseline"] = cpu
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -135,7 +135,10 @@ int zkgpu_load_rows_dev(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint6
  * least zkgpu_load_rows_stage_bytes bytes), so kernels on the library stream
  * -- the previous proof -- run while the trace crosses PCIe.  `rows`, `cols`
  * and `stage` stay untouched by the caller until zkgpu_load_wait(ticket)
- * returns (the load's status; the ticket is freed).  No reference
+ * returns (the load's status, and on failure the loader's message in
+ * zkgpu_last_error() of the waiting thread; the ticket is freed).  The load
+ * is ordered after everything already queued on the library stream (e.g. the
+ * zeroing of freshly allocated `cols` / `stage`).  No reference
  * counterpart: the reference's batch prover loads each trace before its
  * genProof (prover.cpp:94-116). */
 uint64_t zkgpu_load_rows_stage_bytes(uint64_t nrows, uint64_t ncols, uint64_t block_rows);

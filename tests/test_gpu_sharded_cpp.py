@@ -195,6 +195,10 @@ def test_sharded_multiprocess_equals_oracle(oracle_proofs, world, name, comm):
         # packed exchanges: one message per peer and direction, whatever the
         # column count (the commits of fork-9's 751 columns included)
         assert 0 < timers["COUNT_COMM_MAX_OPS"] <= 2 * (world - 1), timers["COUNT_COMM_MAX_OPS"]
+        # the communicator's world and this proof's exchange volume
+        assert timers["COUNT_COMM_WORLD"] == world
+        assert timers["COUNT_COMM_EXCHANGES"] > 0
+        assert timers["COUNT_COMM_BYTES_SENT"] >= timers["COUNT_COMM_MAX_BYTES_SENT"] > 0
 
 
 @pytest.mark.parametrize("world", [4, 8])

@@ -140,6 +140,40 @@ def test_set_cm1_async_pipelined_proofs(oracle, zkgpu):
     g.close()
 
 
+def test_set_cm1_async_first_load_after_queued_work(oracle, zkgpu):
+    """the first set_cm1_async allocates the second cm1 buffer and
+    the loader stage, zeroed on the library stream.  With ~0.1 s of LDE work
+    queued on that stream just before, those memsets run late; the loader's
+    copies (its own non-blocking streams) must still land after them -- the
+    queued trace is what the next proof sees."""
+    import torch
+    from oracle.stark_prover import OracleStark
+    from zkgpu.synthetic import SyntheticStark
+    from zkgpu.stark import GpuStark
+    inst = SyntheticStark(n_bits=12, t=3, m=1, n_free=60, n_queries=8)
+    free = list(range(3 * inst.t, 3 * inst.t + inst.n_free))
+    o = OracleStark(inst)
+    o.witness()
+    trace = o.S[0].copy()
+    trace[:, free] = rand_gl(np.random.default_rng(5), (o.N, len(free)))
+    o.S[0][:] = trace
+    want = o.prove()
+    g = GpuStark(inst)
+    g.witness()
+    n, C = 1 << 22, 32
+    src = torch.randint(0, 2**62, (C, n), dtype=torch.int64, device="cuda")
+    out = torch.empty((C, 2 * n), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    for _ in range(4):  # queued, not waited for
+        zkgpu.extend_pol_dev(out, 2 * n, src, n, 2 * n, n, C)
+    g.set_cm1_async(trace)
+    g.prove()  # the witness's proof; the queued trace is taken when it returns
+    assert np.array_equal(g.get_cm1(), trace)
+    assert g.prove() == want
+    g.close()
+    del src, out
+
+
 def test_lookup_value_not_in_table_fails_loudly(oracle, zkgpu):
     """An f value outside the table stops the GPU prover with the reference's
     "Number not included" error (polinomial.hpp:409-413)."""

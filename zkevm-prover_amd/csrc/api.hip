@@ -647,8 +647,13 @@ static uint64_t load_block_rows(uint64_t block_rows, uint64_t nrows, uint64_t nc
 
 // one load on its own streams (transposes on ts): the shared body of the
 // synchronous and the background loader
+// `after` (optional): an event both streams wait for before their first
+// command -- the background loader's streams are non-blocking and would
+// otherwise overtake work the caller queued on the library stream into the
+// same buffers (the zeroing memsets of freshly allocated cols / stage).
 static int load_rows_streams(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint64_t nrows, uint64_t ncols,
-                             uint64_t block_rows, uint64_t *stage, hipStream_t ts, bool register_host)
+                             uint64_t block_rows, uint64_t *stage, hipStream_t ts, bool register_host,
+                             hipEvent_t after = nullptr)
 {
     int rc = 0;
     const size_t total = nrows * ncols * sizeof(uint64_t);
@@ -665,6 +670,8 @@ static int load_rows_streams(uint64_t *cols, uint64_t ld, const uint64_t *rows, 
         rc = check_hip(hipEventCreateWithFlags(&copied[k], hipEventDisableTiming), "event");
         if (!rc) rc = check_hip(hipEventCreateWithFlags(&freed[k], hipEventDisableTiming), "event");
     }
+    if (!rc && after) rc = check_hip(hipStreamWaitEvent(cs, after, 0), "wait");
+    if (!rc && after) rc = check_hip(hipStreamWaitEvent(ts, after, 0), "wait");
     if (!rc) rc = load_rows_blocks(cols, ld, rows, nrows, ncols, block_rows, stage, cs, ts, copied, freed);
     if (!rc) rc = check_hip(hipStreamSynchronize(ts), "load_rows sync");
     if (cs) (void)hipStreamSynchronize(cs);
@@ -698,6 +705,8 @@ int zkgpu_load_rows_dev(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint6
 struct LoadTicket {
     std::thread th;
     int rc = 0;
+    hipEvent_t after = nullptr;  // the library stream's work queued before the load
+    char err[512] = "";          // the loader thread's error text (g_err is thread-local)
 };
 
 uint64_t zkgpu_load_rows_stage_bytes(uint64_t nrows, uint64_t ncols, uint64_t block_rows)
@@ -719,6 +728,14 @@ int zkgpu_load_rows_async(uint64_t *cols, uint64_t ld, const uint64_t *rows, uin
                          (unsigned long long)stage_bytes, (unsigned long long)(2 * block_rows * ncols * 8));
     LoadTicket *t = new (std::nothrow) LoadTicket();
     if (!t) return set_error(ZKGPU_ERR_OOM, "load_rows_async: ticket");
+    if (nrows && ncols) {
+        if ((rc = check_hip(hipEventCreateWithFlags(&t->after, hipEventDisableTiming), "event")) ||
+            (rc = check_hip(hipEventRecord(t->after, g_ctx.stream), "record"))) {
+            if (t->after) (void)hipEventDestroy(t->after);
+            delete t;
+            return rc;
+        }
+    }
     const int device = g_ctx.device;
     try {
         t->th = std::thread([=] {
@@ -726,11 +743,13 @@ int zkgpu_load_rows_async(uint64_t *cols, uint64_t ld, const uint64_t *rows, uin
         int r = check_hip(hipSetDevice(device), "hipSetDevice (loader)");
         hipStream_t ts = nullptr;
         if (!r) r = check_hip(hipStreamCreateWithFlags(&ts, hipStreamNonBlocking), "loader stream");
-        if (!r) r = load_rows_streams(cols, ld, rows, nrows, ncols, block_rows, stage, ts, false);
+        if (!r) r = load_rows_streams(cols, ld, rows, nrows, ncols, block_rows, stage, ts, false, t->after);
         if (ts) (void)hipStreamDestroy(ts);
+        if (r) snprintf(t->err, sizeof t->err, "%s", g_err);
         t->rc = r;
         });
     } catch (...) {  // no thread: nothing started
+        if (t->after) (void)hipEventDestroy(t->after);
         delete t;
         return set_error(ZKGPU_ERR_ARG, "load_rows_async: cannot start the loader thread");
     }
@@ -744,6 +763,8 @@ int zkgpu_load_wait(void *ticket)
     LoadTicket *t = (LoadTicket *)ticket;
     if (t->th.joinable()) t->th.join();
     const int rc = t->rc;
+    if (rc) set_error(rc, "%s", t->err);  // the loader's message, on the waiting thread
+    if (t->after) (void)hipEventDestroy(t->after);
     delete t;
     return rc;
 }

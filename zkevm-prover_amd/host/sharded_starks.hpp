@@ -67,6 +67,9 @@ public:
     uint64_t *pack_s = nullptr, *pack_r = nullptr;
     uint64_t stride_s = 0, stride_r = 0;
     uint32_t max_ops = 0;  // largest exchange so far (operations posted by this rank)
+    // this proof's exchanges: count, bytes this rank sent, the largest one's
+    // sent bytes (reported as COUNT_COMM_* beside the stage timers)
+    uint64_t n_exch = 0, sent_bytes = 0, max_sent = 0;
     uint64_t *puw = nullptr;    // one plookup's f, t, h1, h2 over the whole n domain (12 x N)
     uint64_t slot = 0, hcap = 0;
     struct Tree {
@@ -250,10 +253,23 @@ public:
     {
         if (ops.empty()) return 0;
         max_ops = std::max(max_ops, (uint32_t)ops.size());
-        if (ops.size() > 2ULL * (W - 1))
-            return fail("exchange of %zu operations: more than one send and one receive per peer", ops.size());
+        if (ops.size() > 2ULL * (W - 1)) {
+            // still enter the collective exchange, with nothing posted: the
+            // peers' receives from this rank then fail (host exchange: "sent
+            // fewer slices") instead of waiting at its barrier forever
+            const size_t n = ops.size();
+            ops.clear();
+            (void)comm.exchange(comm.ctx, ops.data(), 0);
+            return fail("exchange of %zu operations: more than one send and one receive per peer", n);
+        }
         if (comm.exchange(comm.ctx, ops.data(), (uint32_t)ops.size()))
             return fail("zkgpu_comm exchange of %zu operations failed (rank %u of %u)", ops.size(), R, W);
+        uint64_t sent = 0;
+        for (const zkgpu_comm_op &o : ops)
+            if (o.send) sent += o.bytes;
+        n_exch++;
+        sent_bytes += sent;
+        max_sent = std::max(max_sent, sent);
         ops.clear();
         return 0;
     }
@@ -848,6 +864,7 @@ public:
     int prove_sharded(uint64_t *out)
     {
         timers.clear();
+        n_exch = sent_bytes = max_sent = 0;
         auto tall = clk::now();
         Transcript tr;
         tr.put(verkey, 4);
@@ -937,7 +954,14 @@ public:
         const int rc = fri_and_queries(tr, &roots[0][0], evals, out, tall);
         // a count, not a time: the largest exchange this rank posted (every
         // exchange is at most one send and one receive per peer, 2 (W - 1))
-        if (W > 1) timers.emplace_back("COUNT_COMM_MAX_OPS", (double)max_ops);
+        // and the communicator's world and this proof's exchange volume
+        if (W > 1) {
+            timers.emplace_back("COUNT_COMM_MAX_OPS", (double)max_ops);
+            timers.emplace_back("COUNT_COMM_WORLD", (double)comm.world);
+            timers.emplace_back("COUNT_COMM_EXCHANGES", (double)n_exch);
+            timers.emplace_back("COUNT_COMM_BYTES_SENT", (double)sent_bytes);
+            timers.emplace_back("COUNT_COMM_MAX_BYTES_SENT", (double)max_sent);
+        }
         return rc;
     }
 

@@ -281,7 +281,8 @@ def load_rows_dev(cols, ld, rows, block_rows=0, register_host=False):
 class RowsLoad:
     """Background hand-off (zkgpu_load_rows_async): wait() returns once the
     columns hold the rows.  Keeps the host rows and the staging buffer alive
-    until then."""
+    until then; dropping the object without wait() waits in the finalizer
+    (the loader thread still reads `rows` and writes `cols` / `stage`)."""
 
     def __init__(self, cols, ld, rows, stage, ticket):
         self.cols, self.rows, self.stage, self.ticket = cols, rows, stage, ticket
@@ -290,6 +291,11 @@ class RowsLoad:
         if self.ticket is not None:
             t, self.ticket = self.ticket, None
             _check(lib().zkgpu_load_wait(t), "zkgpu_load_wait")
+
+    def __del__(self):
+        t, self.ticket = getattr(self, "ticket", None), None
+        if t is not None and _lib is not None:
+            _lib.zkgpu_load_wait(t)  # status dropped: nobody is left to receive it
 
 
 def load_rows_async(cols, ld, rows, stage, block_rows=0):
