@@ -186,6 +186,15 @@ uint64_t oc_gl_pow(uint64_t a, uint64_t e) { return gl_pow(a, e); }
 uint64_t oc_gl_w(unsigned n) { return gl_w(n); }
 void oc_gl3_mul(uint64_t *o, const uint64_t *a, const uint64_t *b) { gl3_mul(o, a, b); }
 void oc_gl3_inv(uint64_t *o, const uint64_t *a) { gl3_inv(o, a); }
+/* out[k] = base^k in F_p^3, k < n (the xi powers of Starks::genProof's LEv /
+   LpEv, starks.cpp:314-327) */
+void oc_powers3(uint64_t *out, const uint64_t *base, uint64_t n)
+{
+    if (n == 0) return;
+    out[0] = 1;
+    out[1] = out[2] = 0;
+    for (uint64_t k = 1; k < n; k++) gl3_mul(out + 3 * k, out + 3 * (k - 1), base);
+}
 int oc_num_threads(void) { return omp_get_max_threads(); }
 void oc_set_num_threads(int n) { omp_set_num_threads(n); }
 

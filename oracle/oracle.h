@@ -34,6 +34,7 @@ uint64_t oc_gl_inv(uint64_t a);
 uint64_t oc_gl_pow(uint64_t a, uint64_t e);
 uint64_t oc_gl_w(unsigned n);
 void oc_gl3_mul(uint64_t *o, const uint64_t *a, const uint64_t *b);
+void oc_powers3(uint64_t *out, const uint64_t *base, uint64_t n);
 void oc_gl3_inv(uint64_t *o, const uint64_t *a);
 
 /* ---- NTT family (ntt.c) ----

@@ -38,6 +38,7 @@ def lib():
             "oc_gl_pow": (u64, [u64, u64]),
             "oc_gl_w": (u64, [ctypes.c_uint]),
             "oc_gl3_mul": (None, [ptr, ptr, ptr]),
+            "oc_powers3": (None, [ptr, ptr, u64]),
             "oc_gl3_inv": (None, [ptr, ptr]),
             "oc_ntt": (None, [ptr, ptr, u64, u64, ctypes.c_int]),
             "oc_dft_naive": (None, [ptr, ptr, u64, u64, ctypes.c_int]),
@@ -72,6 +73,10 @@ def lib():
             "oc_parser_eval": (ctypes.c_int, [ctypes.c_int, ptr, u64, ptr, u64, ctypes.c_uint32, ptr, ptr,
                                               ctypes.c_void_p, ptr, u64, u64, u64, ctypes.c_uint32, ctypes.c_uint32,
                                               ptr, ptr, ptr, ptr, ptr, u64, ptr, ptr, ptr, ptr]),
+            "oc_parser_eval_rows": (ctypes.c_int, [ctypes.c_int, ptr, u64, ptr, u64, ctypes.c_uint32, ptr, ptr,
+                                                   ctypes.c_void_p, ptr, u64, u64, u64, ctypes.c_uint32,
+                                                   ctypes.c_uint32, ptr, ptr, ptr, ptr, ptr, u64, ptr, ptr, ptr, ptr,
+                                                   ptr, u64, ptr, u64]),
             "oc_evmap": (None, [ptr, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, u64, ptr,
                                 ptr, u64, ctypes.c_uint32]),
             "oc_xdivxsub": (None, [ptr, ptr, ptr, u64, ptr, u64]),
@@ -295,3 +300,26 @@ def parser_eval(parser, ops, args, sections, cpols, dom, native_dom, n_tmp1, n_t
                                 ctypes.cast(ptrs, ctypes.c_void_p), _p(cpols), cpols.shape[1], dom, native_dom,
                                 n_tmp1, n_tmp3, _p(challenges), _p(publics), _p(evals), _p(x), _p(zhinv), zhinv.size,
                                 *[_p(a) if a is not None else None for a in (xdiv, xdivw, q, f)])
+
+
+def parser_eval_rows(parser, ops, args, sections, cpols, dom, native_dom, n_tmp1, n_tmp3, challenges, publics, evals,
+                     x, zhinv, rows, rmap, xdiv=None, xdivw=None, q=None, f=None):
+    """oracle/parser.c oc_parser_eval_rows: the interpreter on the rows `rows`
+    of a dom-row domain; every row-indexed array (sections, cpols, x, xdiv,
+    xdivw, q, f) holds only the rows of `rmap` (sorted ascending), in that
+    order.  Returns the status."""
+    ops = np.ascontiguousarray(ops, np.uint64)
+    args = np.ascontiguousarray(args, np.uint64)
+    rows = np.ascontiguousarray(rows, np.uint64)
+    rmap = np.ascontiguousarray(rmap, np.uint64)
+    off = np.array([s[0] for s in sections], np.uint64)
+    stride = np.array([s[1] for s in sections], np.uint64)
+    for s in sections:
+        assert s[2].shape == (rmap.size, s[1]) and s[2].flags.c_contiguous
+    ptrs = (ctypes.c_void_p * len(sections))(*[s[2].ctypes.data for s in sections])
+    return lib().oc_parser_eval_rows(parser, _p(ops), ops.size, _p(args), args.size, len(sections), _p(off),
+                                     _p(stride), ctypes.cast(ptrs, ctypes.c_void_p), _p(cpols), cpols.shape[1], dom,
+                                     native_dom, n_tmp1, n_tmp3, _p(challenges), _p(publics), _p(evals), _p(x),
+                                     _p(zhinv), zhinv.size,
+                                     *[_p(a) if a is not None else None for a in (xdiv, xdivw, q, f)],
+                                     _p(rows), rows.size, _p(rmap), rmap.size)

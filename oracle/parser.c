@@ -41,13 +41,33 @@ typedef struct {
     uint64_t zhinv_mask;
     uint64_t *q, *f; /* dom x 3 outputs (step42ns / step52ns) */
     int err;
+    /* sampled rows (oc_parser_eval_rows): every row-indexed array holds only
+     * the rows rmap[0..nmap) (sorted), row r at index rix(r); NULL: all rows */
+    const uint64_t *rmap;
+    uint64_t nmap;
 } penv;
+
+static uint64_t rix(penv *e, uint64_t row)
+{
+    if (!e->rmap) return row;
+    uint64_t lo = 0, hi = e->nmap;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (e->rmap[mid] < row) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo == e->nmap || e->rmap[lo] != row) {
+        e->err = 5; /* a row the caller did not provide */
+        return 0;
+    }
+    return lo;
+}
 
 static uint64_t *mp(penv *e, uint64_t off, uint64_t row, uint64_t stride)
 {
     for (uint32_t k = 0; k < e->n_sec; k++)
         if (e->sec_stride[k] == stride && off >= e->sec_off[k] && off < e->sec_off[k] + stride)
-            return e->sec_ptr[k] + row * stride + (off - e->sec_off[k]);
+            return e->sec_ptr[k] + rix(e, row) * stride + (off - e->sec_off[k]);
     e->err = 1;
     static uint64_t sink[4];
     return sink;
@@ -114,12 +134,12 @@ static void st3(uint64_t *p, const uint64_t *v)
 #define PSP(o, h, m, s) mp(e, A(o), srow(e, i, A(h), A(m)), A(s)) /* pols[a_o + ((i+a_h)%a_m)*a_s] */
 #define PV(o, s) (*PP(o, s))
 #define PSV(o, h, m, s) (*PSP(o, h, m, s))
-#define KV(c) (e->cpols[i * e->numpols + A(c)])
-#define KSV(c, h, m) (e->cpols[srow(e, i, A(h), A(m)) * e->numpols + A(c)])
+#define KV(c) (e->cpols[rix(e, i) * e->numpols + A(c)])
+#define KSV(c, h, m) (e->cpols[rix(e, srow(e, i, A(h), A(m))) * e->numpols + A(c)])
 #define LV(k) (A(k))
 #define CH(k) (e->challenges + 3 * A(k))
 #define UV(k) (e->publics[A(k)])
-#define XV (e->x[i])
+#define XV (e->x[rix(e, i)])
 
 /* opcodes 0..83, shared by step2prev / step3prev / step3 / step42ns (the
  * stage-3 parsers read x_n and constPols, step42ns x_2ns and constPols2ns:
@@ -200,8 +220,8 @@ static int op_common(penv *e, uint64_t op, const uint64_t *args, uint64_t ia, ui
     case 68: m13(T3(0), XV, T3(1)); return 2;
     case 69: /* q_2ns[i] = zhInv(i) * tmp3 */
         if (!e->q) e->err = 3;
-        else m13(e->q + 3 * i, e->zhinv[i & e->zhinv_mask], T3(0));
-        if (e->q) st3(e->q + 3 * i, e->q + 3 * i);
+        else m13(e->q + 3 * rix(e, i), e->zhinv[i & e->zhinv_mask], T3(0));
+        if (e->q) st3(e->q + 3 * rix(e, i), e->q + 3 * rix(e, i));
         return 1;
     case 70: m33(T3(0), T3(2), CH(1)); return 3;
     case 71: m33(T3(0), T3(1), T3(2)); return 3;
@@ -334,8 +354,8 @@ static int op_52ns(penv *e, uint64_t op, const uint64_t *args, uint64_t ia, uint
     case 2: m33(T0, T0, v2); return 0;
     case 3: m33(T1a, T0, v1); return 0;
     case 4: m33(T0, T2, v2); return 0;
-    case 5: m33(T0, T0, e->xdiv + 3 * i); return 0;
-    case 6: m33(T0, T0, e->xdivw + 3 * i); return 0;
+    case 5: m33(T0, T0, e->xdiv + 3 * rix(e, i)); return 0;
+    case 6: m33(T0, T0, e->xdivw + 3 * rix(e, i)); return 0;
     case 7: a33(T0, T0, T2); return 0;
     case 8: a33(T0, T1a, T0); return 0;
     case 9: a33(T0, T0, PP(0, 1)); return 2;
@@ -343,8 +363,8 @@ static int op_52ns(penv *e, uint64_t op, const uint64_t *args, uint64_t ia, uint
     case 11: s13(T2, PV(0, 1), ev + 3 * A(2)); return 3;
     case 12: s33(T2, PP(0, 1), ev + 3 * A(2)); return 3;
     case 13: s13(T2, KV(0), ev + 3 * A(1)); return 2;
-    case 14: s13(T0, e->cpols[i * e->numpols + 5], ev); return 0;
-    case 15: st3(e->f + 3 * i, T0); return 0;
+    case 14: s13(T0, e->cpols[rix(e, i) * e->numpols + 5], ev); return 0;
+    case 15: st3(e->f + 3 * rix(e, i), T0); return 0;
     case 16: m33(T0, T0, v1); a13(T0, PV(0, 1), T0); return 2;
     case 17: m33(T0, T0, v1); a33(T0, T0, PP(0, 1)); return 2;
     case 18: m33(T0, T0, v2); s13(T2, PV(0, 1), ev + 3 * A(2)); a33(T0, T0, T2); return 3;
@@ -355,28 +375,30 @@ static int op_52ns(penv *e, uint64_t op, const uint64_t *args, uint64_t ia, uint
     }
 }
 
-/* parser: 0 step2prev, 1 step3prev, 2 step3, 3 step42ns, 4 step52ns.
- * Returns 0, or -1 (unknown opcode / argument overrun), -2 (an access outside
- * the given sections), -3 (a shifted access whose modulus is not native_dom),
- * -4 (q_2ns store without an output). */
-int oc_parser_eval(int parser, const uint64_t *ops, uint64_t n_ops, const uint64_t *args, uint64_t n_args,
-                   uint32_t n_sec, const uint64_t *sec_off, const uint64_t *sec_stride, uint64_t *const *sec_ptr,
-                   const uint64_t *cpols, uint64_t numpols, uint64_t dom, uint64_t native_dom, uint32_t n_tmp1,
-                   uint32_t n_tmp3, const uint64_t *challenges, const uint64_t *publics, const uint64_t *evals,
-                   const uint64_t *x, const uint64_t *zhinv, uint64_t zhinv_size, const uint64_t *xdiv,
-                   const uint64_t *xdivw, uint64_t *q, uint64_t *f)
+/* the shared row loop: rows[0..n_rows) of the dom-row domain, or every row
+ * (rows NULL); rmap / nmap as in penv */
+static int parser_run(int parser, const uint64_t *ops, uint64_t n_ops, const uint64_t *args, uint64_t n_args,
+                      uint32_t n_sec, const uint64_t *sec_off, const uint64_t *sec_stride, uint64_t *const *sec_ptr,
+                      const uint64_t *cpols, uint64_t numpols, uint64_t dom, uint64_t native_dom, uint32_t n_tmp1,
+                      uint32_t n_tmp3, const uint64_t *challenges, const uint64_t *publics, const uint64_t *evals,
+                      const uint64_t *x, const uint64_t *zhinv, uint64_t zhinv_size, const uint64_t *xdiv,
+                      const uint64_t *xdivw, uint64_t *q, uint64_t *f, const uint64_t *rows, uint64_t n_rows,
+                      const uint64_t *rmap, uint64_t nmap)
 {
     int status = 0;
+    const uint64_t n_iter = rows ? n_rows : dom;
 #pragma omp parallel
     {
         penv e = {n_sec,  sec_off, sec_stride, sec_ptr, cpols, numpols, dom,   native_dom, challenges, publics, evals,
-                  x,      zhinv,   xdiv,       xdivw,   zhinv_size ? zhinv_size - 1 : 0,  q,     f,          0};
+                  x,      zhinv,   xdiv,       xdivw,   zhinv_size ? zhinv_size - 1 : 0,  q,     f,          0,
+                  rmap,   nmap};
         uint64_t *t1 = (uint64_t *)calloc(n_tmp1 + 1, 8);
         uint64_t *t3 = (uint64_t *)calloc(3 * (uint64_t)n_tmp3 + 9, 8);
         int bad = 0;
 #pragma omp for schedule(static)
-        for (uint64_t i = 0; i < dom; i++) {
+        for (uint64_t it = 0; it < n_iter; it++) {
             if (bad) continue;
+            const uint64_t i = rows ? rows[it] : it;
             uint64_t ia = 0;
             if (parser == 4) memset(t3, 0, 9 * 8); /* step52ns: tmp2 = 0 per row (tmp0/1 set before use) */
             for (uint64_t k = 0; k < n_ops && !bad; k++) {
@@ -393,7 +415,7 @@ int oc_parser_eval(int parser, const uint64_t *ops, uint64_t n_ops, const uint64
                 if (ia > n_args) bad = -1;
             }
             if (!bad && ia != n_args) bad = -1;
-            if (!bad && e.err) bad = e.err == 1 ? -2 : e.err == 2 ? -3 : -4;
+            if (!bad && e.err) bad = e.err == 1 ? -2 : e.err == 2 ? -3 : e.err == 5 ? -5 : -4;
         }
 #pragma omp critical
         if (bad && !status) status = bad;
@@ -401,4 +423,42 @@ int oc_parser_eval(int parser, const uint64_t *ops, uint64_t n_ops, const uint64
         free(t3);
     }
     return status;
+}
+
+/* parser: 0 step2prev, 1 step3prev, 2 step3, 3 step42ns, 4 step52ns.
+ * Returns 0, or -1 (unknown opcode / argument overrun), -2 (an access outside
+ * the given sections), -3 (a shifted access whose modulus is not native_dom),
+ * -4 (q_2ns store without an output). */
+int oc_parser_eval(int parser, const uint64_t *ops, uint64_t n_ops, const uint64_t *args, uint64_t n_args,
+                   uint32_t n_sec, const uint64_t *sec_off, const uint64_t *sec_stride, uint64_t *const *sec_ptr,
+                   const uint64_t *cpols, uint64_t numpols, uint64_t dom, uint64_t native_dom, uint32_t n_tmp1,
+                   uint32_t n_tmp3, const uint64_t *challenges, const uint64_t *publics, const uint64_t *evals,
+                   const uint64_t *x, const uint64_t *zhinv, uint64_t zhinv_size, const uint64_t *xdiv,
+                   const uint64_t *xdivw, uint64_t *q, uint64_t *f)
+{
+    return parser_run(parser, ops, n_ops, args, n_args, n_sec, sec_off, sec_stride, sec_ptr, cpols, numpols, dom,
+                      native_dom, n_tmp1, n_tmp3, challenges, publics, evals, x, zhinv, zhinv_size, xdiv, xdivw, q, f,
+                      NULL, 0, NULL, 0);
+}
+
+/* The same interpreter on sampled rows of a dom-row domain too large to hold
+ * on the host: rows[0..n_rows) are evaluated (row indices of the whole
+ * domain: shifts wrap mod dom, zhInv by the true row), and every row-indexed
+ * input and output -- the sections, constant pols, x, xDivXSub, q / f --
+ * holds only the rows rmap[0..nmap) (sorted ascending, every evaluated row and
+ * every row a shifted access reaches), row r at its index in rmap.  Returns
+ * as oc_parser_eval, or -5 (an access to a row missing from rmap). */
+int oc_parser_eval_rows(int parser, const uint64_t *ops, uint64_t n_ops, const uint64_t *args, uint64_t n_args,
+                        uint32_t n_sec, const uint64_t *sec_off, const uint64_t *sec_stride, uint64_t *const *sec_ptr,
+                        const uint64_t *cpols, uint64_t numpols, uint64_t dom, uint64_t native_dom, uint32_t n_tmp1,
+                        uint32_t n_tmp3, const uint64_t *challenges, const uint64_t *publics, const uint64_t *evals,
+                        const uint64_t *x, const uint64_t *zhinv, uint64_t zhinv_size, const uint64_t *xdiv,
+                        const uint64_t *xdivw, uint64_t *q, uint64_t *f, const uint64_t *rows, uint64_t n_rows,
+                        const uint64_t *rmap, uint64_t nmap)
+{
+    for (uint64_t k = 1; k < nmap; k++)
+        if (rmap[k] <= rmap[k - 1]) return -6; /* rmap must be strictly ascending */
+    return parser_run(parser, ops, n_ops, args, n_args, n_sec, sec_off, sec_stride, sec_ptr, cpols, numpols, dom,
+                      native_dom, n_tmp1, n_tmp3, challenges, publics, evals, x, zhinv, zhinv_size, xdiv, xdivw, q, f,
+                      rows, n_rows, rmap, nmap);
 }

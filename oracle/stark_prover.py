@@ -175,11 +175,7 @@ class OracleStark:
 
     def _powers3(self, base, n):
         out = np.zeros((n, 3), np.uint64)
-        out[0] = [1, 0, 0]
-        cur = np.array([1, 0, 0], np.uint64)
-        for k in range(1, n):
-            cur = oc.gl3_mul(cur, base)
-            out[k] = cur
+        oc.lib().oc_powers3(_p(out), _p(np.ascontiguousarray(base, dtype=np.uint64)), n)
         return out
 
     def evmap(self, lev, lpev):
