@@ -159,6 +159,14 @@ int zkgpu_gl_merkle_open_dev(uint64_t *vals_out, uint64_t *sibs_out, const uint6
  * special_x: host pointer to 3 u64; shift_inv: polShiftInv of this step. */
 int zkgpu_fri_fold_dev(uint64_t *out, const uint64_t *pol, uint32_t pol_bits, uint32_t out_bits,
                        const uint64_t special_x[3], uint64_t shift_inv);
+/* The same fold for output groups [g0, g0 + ngroups) only, reading those
+ * groups' getTransposed rows (row g - g0 = the 2^(pol_bits - out_bits)
+ * elements pol[g + i 2^out_bits], 3 u64 each: the layout
+ * zkgpu_fri_transpose_dev writes with transpose_bits = out_bits); out gets
+ * the ngroups folded elements.  The row-sharded prover's first fold, each
+ * rank on its block of groups (friProve.cpp:44-108 restricted to g). */
+int zkgpu_fri_fold_rows_dev(uint64_t *out, const uint64_t *rows, uint64_t g0, uint64_t ngroups, uint32_t pol_bits,
+                            uint32_t out_bits, const uint64_t special_x[3], uint64_t shift_inv);
 /* FRIProve::getTransposed (friProve.cpp:252-270), ext elements, device */
 int zkgpu_fri_transpose_dev(uint64_t *aux, const uint64_t *pol, uint64_t degree, uint32_t transpose_bits);
 

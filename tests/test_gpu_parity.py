@@ -158,6 +158,25 @@ def test_fri_fold_vs_oracle(oracle, zkgpu, pol_bits, out_bits):
     assert np.array_equal(zkgpu.from_device(dout), oracle.fri_fold(pol, pol_bits, out_bits, sx, sinv))
 
 
+@pytest.mark.parametrize("pol_bits,out_bits,g0,ng", [(12, 8, 64, 64), (16, 12, 0, 512), (11, 7, 96, 32), (10, 5, 31, 1)])
+def test_fri_fold_rows_vs_oracle(oracle, zkgpu, pol_bits, out_bits, g0, ng):
+    """zkgpu_fri_fold_rows_dev (the sharded prover's first fold): groups
+    [g0, g0 + ng) from their getTransposed rows == those outputs of the
+    oracle's whole fold"""
+    import torch
+    rng = np.random.default_rng(pol_bits * 7 + g0)
+    pol = rand_gl(rng, 3 << pol_bits)
+    sx = rand_gl(rng, 3)
+    sinv = oracle.gl_pow(oracle.gl_inv(7), 1 << (pol_bits % 5))
+    kk = 1 << (pol_bits - out_bits)
+    rows = oracle.fri_get_transposed(pol, out_bits).reshape(1 << out_bits, 3 * kk)[g0:g0 + ng]
+    dout = torch.zeros(3 * ng, dtype=torch.int64, device="cuda:0")
+    zkgpu.fri_fold_rows_dev(dout, zkgpu.to_device(np.ascontiguousarray(rows)), g0, ng, pol_bits, out_bits, sx, sinv)
+    torch.cuda.synchronize()
+    want = oracle.fri_fold(pol, pol_bits, out_bits, sx, sinv).reshape(-1, 3)[g0:g0 + ng]
+    assert np.array_equal(zkgpu.from_device(dout).reshape(-1, 3), want)
+
+
 def test_fri_transpose(oracle, zkgpu):
     import torch
     rng = np.random.default_rng(23)

@@ -25,6 +25,11 @@ INSTANCES = {
     # the fork-9 widths with the five zkEVM-shaped expression programs in the
     # stage slots (zkgpu/zkevm_shaped.py): configs[4]'s programs
     "zkevm": dict(zkevm=True, n_bits=10),
+    # FRI layer 1 + first fold over the ranks (host/sharded_starks.hpp
+    # fri_transpose_layer): four layers; and a first reduction of 4 (kk = 4),
+    # which splits over 2 / 4 ranks but not over 8 (the replicated fold)
+    "fri4": dict(n_bits=10, t=3, m=2, n_free=2, n_lookups=1, n_queries=8, fri_steps=[11, 7, 4, 2]),
+    "fri_kk4": dict(n_bits=9, t=3, m=1, n_lookups=1, n_queries=8, fri_steps=[10, 8, 5]),
 }
 
 
@@ -165,7 +170,8 @@ def _free_port():
 @pytest.mark.parametrize("world,name,comm", [(2, "lookups", "gloo"), (4, "lookups", "gloo"), (2, "blowup4", "gloo"),
                                              (2, "lookups", "shm"), (4, "blowup4", "shm"), (8, "lookups", "shm"),
                                              (2, "fork9", "gloo"), (8, "fork9", "shm"), (4, "lookups", "shm-rows"),
-                                             (2, "zkevm", "shm"), (8, "zkevm", "shm")])
+                                             (2, "zkevm", "shm"), (8, "zkevm", "shm"), (2, "fri4", "shm"),
+                                             (8, "fri4", "shm"), (4, "fri_kk4", "shm"), (8, "fri_kk4", "shm")])
 def test_sharded_multiprocess_equals_oracle(oracle_proofs, world, name, comm):
     """gloo = HostStagedComm (Python, torch.distributed); shm = ShmComm
     (host/comm_host.hpp, shared memory + process-shared barriers); -rows: the

@@ -1503,6 +1503,14 @@ int zkgpu_fri_fold_dev(uint64_t *out, const uint64_t *pol, uint32_t pol_bits, ui
     return fri_fold(out, pol, pol_bits, out_bits, special_x, shift_inv, g_ctx.stream);
 }
 
+int zkgpu_fri_fold_rows_dev(uint64_t *out, const uint64_t *rows, uint64_t g0, uint64_t ngroups, uint32_t pol_bits,
+                            uint32_t out_bits, const uint64_t special_x[3], uint64_t shift_inv)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    return fri_fold_rows(out, rows, g0, ngroups, pol_bits, out_bits, special_x, shift_inv, g_ctx.stream);
+}
+
 int zkgpu_fri_transpose_dev(uint64_t *aux, const uint64_t *pol, uint64_t degree, uint32_t transpose_bits)
 {
     int rc;

@@ -81,6 +81,8 @@ int merkle_open_cols(uint64_t *vals, uint64_t *sibs, const uint64_t *nodes, cons
 // ---- fri.hip
 int fri_fold(uint64_t *out, const uint64_t *pol, uint32_t pol_bits, uint32_t out_bits, const uint64_t sx[3],
              uint64_t shift_inv, hipStream_t s);
+int fri_fold_rows(uint64_t *out, const uint64_t *rows, uint64_t g0, uint64_t n_local, uint32_t pol_bits,
+                  uint32_t out_bits, const uint64_t sx[3], uint64_t shift_inv, hipStream_t s);
 int fri_transpose(uint64_t *aux, const uint64_t *pol, uint64_t degree, uint32_t tbits, hipStream_t s);
 
 // ---- stark.hip

@@ -34,9 +34,13 @@
 //       (starks.cpp:255-296) run on every rank, each commits its rows.
 //   stage 5  LEv / LpEv (closed form) and evmap on the rank's n-domain rows,
 //       partial sums all-gathered and added mod p; xDivXSub and the FRI
-//       program on the rank's 2n rows, f gathered.
-//   FRI      folds on every rank (2n x 3 elements); a layer tree whose
-//       groups split into W blocks is row-sharded like the commits.
+//       program on the rank's 2n rows.
+//   FRI      layer 1 and the first fold over the ranks: one all-to-all
+//       gives each rank all elements of its block of layer-1 groups (tree rows
+//       and fold input, fri_transpose_layer), the folded 2^steps[1] elements
+//       are all-gathered; the later folds (<= 1/16 of f) on every rank; a
+//       layer tree whose groups split into W blocks is row-sharded like the
+//       commits.
 //   queries  each s0 opening by the rank owning its row (subtree siblings +
 //       top levels), all-gathered.
 // The constants are set up once (build / load, untimed) on a transient whole
@@ -701,6 +705,63 @@ public:
 
     bool fri_sharded(uint64_t ngroups) const { return W > 1 && ngroups % W == 0 && ngroups / W >= 2; }
 
+    // ---- FRI's first layer over the ranks (friProve.cpp:44-133)
+    // Layer 1's group g < w = 2^steps[1] holds the kk = 2^(steps[0] - steps[1])
+    // elements f[g + k w], and the first fold maps exactly those to folded
+    // element g.  Rank R's f rows [R B, (R+1) B) are k in [R kk/W, (R+1) kk/W)
+    // of every group, so ONE all-to-all (rank s sends d its kk/W chunks of d's
+    // bl = w / W groups, 3 columns: 3 NE / W^2 words per peer) leaves each rank
+    // all kk elements of its bl groups: its block of layer 1's tree rows
+    // (getTransposed) and the input of its block of the first fold.  The fold
+    // output (1/kk of f) is then all-gathered and the later, smaller layers run
+    // as before.  Replaces the all-gather of f (3 NE words to every rank) and
+    // the fold of the whole 2^steps[0] domain on every rank.
+    bool fri_first_sharded() const
+    {
+        if (W == 1 || fri_steps.size() < 2) return false;
+        const uint64_t w = 1ULL << fri_steps[1], kk = 1ULL << (fri_steps[0] - fri_steps[1]);
+        return kk % W == 0 && fri_sharded(w);
+    }
+
+    int fri_transpose_layer(size_t si, uint64_t *aux, const uint64_t *pol, uint64_t degree, uint32_t nb) override
+    {
+        if (si != 0 || !fri_first_sharded()) return Starks::fri_transpose_layer(si, aux, pol, degree, nb);
+        const uint64_t w = 1ULL << nb, kk = NE / w, kw = kk / W, bl = w / W, msg = 3 * kw * bl;
+        const uint64_t *f = S.sec[SEC_F_2NS];  // the rank's f rows: 3 columns, ld B
+        // one message per peer, column-major bl x 3 kw (column 3 kc + c: chunk
+        // kc, component c); the rank's own lands straight in gath
+        for (uint32_t d = 0; d < W; d++) {
+            uint64_t *m = d == R ? gath + (uint64_t)R * msg : pack_s + d * stride_s;
+            for (uint64_t kc = 0; kc < kw; kc++)
+                CK(zkgpu_copy_rows_dev(m + kc * 3 * bl, bl, 0, nullptr, f + kc * w + (uint64_t)d * bl, B, 0, 0, nullptr,
+                                       3, bl));
+            if (d != R) op(d, 1, m, msg * 8);
+        }
+        for (uint32_t s = 0; s < W; s++)
+            if (s != R) op(s, 0, gath + (uint64_t)s * msg, msg * 8);
+        if (exchange()) return -1;
+        // gath is now a column-major bl x 3 kk matrix, column 3 k + c = element
+        // k (from rank k / kw), component c: the row-major transpose is the
+        // groups' getTransposed rows
+        CK(zkgpu_cols_to_rows_dev(aux + (uint64_t)R * bl * 3 * kk, gath, bl, bl, 3 * kk));
+        return 0;
+    }
+
+    int fri_fold_step(size_t si, uint64_t *dst, const uint64_t *src, uint32_t pol_bits, uint32_t out_bits,
+                      const uint64_t sx[3], uint64_t shift_inv) override
+    {
+        if (si != 1 || !fri_first_sharded())
+            return Starks::fri_fold_step(si, dst, src, pol_bits, out_bits, sx, shift_inv);
+        const uint64_t w = 1ULL << out_bits, bl = w / W, kk = 1ULL << (pol_bits - out_bits);
+        CK(zkgpu_fri_fold_rows_dev(dst + 3ULL * R * bl, fri_aux[1] + (uint64_t)R * bl * 3 * kk, (uint64_t)R * bl, bl,
+                                   pol_bits, out_bits, sx, shift_inv));
+        for (uint32_t d = 0; d < W; d++)
+            if (d != R) op(d, 1, dst + 3ULL * R * bl, 3 * bl * 8);
+        for (uint32_t s = 0; s < W; s++)
+            if (s != R) op(s, 0, dst + 3ULL * s * bl, 3 * bl * 8);
+        return exchange();
+    }
+
     // FRI layer tree: each rank hashes its block of groups (friProve.cpp:125-133)
     int fri_commit(size_t si, uint64_t ngroups, uint64_t width, uint64_t root[4]) override
     {
@@ -948,8 +1009,10 @@ public:
         tstart();
         const uint64_t xo = 3ULL * R * B;  // xdiv rows are interleaved F_p^3
         if (run_block(step52ns, ch, evals.data(), info.n_ev, xdiv + xo, xdivw + xo)) return -1;
-        if (gather_rows(S.sec[SEC_F_2NS], gath)) return -1;
-        CK(zkgpu_cols3_to_interleaved_dev(fri_pol[0], gath, NE, NE));
+        if (!fri_first_sharded()) {  // else f stays in row blocks (fri_transpose_layer)
+            if (gather_rows(S.sec[SEC_F_2NS], gath)) return -1;
+            CK(zkgpu_cols3_to_interleaved_dev(fri_pol[0], gath, NE, NE));
+        }
         if (tstop("STARK_STEP_5_CALCULATE_EXPS")) return -1;
         const int rc = fri_and_queries(tr, &roots[0][0], evals, out, tall);
         // a count, not a time: the largest exchange this rank posted (every

@@ -751,14 +751,14 @@ public:
             uint64_t sx[3];
             tr.get_field(sx);
             if (si > 0) {
-                CK(zkgpu_fri_fold_dev(fri_pol[cur ^ 1], fri_pol[cur], pol_bits, fri_steps[si], sx, shift_inv));
+                if (fri_fold_step(si, fri_pol[cur ^ 1], fri_pol[cur], pol_bits, fri_steps[si], sx, shift_inv)) return -1;
                 cur ^= 1;
             }
             if (si < fri_steps.size() - 1) {
                 uint32_t nb = fri_steps[si + 1];
                 uint64_t ngroups = 1ULL << nb;
                 uint64_t width = (3ULL << fri_steps[si]) / ngroups;
-                CK(zkgpu_fri_transpose_dev(fri_aux[si + 1], fri_pol[cur], 1ULL << fri_steps[si], nb));
+                if (fri_transpose_layer(si, fri_aux[si + 1], fri_pol[cur], 1ULL << fri_steps[si], nb)) return -1;
                 if (fri_commit(si + 1, ngroups, width, &fri_roots[4 * (si + 1)])) return -1;
                 tr.put(&fri_roots[4 * (si + 1)], 4);
             } else {
@@ -800,6 +800,22 @@ public:
         return 0;
     }
 
+    // fold step si: 2^pol_bits -> 2^out_bits elements (friProve.cpp:44-108)
+    virtual int fri_fold_step(size_t si, uint64_t *dst, const uint64_t *src, uint32_t pol_bits, uint32_t out_bits,
+                              const uint64_t sx[3], uint64_t shift_inv)
+    {
+        (void)si;
+        CK(zkgpu_fri_fold_dev(dst, src, pol_bits, out_bits, sx, shift_inv));
+        return 0;
+    }
+    // layer si + 1's tree rows: getTransposed of the 2^pol_bits-element
+    // polynomial of step si into 2^nb groups (friProve.cpp:111-121)
+    virtual int fri_transpose_layer(size_t si, uint64_t *aux, const uint64_t *pol, uint64_t degree, uint32_t nb)
+    {
+        (void)si;
+        CK(zkgpu_fri_transpose_dev(aux, pol, degree, nb));
+        return 0;
+    }
     // FRI layer si's tree over its ngroups x width row-major groups (friProve.cpp:125-133)
     virtual int fri_commit(size_t si, uint64_t ngroups, uint64_t width, uint64_t root[4])
     {

@@ -68,6 +68,7 @@ _SIGS = {
     "zkgpu_gl_merkletree_rows_dev": (ctypes.c_int, [vp, vp, u64, u64]),
     "zkgpu_gl_merkle_open_dev": (ctypes.c_int, [vp, vp, vp, vp, u64, u64, u64, vp, u64]),
     "zkgpu_fri_fold_dev": (ctypes.c_int, [vp, vp, u32, u32, vp, u64]),
+    "zkgpu_fri_fold_rows_dev": (ctypes.c_int, [vp, vp, u64, u64, u32, u32, vp, u64]),
     "zkgpu_fri_transpose_dev": (ctypes.c_int, [vp, vp, u64, u32]),
     "zkgpu_gl_field_selftest_dev": (ctypes.c_int, [vp, vp, vp, u64, ctypes.c_int]),
     "zkgpu_gl_field_selftest_rb_dev": (ctypes.c_int, [vp, vp, vp, vp, u64, ctypes.c_int, ctypes.c_int]),
@@ -359,6 +360,13 @@ def fri_fold_dev(out, pol, pol_bits, out_bits, special_x, shift_inv):
     sx = _np(special_x)
     _check(lib().zkgpu_fri_fold_dev(_addr(out), _addr(pol), pol_bits, out_bits, sx.ctypes.data, shift_inv),
            "zkgpu_fri_fold_dev")
+
+
+def fri_fold_rows_dev(out, rows, g0, ngroups, pol_bits, out_bits, special_x, shift_inv):
+    """the fold for output groups [g0, g0 + ngroups) from their getTransposed rows"""
+    sx = _np(special_x)
+    _check(lib().zkgpu_fri_fold_rows_dev(_addr(out), _addr(rows), g0, ngroups, pol_bits, out_bits, sx.ctypes.data,
+                                         shift_inv), "zkgpu_fri_fold_rows_dev")
 
 
 def fri_transpose_dev(aux, pol, degree, transpose_bits):
