@@ -170,6 +170,39 @@ int zkgpu_fri_fold_rows_dev(uint64_t *out, const uint64_t *rows, uint64_t g0, ui
 /* FRIProve::getTransposed (friProve.cpp:252-270), ext elements, device */
 int zkgpu_fri_transpose_dev(uint64_t *aux, const uint64_t *pol, uint64_t degree, uint32_t transpose_bits);
 
+/* ---- calculateH1H2 over row-sharded f / t --------------------------------
+ * Polinomial::calculateH1H2_opt1/opt3 (polinomial.hpp:349-583, starks.cpp:
+ * 104-127) when W ranks each hold rows [row0, row0 + nrows) of f and t (the
+ * row-sharded prover, host/sharded_starks.hpp; the same h1 / h2 as
+ * zkgpu_h1h2_dev on the whole columns).  Records are 5 u64 {k0, k1, k2,
+ * global row, val}: a rank's distinct t keys (largest row, val = ~0) and f
+ * keys (smallest row, val = count), each sent to the rank owning its key.
+ *   route:  dedupe the rank's rows, write the records bucketed by owner into
+ *           recs (owner order, t records first in each bucket; at most cap
+ *           records), n_t / n_f (host, world entries) = the bucket sizes
+ *   owner:  over every record this rank owns (all ranks' buckets for it,
+ *           concatenated, each t-first): ret[k] = the f count summed over the
+ *           ranks for t record k if its row is the key's largest, else 0;
+ *           missing_row = the smallest f row whose key has no t row (~0 if
+ *           none: the reference's "Number not included")
+ *   counts: the sender, ret aligned with its own recs (nsent records):
+ *           cnt[j] = 1 + ret of row j's record, start = exclusive scan of cnt
+ *           (the rank's multiset positions, relative); total (host) = sum
+ *   deal:   seg[c * seg_ld + start[j] + m] = t[c * t_ld + j], m < cnt[j]
+ *   place:  buf holds multiset positions [pos0, pos0 + len) (column c at
+ *           buf + c * buf_ld): even positions p to h1, odd to h2, at local
+ *           row p / 2 - row0. */
+int zkgpu_h1h2_shard_route(uint64_t *recs, uint64_t cap, uint32_t *n_t, uint32_t *n_f, const uint64_t *f,
+                           uint64_t f_ld, const uint64_t *t, uint64_t t_ld, uint64_t nrows, uint64_t row0, uint32_t dim,
+                           uint32_t world);
+int zkgpu_h1h2_shard_owner(uint64_t *ret, const uint64_t *recs, uint64_t nrec, uint32_t dim, uint64_t *missing_row);
+int zkgpu_h1h2_shard_counts(uint32_t *start, uint32_t *cnt, uint64_t *total, const uint64_t *sent, const uint64_t *ret,
+                            uint64_t nsent, uint64_t nrows, uint64_t row0);
+int zkgpu_h1h2_shard_deal(uint64_t *seg, uint64_t seg_ld, const uint64_t *t, uint64_t t_ld, const uint32_t *start,
+                          const uint32_t *cnt, uint64_t nrows, uint32_t dim);
+int zkgpu_h1h2_shard_place(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint64_t *buf,
+                           uint64_t buf_ld, uint64_t pos0, uint64_t len, uint64_t row0, uint32_t dim);
+
 /* ---- device memory (the host orchestrator owns HBM through these) -------- */
 int zkgpu_dev_malloc(void **ptr, uint64_t bytes);
 /* free / total HBM of the bound device (hipMemGetInfo) */

@@ -125,6 +125,14 @@ def _worker(rank, world, port, q, name, shm, rows=False):
             g.set_cm1(a)
             g.set_cm1_async(b)
             proof = (g.prove(), g.prove())
+        elif rows == "missing":  # an f value outside its table: every rank must fail, naming the row
+            from oracle.stark_prover import OracleStark
+            o = OracleStark(_inst(name))
+            o.witness()
+            r = o.S[0].copy()
+            r[9, _inst(name).cm1_lk[2]] = 12345
+            g.set_cm1(r)
+            proof = g.prove()
         elif rows:  # the executor's row-major cm1 (each rank takes its rows + halo)
             from oracle.stark_prover import OracleStark
             o = OracleStark(_inst(name))
@@ -243,3 +251,28 @@ def test_sharded_set_cm1_async(oracle, world):
     for _, (pa, pb), _, _ in res:
         _assert_same(pa, want[0])
         _assert_same(pb, want[1])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_lookup_value_not_in_table(oracle, world):
+    """calculateH1H2 over the ranks (h1h2_sharded): an f value that is in no
+    table row stops EVERY rank with the reference's error and the f row
+    (polinomial.hpp:409-413), as on one GPU (test_gpu_stark.py)"""
+    import multiprocessing as mp
+    import uuid
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    shm = "/zkgpu_t_%s" % uuid.uuid4().hex[:12]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, "lookups", shm, "missing")) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=240) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for _, proof, _, err in res:
+        assert proof is None and err and "Number not included: w=9" in err, err

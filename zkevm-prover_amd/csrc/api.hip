@@ -1465,6 +1465,61 @@ int zkgpu_h1h2_dev(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, c
     return h1h2(h1, h1_ld, h2, h2_ld, f, f_ld, t, t_ld, n, dim, missing_row, g_ctx.stream);
 }
 
+// ---- calculateH1H2 over row-sharded f / t (include/zkgpu.h)
+static int h1h2_shard_args(uint32_t dim, uint64_t n)
+{
+    if (dim != 1 && dim != 3) return set_error(ZKGPU_ERR_ARG, "h1h2 (sharded): dim must be 1 or 3");
+    if (n > 0x7FFFFFFFULL) return set_error(ZKGPU_ERR_ARG, "h1h2 (sharded): n too large");
+    return 0;
+}
+
+int zkgpu_h1h2_shard_route(uint64_t *recs, uint64_t cap, uint32_t *n_t, uint32_t *n_f, const uint64_t *f,
+                           uint64_t f_ld, const uint64_t *t, uint64_t t_ld, uint64_t nrows, uint64_t row0, uint32_t dim,
+                           uint32_t world)
+{
+    int rc;
+    if ((rc = require_init()) || (rc = h1h2_shard_args(dim, nrows))) return rc;
+    if (!world || !nrows) return set_error(ZKGPU_ERR_ARG, "h1h2 (sharded): empty world or block");
+    if (f_ld < nrows || t_ld < nrows) return set_error(ZKGPU_ERR_ARG, "h1h2 (sharded): ld < nrows");
+    if (row0 + nrows > 0xFFFFFFFFULL) return set_error(ZKGPU_ERR_ARG, "h1h2 (sharded): rows beyond 2^32");
+    return h1h2_shard_route(recs, cap, n_t, n_f, f, f_ld, t, t_ld, nrows, row0, dim, world, g_ctx.stream);
+}
+
+int zkgpu_h1h2_shard_owner(uint64_t *ret, const uint64_t *recs, uint64_t nrec, uint32_t dim, uint64_t *missing_row)
+{
+    int rc;
+    *missing_row = ~0ULL;
+    if ((rc = require_init()) || (rc = h1h2_shard_args(dim, nrec))) return rc;
+    return h1h2_shard_owner(ret, recs, nrec, dim, missing_row, g_ctx.stream);
+}
+
+int zkgpu_h1h2_shard_counts(uint32_t *start, uint32_t *cnt, uint64_t *total, const uint64_t *sent, const uint64_t *ret,
+                            uint64_t nsent, uint64_t nrows, uint64_t row0)
+{
+    int rc;
+    if ((rc = require_init()) || (rc = h1h2_shard_args(1, nrows))) return rc;
+    if (!nrows) return set_error(ZKGPU_ERR_ARG, "h1h2 (sharded): empty block");
+    return h1h2_shard_counts(start, cnt, total, sent, ret, nsent, nrows, row0, g_ctx.stream);
+}
+
+int zkgpu_h1h2_shard_deal(uint64_t *seg, uint64_t seg_ld, const uint64_t *t, uint64_t t_ld, const uint32_t *start,
+                          const uint32_t *cnt, uint64_t nrows, uint32_t dim)
+{
+    int rc;
+    if ((rc = require_init()) || (rc = h1h2_shard_args(dim, nrows))) return rc;
+    if (!nrows) return 0;
+    return h1h2_shard_deal(seg, seg_ld, t, t_ld, start, cnt, nrows, dim, g_ctx.stream);
+}
+
+int zkgpu_h1h2_shard_place(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint64_t *buf,
+                           uint64_t buf_ld, uint64_t pos0, uint64_t len, uint64_t row0, uint32_t dim)
+{
+    int rc;
+    if ((rc = require_init()) || (rc = h1h2_shard_args(dim, len))) return rc;
+    if (len && (pos0 >> 1) < row0) return set_error(ZKGPU_ERR_ARG, "h1h2 (sharded): position before the block");
+    return h1h2_shard_place(h1, h1_ld, h2, h2_ld, buf, buf_ld, pos0, len, row0, dim, g_ctx.stream);
+}
+
 int zkgpu_cols3_to_interleaved_dev(uint64_t *out, const uint64_t *cols, uint64_t ld, uint64_t n)
 {
     int rc;

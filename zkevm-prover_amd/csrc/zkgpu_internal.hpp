@@ -78,6 +78,19 @@ int merkle_levels(uint64_t *nodes, uint64_t nrows, hipStream_t s);
 int merkle_open_cols(uint64_t *vals, uint64_t *sibs, const uint64_t *nodes, const uint64_t *src, uint64_t ncols,
                      uint64_t nrows, uint64_t ld, const uint64_t *idx, uint64_t nq, hipStream_t s);
 
+// ---- h1h2.hip, row-sharded calculateH1H2 (host/sharded_starks.hpp)
+int h1h2_shard_route(uint64_t *recs, uint64_t cap, uint32_t *n_t, uint32_t *n_f, const uint64_t *f, uint64_t f_ld,
+                     const uint64_t *t, uint64_t t_ld, uint64_t n, uint64_t row0, uint32_t dim, uint32_t world,
+                     hipStream_t s);
+int h1h2_shard_owner(uint64_t *ret, const uint64_t *recs, uint64_t nrec, uint32_t dim, uint64_t *miss_row,
+                     hipStream_t s);
+int h1h2_shard_counts(uint32_t *start, uint32_t *cnt, uint64_t *total, const uint64_t *sent, const uint64_t *ret,
+                      uint64_t nsent, uint64_t n, uint64_t row0, hipStream_t s);
+int h1h2_shard_deal(uint64_t *seg, uint64_t seg_ld, const uint64_t *t, uint64_t t_ld, const uint32_t *start,
+                    const uint32_t *cnt, uint64_t n, uint32_t dim, hipStream_t s);
+int h1h2_shard_place(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint64_t *buf, uint64_t buf_ld,
+                     uint64_t pos0, uint64_t len, uint64_t row0, uint32_t dim, hipStream_t s);
+
 // ---- fri.hip
 int fri_fold(uint64_t *out, const uint64_t *pol, uint32_t pol_bits, uint32_t out_bits, const uint64_t sx[3],
              uint64_t shift_inv, hipStream_t s);

@@ -17,8 +17,10 @@
 //       row 0: the wrap-around of the reference's (i + 1) % N).  calculateZ:
 //       each rank its block, a scan of the W block totals, the block redone
 //       with the product of the earlier ranks' totals (polinomial.hpp:586-607).
-//       calculateH1H2 (starks.cpp:104-127) is a global multiset sort: f and t
-//       are all-gathered, h1/h2 computed on every rank, each keeps its rows.
+//       calculateH1H2 (starks.cpp:104-127), a global multiset sort: distinct
+//       keys routed to their owner ranks, counts back to the table rows'
+//       ranks, each rank deals its table rows' copies and sends every piece
+//       of the multiset to the rank holding those h1/h2 rows (h1h2_sharded).
 //   commit (stages 1-3 and the constants, starks.cpp:53-57,134-138,215-219)
 //       the NTT transpose: the rank's rows of every column go to the rank
 //       owning the column (all-to-all; each (column, rank) slice is contiguous
@@ -74,7 +76,14 @@ public:
     // this proof's exchanges: count, bytes this rank sent, the largest one's
     // sent bytes (reported as COUNT_COMM_* beside the stage timers)
     uint64_t n_exch = 0, sent_bytes = 0, max_sent = 0;
-    uint64_t *puw = nullptr;    // one plookup's f, t, h1, h2 over the whole n domain (12 x N)
+    uint64_t *puw = nullptr;    // W = 1: one plookup's f, t, h1, h2 over the whole n domain (12 x N)
+    // W > 1, calculateH1H2 over the ranks (h1h2_sharded): route records out /
+    // in (5 words each), the owner's returns out / in, the multiset segment
+    // (3 x (nb + N): the rank's table rows can hold up to nb + N copies), the
+    // per-row counts and starts (u32)
+    uint64_t *hs_send = nullptr, *hs_recv = nullptr, *hs_ret = nullptr, *hs_ret_in = nullptr, *hs_seg = nullptr;
+    uint32_t *hs_cnt = nullptr, *hs_start = nullptr;
+    uint64_t hs_recv_cap = 0;
     uint64_t slot = 0, hcap = 0;
     struct Tree {
         uint64_t *nodes = nullptr;
@@ -228,10 +237,22 @@ public:
             stride_r = std::max<uint64_t>({3 * B, piece, 6 * nb});
             if (dalloc(&pack_s, W * stride_s) || dalloc(&pack_r, W * stride_r)) return -1;
         }
-        if (info.n_pu && dalloc(&puw, 12 * N)) return -1;
+        if (info.n_pu && W == 1 && dalloc(&puw, 12 * N)) return -1;
+        if (info.n_pu && W > 1) {
+            // a rank sends <= 2 nb records (its distinct t and f keys); an
+            // owner expects ~2 N / W of them, room for twice that (every rank
+            // checks every owner's total before the exchange, h1h2_sharded)
+            hs_recv_cap = std::min<uint64_t>(2 * N, 4 * N / W + 4096);
+            uint64_t *cs = nullptr;
+            if (dalloc(&hs_send, 5 * 2 * nb) || dalloc(&hs_recv, 5 * hs_recv_cap) || dalloc(&hs_ret, hs_recv_cap) ||
+                dalloc(&hs_ret_in, 2 * nb) || dalloc(&hs_seg, 3 * (nb + N)) || dalloc(&cs, nb))
+                return -1;
+            hs_cnt = (uint32_t *)cs;
+            hs_start = hs_cnt + nb;
+        }
         for (auto &t : trees)
             if (dalloc(&t.nodes, zkgpu_gl_merkle_num_elements(B))) return -1;
-        slot = std::max<uint64_t>(4, std::max<uint64_t>(3ULL * info.n_ev, (uint64_t)q() * s0_record()));
+        slot = std::max<uint64_t>({4, 2ULL * W, 3ULL * info.n_ev, (uint64_t)q() * s0_record()});
         ftrees.assign(fri_steps.size(), Tree{});
         for (size_t si = 1; si < fri_steps.size(); si++) {
             const uint64_t ngroups = 1ULL << fri_steps[si], width = (3ULL << fri_steps[si - 1]) / ngroups;
@@ -856,16 +877,130 @@ public:
         return refresh_halos(zs.cols);
     }
 
-    // calculateH1H2 (starks.cpp:104-127) of every plookup: a global multiset
-    // sort, so f and t are all-gathered, h1 / h2 computed whole on every rank
-    // and each keeps its rows (with the halo: no refresh needed)
+    // calculateH1H2 of plookup k over the ranks (zkgpu_h1h2_shard_*,
+    // include/zkgpu.h): each rank routes its distinct t / f keys to the key's
+    // owner, the owner finds each key's last table row and its f count, the
+    // counts go back to the table rows' ranks, every rank deals its table
+    // rows' copies into its segment of the 2N-long multiset (offset = the
+    // earlier ranks' totals) and sends each piece to the rank holding those
+    // h1 / h2 rows.  Five exchanges (two of them small all-gathers), at most
+    // one message per peer each; the data moved is the distinct keys and the
+    // multiset, not f and t to every rank.
+    int h1h2_sharded(uint32_t k)
+    {
+        const uint32_t *q = &pu[5 * k];
+        const uint32_t d = q[4];
+        const uint64_t *f = S.sec[SEC_TMP_N] + (uint64_t)q[0] * ldn, *t = S.sec[SEC_TMP_N] + (uint64_t)q[1] * ldn;
+        uint64_t *h1 = S.sec[SEC_CM2_N] + (uint64_t)q[2] * ldn, *h2 = S.sec[SEC_CM2_N] + (uint64_t)q[3] * ldn;
+        // 1. the rank's records, bucketed by owner
+        std::vector<uint32_t> nt(W), nf(W);
+        CK(zkgpu_h1h2_shard_route(hs_send, 2 * nb, nt.data(), nf.data(), f, ldn, t, ldn, nb, r0(), d, W));
+        std::vector<uint64_t> mine(2 * W), all;
+        for (uint32_t o = 0; o < W; o++) {
+            mine[2 * o] = nt[o];
+            mine[2 * o + 1] = nf[o];
+        }
+        if (allgather(mine.data(), 2 * W, all)) return -1;
+        auto nt_of = [&](uint32_t s, uint32_t o) { return all[(uint64_t)s * 2 * W + 2 * o]; };
+        auto nr_of = [&](uint32_t s, uint32_t o) { return all[(uint64_t)s * 2 * W + 2 * o] + all[(uint64_t)s * 2 * W + 2 * o + 1]; };
+        std::vector<uint64_t> soff(W + 1, 0), roff(W + 1, 0);
+        for (uint32_t o = 0; o < W; o++) soff[o + 1] = soff[o] + nr_of(R, o);
+        for (uint32_t s = 0; s < W; s++) roff[s + 1] = roff[s] + nr_of(s, R);
+        for (uint32_t o = 0; o < W; o++) {  // the same verdict on every rank, before anything moves
+            uint64_t tot = 0;
+            for (uint32_t s = 0; s < W; s++) tot += nr_of(s, o);
+            if (tot > hs_recv_cap)
+                return fail("calculateH1H2 (sharded): rank %u owns %llu keys, more than its %llu-record buffer", o,
+                            (unsigned long long)tot, (unsigned long long)hs_recv_cap);
+        }
+        // 2. records to their owners
+        const uint64_t RW = 5 * 8;  // bytes per record
+        for (uint32_t o = 0; o < W; o++)
+            if (o != R && nr_of(R, o)) op(o, 1, hs_send + 5 * soff[o], nr_of(R, o) * RW);
+        for (uint32_t s = 0; s < W; s++)
+            if (s != R && nr_of(s, R)) op(s, 0, hs_recv + 5 * roff[s], nr_of(s, R) * RW);
+        if (nr_of(R, R)) CK(zkgpu_memcpy_d2d(hs_recv + 5 * roff[R], hs_send + 5 * soff[R], nr_of(R, R) * RW));
+        if (exchange()) return -1;
+        // 3. the owner's side, then each t record's count back to its sender
+        uint64_t miss = ~0ULL;
+        CK(zkgpu_h1h2_shard_owner(hs_ret, hs_recv, roff[W], d, &miss));
+        for (uint32_t s = 0; s < W; s++)
+            if (s != R && nt_of(s, R)) op(s, 1, hs_ret + roff[s], nt_of(s, R) * 8);
+        for (uint32_t o = 0; o < W; o++)
+            if (o != R && nt_of(R, o)) op(o, 0, hs_ret_in + soff[o], nt_of(R, o) * 8);
+        if (nt_of(R, R)) CK(zkgpu_memcpy_d2d(hs_ret_in + soff[R], hs_ret + roff[R], nt_of(R, R) * 8));
+        if (exchange()) return -1;
+        // 4. counts, the rank's multiset total; totals and the smallest missing f row everywhere
+        uint64_t tot = 0;
+        CK(zkgpu_h1h2_shard_counts(hs_start, hs_cnt, &tot, hs_send, hs_ret_in, soff[W], nb, r0()));
+        const uint64_t tm[2] = {tot, miss};
+        std::vector<uint64_t> tms;
+        if (allgather(tm, 2, tms)) return -1;
+        uint64_t gmiss = ~0ULL, O = 0, sum = 0;
+        std::vector<uint64_t> off(W);
+        for (uint32_t s = 0; s < W; s++) {
+            gmiss = std::min(gmiss, tms[2 * s + 1]);
+            off[s] = sum;
+            sum += tms[2 * s];
+        }
+        if (gmiss != ~0ULL)
+            return fail("Polinomial::calculateH1H2() Number not included: w=%llu plookup_number=%u",
+                        (unsigned long long)gmiss, k);
+        if (sum != 2 * N) return fail("calculateH1H2 (sharded): the multiset has %llu entries, not 2N", (unsigned long long)sum);
+        O = off[R];
+        // 5. the rank's segment [O, O + tot) of the multiset, each piece to the rank holding its h rows
+        const uint64_t sld = tot ? tot : 1;
+        CK(zkgpu_h1h2_shard_deal(hs_seg, sld, t, ldn, hs_start, hs_cnt, nb, d));
+        auto piece = [&](uint64_t o0, uint64_t len, uint32_t e, uint64_t &a, uint64_t &b) {
+            a = std::max<uint64_t>(o0, 2ULL * e * nb);
+            b = std::min<uint64_t>(o0 + len, 2ULL * (e + 1) * nb);
+            return a < b;
+        };
+        for (uint32_t e = 0; e < W; e++) {
+            uint64_t a, b;
+            if (!piece(O, tot, e, a, b)) continue;
+            if (e == R) {
+                CK(zkgpu_h1h2_shard_place(h1, ldn, h2, ldn, hs_seg + (a - O), sld, a, b - a, r0(), d));
+                continue;
+            }
+            CK(zkgpu_copy_rows_dev(pack_s + e * stride_s, b - a, 0, nullptr, hs_seg, sld, a - O, 0, nullptr, d, b - a));
+            op(e, 1, pack_s + e * stride_s, (b - a) * d * 8);
+        }
+        std::vector<std::pair<uint64_t, uint64_t>> got(W, {0, 0});
+        for (uint32_t s = 0; s < W; s++) {
+            uint64_t a, b;
+            if (s == R || !piece(off[s], tms[2 * s], R, a, b)) continue;
+            got[s] = {a, b};
+            op(s, 0, pack_r + s * stride_r, (b - a) * d * 8);
+        }
+        if (exchange()) return -1;
+        for (uint32_t s = 0; s < W; s++)
+            if (got[s].second > got[s].first)
+                CK(zkgpu_h1h2_shard_place(h1, ldn, h2, ldn, pack_r + s * stride_r, got[s].second - got[s].first,
+                                          got[s].first, got[s].second - got[s].first, r0(), d));
+        return 0;
+    }
+
+    // calculateH1H2 (starks.cpp:104-127) of every plookup: over the ranks
+    // (h1h2_sharded), then the h1 / h2 halos; one rank: the whole-column form
     int h1h2_all() override
     {
+        if (W > 1) {
+            Stores hs;
+            for (uint32_t k = 0; k < info.n_pu; k++) {
+                if (h1h2_sharded(k)) return -1;
+                const uint32_t *q = &pu[5 * k];
+                for (uint32_t c = 0; c < q[4]; c++) {
+                    hs.cols[SEC_CM2_N].push_back(q[2] + c);
+                    hs.cols[SEC_CM2_N].push_back(q[3] + c);
+                }
+            }
+            return refresh_halos(hs.cols);
+        }
         for (uint32_t k = 0; k < info.n_pu; k++) {
             const uint32_t *q = &pu[5 * k];
             const uint32_t d = q[4];
             uint64_t *fw = puw, *tw = puw + 3 * N, *h1w = puw + 6 * N, *h2w = puw + 9 * N;
-            // the rank's f and t rows as one message (2d columns, ld nb) to every peer
             std::vector<uint32_t> ft;
             for (uint32_t part = 0; part < 2; part++)
                 for (uint32_t c = 0; c < d; c++) ft.push_back(q[part] + c);
@@ -873,19 +1008,6 @@ public:
             for (uint32_t part = 0; part < 2; part++)
                 for (uint32_t c = 0; c < d; c++) dst.push_back(3 * part + c);
             CK(zkgpu_copy_rows_dev(fw, N, r0(), dst.data(), S.sec[SEC_TMP_N], ldn, 0, 0, ft.data(), 2 * d, nb));
-            if (W > 1) {
-                CK(zkgpu_copy_rows_dev(pack_s, nb, 0, nullptr, S.sec[SEC_TMP_N], ldn, 0, 0, ft.data(), 2 * d, nb));
-                for (uint32_t p = 0; p < W; p++) {
-                    if (p == R) continue;
-                    op(p, 1, pack_s, 2ULL * d * nb * 8);
-                    op(p, 0, pack_r + p * stride_r, 2ULL * d * nb * 8);
-                }
-                if (exchange()) return -1;
-                for (uint32_t p = 0; p < W; p++)
-                    if (p != R)
-                        CK(zkgpu_copy_rows_dev(fw, N, (uint64_t)p * nb, dst.data(), pack_r + p * stride_r, nb, 0, 0,
-                                               nullptr, 2 * d, nb));
-            }
             uint64_t miss = 0;
             const int rc = zkgpu_h1h2_dev(h1w, N, h2w, N, fw, N, tw, N, N, d, &miss);
             if (rc) {

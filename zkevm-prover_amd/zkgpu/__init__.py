@@ -100,6 +100,11 @@ _SIGS = {
     "zkgpu_scale_by_powers_dev": (ctypes.c_int, [vp, u64, u32, u64, u64]),
     "zkgpu_cols3_to_interleaved_dev": (ctypes.c_int, [vp, vp, u64, u64]),
     "zkgpu_h1h2_dev": (ctypes.c_int, [vp, u64, vp, u64, vp, u64, vp, u64, u64, u32, pu64]),
+    "zkgpu_h1h2_shard_route": (ctypes.c_int, [vp, u64, vp, vp, vp, u64, vp, u64, u64, u64, u32, u32]),
+    "zkgpu_h1h2_shard_owner": (ctypes.c_int, [vp, vp, u64, u32, pu64]),
+    "zkgpu_h1h2_shard_counts": (ctypes.c_int, [vp, vp, pu64, vp, vp, u64, u64, u64]),
+    "zkgpu_h1h2_shard_deal": (ctypes.c_int, [vp, u64, vp, u64, vp, vp, u64, u32]),
+    "zkgpu_h1h2_shard_place": (ctypes.c_int, [vp, u64, vp, u64, vp, u64, u64, u64, u64, u32]),
     "zkgpu_gl_merkle_open_rows_dev": (ctypes.c_int, [vp, vp, vp, vp, u64, u64, vp, u64]),
     "zkgpu_prof_enable": (ctypes.c_int, [ctypes.c_int]),
     "zkgpu_prof_reset": (ctypes.c_int, []),
