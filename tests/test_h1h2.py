@@ -113,33 +113,102 @@ def test_gpu_h1h2_non_canonical_and_missing(oracle, zkgpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sort_path", [False, True])
-def test_gpu_h1h2_dim3_shared_components(oracle, zkgpu, sort_path, monkeypatch):
+def test_gpu_h1h2_dim3_shared_components(oracle, zkgpu):
     """dim 3 keys that agree in one or two components (the table must compare
-    all three), non-canonical words in components 1/2, at 2^20 rows; both the
-    hash path (default) and the sort path (ZKGPU_H1H2_SORT=1, read once per
-    process: run in a child) give the oracle's h1/h2."""
-    import subprocess
-    import sys
-    if sort_path:
-        code = ("import sys; sys.path[:0] = %r\n"
-                "import test_h1h2 as T\n"
-                "from oracle import oracle as oc\nimport zkgpu\noc.lib()\nzkgpu.init()\n"
-                "T._shared_components_case(oc, zkgpu)\n") % ([ROOT_DIR, ROOT_DIR + "/zkevm-prover_amd",
-                                                               ROOT_DIR + "/tests"],)
-        env = dict(__import__("os").environ, ZKGPU_H1H2_SORT="1")
-        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
-        assert r.returncode == 0, r.stderr[-2000:]
-    else:
-        _shared_components_case(oracle, zkgpu)
+    all three), non-canonical words in components 1/2, at 2^20 rows: the
+    oracle's h1/h2."""
+    _shared_components_case(oracle, zkgpu)
 
 
-ROOT_DIR = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
-
-
-def _shared_components_case(oracle, zkgpu):
+def _sharded_h1h2(zkgpu, df, dt, n, d, W):
+    """calculateH1H2 through the row-sharded primitives (zkgpu_h1h2_shard_*)
+    for W ranks of n / W rows, the exchanges of host/sharded_starks.hpp
+    h1h2_sharded emulated by device copies in one process.  Returns (h1, h2)
+    (d x n device columns) or the missing f row."""
     import torch
+    nb = n // W
+    dev = "cuda:0"
+    recs, cnts = [], []
+    for r in range(W):
+        rec = torch.zeros(5 * 2 * nb, dtype=torch.int64, device=dev)
+        nt, nf = zkgpu.h1h2_shard_route(rec, 2 * nb, df.data_ptr() + 8 * r * nb, n, dt.data_ptr() + 8 * r * nb, n, nb,
+                                        r * nb, d, W)
+        recs.append(rec)
+        cnts.append((nt.astype(np.int64), nf.astype(np.int64)))
+    nr = lambda s, o: int(cnts[s][0][o] + cnts[s][1][o])  # noqa: E731
+    soff = [np.concatenate([[0], np.cumsum([nr(s, o) for o in range(W)])]).astype(np.int64) for s in range(W)]
+    rets, roffs, misses = [], [], []
+    for o in range(W):  # the owner's side of the record all-to-all
+        roff = np.concatenate([[0], np.cumsum([nr(s, o) for s in range(W)])]).astype(np.int64)
+        recv = torch.zeros(5 * max(int(roff[-1]), 1), dtype=torch.int64, device=dev)
+        for s in range(W):
+            recv[5 * roff[s]:5 * roff[s + 1]] = recs[s][5 * soff[s][o]:5 * (soff[s][o] + nr(s, o))]
+        ret = torch.zeros(max(int(roff[-1]), 1), dtype=torch.int64, device=dev)
+        misses.append(zkgpu.h1h2_shard_owner(ret, recv, int(roff[-1]), d))
+        rets.append(ret)
+        roffs.append(roff)
+    if any(m is not None for m in misses):
+        return min(m for m in misses if m is not None)
+    tots, starts, cntl = [], [], []
+    for s in range(W):  # the returns all-to-all, then the sender's counts
+        ret_in = torch.zeros(max(2 * nb, 1), dtype=torch.int64, device=dev)
+        for o in range(W):
+            k = int(cnts[s][0][o])
+            ret_in[soff[s][o]:soff[s][o] + k] = rets[o][roffs[o][s]:roffs[o][s] + k]
+        start = torch.zeros(nb, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(nb, dtype=torch.int32, device=dev)
+        tots.append(zkgpu.h1h2_shard_counts(start, cnt, recs[s], ret_in, int(soff[s][-1]), nb, s * nb))
+        starts.append(start)
+        cntl.append(cnt)
+    assert sum(tots) == 2 * n
+    off = np.concatenate([[0], np.cumsum(tots)]).astype(np.int64)
+    h1 = torch.zeros((d, n), dtype=torch.int64, device=dev)
+    h2 = torch.zeros((d, n), dtype=torch.int64, device=dev)
+    for s in range(W):  # deal, then each piece to the rank holding its rows
+        tot = tots[s]
+        seg = torch.zeros(d * max(tot, 1), dtype=torch.int64, device=dev)
+        zkgpu.h1h2_shard_deal(seg, max(tot, 1), dt.data_ptr() + 8 * s * nb, n, starts[s], cntl[s], nb, d)
+        for e in range(W):
+            a, b = max(off[s], 2 * e * nb), min(off[s] + tot, 2 * (e + 1) * nb)
+            if a < b:
+                zkgpu.h1h2_shard_place(h1.data_ptr() + 8 * e * nb, n, h2.data_ptr() + 8 * e * nb, n,
+                                       seg.data_ptr() + 8 * int(a - off[s]), max(tot, 1), int(a), int(b - a), e * nb, d)
+    return h1, h2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_gpu_h1h2_sharded_primitives(oracle, zkgpu, world):
+    """the row-sharded calculateH1H2 (zkgpu_h1h2_shard_*, the steps the
+    sharded prover runs with exchanges) == the oracle: dim 3 with shared
+    components and non-canonical words (2^20 rows), dim 1 with a repeated
+    table value (the last row keeps the counts) and an f that is one value,
+    and the smallest missing f row"""
+    import torch
+    rng = np.random.default_rng(world)
     n = 1 << 20
+    t3, f3 = _shared_components_inputs(n)
+    cols = (lambda a: np.ascontiguousarray(a.T))
+    r1, r2 = oracle.h1h2(f3, t3)
+    h1, h2 = _sharded_h1h2(zkgpu, zkgpu.to_device(cols(f3)), zkgpu.to_device(cols(t3)), n, 3, world)
+    torch.cuda.synchronize()
+    assert np.array_equal(zkgpu.from_device(h1).T, r1) and np.array_equal(zkgpu.from_device(h2).T, r2)
+    n = 1 << 14
+    t = rng.integers(0, P, size=n, dtype=np.uint64)
+    t[7] = t[n - 5]  # a repeated table value: the later row takes the f counts
+    for f in (t[rng.integers(0, n, size=n)], np.full(n, t[n - 5], np.uint64)):
+        r1, r2 = oracle.h1h2(f, t)
+        h1, h2 = _sharded_h1h2(zkgpu, zkgpu.to_device(f), zkgpu.to_device(t), n, 1, world)
+        torch.cuda.synchronize()
+        assert np.array_equal(zkgpu.from_device(h1)[0], r1) and np.array_equal(zkgpu.from_device(h2)[0], r2)
+    f = t[rng.integers(0, n, size=n)]
+    f[9000] = np.uint64(123456789)
+    f[12000] = np.uint64(987654321)
+    if not (t == f[9000]).any() and not (t == f[12000]).any():
+        assert _sharded_h1h2(zkgpu, zkgpu.to_device(f), zkgpu.to_device(t), n, 1, world) == 9000
+
+
+def _shared_components_inputs(n):
     rng = np.random.default_rng(20)
     base = rng.integers(0, P, size=(64, 3), dtype=np.uint64)
     vals = np.repeat(base, 16, axis=0)
@@ -150,6 +219,13 @@ def _shared_components_case(oracle, zkgpu):
     small = t[:, 1] < np.uint64(2**32 - 1)
     t[small, 1] += np.uint64(P)  # same element, non-canonical word
     f = t[rng.integers(0, n, size=n)] % np.uint64(P)
+    return t, f
+
+
+def _shared_components_case(oracle, zkgpu):
+    import torch
+    n = 1 << 20
+    t, f = _shared_components_inputs(n)
     r1, r2 = oracle.h1h2(f, t)
     cols = (lambda a: np.ascontiguousarray(a.T))
     df, dt = zkgpu.to_device(cols(f)), zkgpu.to_device(cols(t))

@@ -18,6 +18,21 @@ def test_stamp_depends_on_sources_and_env(tmp_path, monkeypatch):
     env = dict(os.environ, ZKGPU_LDE3="1")
     s1 = stamp.all_stamps(env)
     assert s1["lde"] != s0["lde"] and s1["poseidon"] == s0["poseidon"] and s1["zxp"] == s0["zxp"]
+    env = dict(os.environ, ZKGPU_ZXP_MAX_TERMS="16")
+    s2 = stamp.all_stamps(env)
+    assert s2["zxp"] != s0["zxp"] and s2["lde"] == s0["lde"]
+    # every environment setting the native code still reads is either listed
+    # here or not a kernel setting
+    import re
+    src = ""
+    for d in ("csrc", "host"):
+        for fn in os.listdir(os.path.join(stamp.PKG, d)):
+            src += open(os.path.join(stamp.PKG, d, fn), errors="replace").read()
+    read = set(re.findall(r'getenv\("(ZKGPU_\w+)"\)', src))
+    not_kernel = {"ZKGPU_ZXP_JIT", "ZKGPU_JIT_CACHE", "ZKGPU_JIT_LOG", "ZKGPU_ZXP_JIT_THREADS", "ZKGPU_ZXP_JIT_ONLY",
+                  "ZKGPU_ZXP_JIT_DUMP", "ZKGPU_RUN_ID"}
+    listed = {k for v in stamp.ENV.values() for k in v}
+    assert read <= listed | not_kernel, read - listed - not_kernel
     # the interpreter/compiled switch is not a kernel setting
     assert stamp.all_stamps(dict(os.environ, ZKGPU_ZXP_JIT="0"))["zxp"] == s0["zxp"]
     ok, why = stamp.check({"stamps": s0}, "zxp")

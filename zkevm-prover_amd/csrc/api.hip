@@ -128,16 +128,12 @@ static uint32_t log2u(uint64_t n)
 // Columns per extend_pol batch: the batch's coefficients (n words per
 // column) and, on the 6-pass path, its 2n-row scratch live in grow-only
 // workspaces, so the batch bounds that memory -- 2^31 words (16 GiB) of
-// scratch unless ZKGPU_LDE_BATCH_COLS says otherwise.  (Batches of 32 columns
+// scratch.  (Batches of 32 columns
 // at 2^24 rows measured 2-3 % slower than one batch of 100: 51.9 vs 53.5
 // Gelem/s, the same box.)
 static uint64_t lde_batch_cols(uint64_t n_ext, uint64_t ncols)
 {
-    static const uint64_t env = [] {
-        const char *e = getenv("ZKGPU_LDE_BATCH_COLS");
-        return e && atoll(e) > 0 ? (uint64_t)atoll(e) : 0ULL;
-    }();
-    uint64_t batch = env ? env : std::max<uint64_t>(1, (1ULL << 31) / (n_ext ? n_ext : 1));
+    const uint64_t batch = std::max<uint64_t>(1, (1ULL << 31) / (n_ext ? n_ext : 1));
     return batch < ncols ? batch : ncols;
 }
 
@@ -1215,10 +1211,8 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
         J.zmask = (uint32_t)(zh - 1);
         J.x_start = x_start % HP;
         J.bytes = L.bytes;
-        const char *env_loop = getenv("ZKGPU_ZXP_JIT_DOTLOOP");
-        const char *env_waves = getenv("ZKGPU_ZXP_JIT_WAVES");
-        J.dot_loop_min = env_loop ? (uint32_t)atoi(env_loop) : 8u;
-        J.waves_per_eu = env_waves ? (uint32_t)atoi(env_waves) : 0u;
+        J.dot_loop_min = 8;  // (zxp_jit.hip zkgpu_zxp_jit_source uses the same settings)
+        J.waves_per_eu = 0;
         J.force_split = 0;
         J.scratch = nullptr;
         J.scratch_ld = 0;
@@ -1296,16 +1290,8 @@ int zkgpu_evmap_dev(uint64_t *evals_out, const uint64_t *const *cols, const uint
         uint32_t prime, sub0;
     };
     if (evmap_group_size() != sizeof(G) || evmap_group_width() != 8) return set_error(ZKGPU_ERR_ARG, "evmap group layout");
-    static const uint32_t GW = [] {  // sub-entries per group: accumulator VGPRs vs shared limb work
-        const char *e = getenv("ZKGPU_EVMAP_G");
-        const uint32_t w = e ? (uint32_t)atoi(e) : 4u;
-        return (w == 1 || w == 2 || w == 4) ? w : 4u;
-    }();
-    static const uint32_t UR = [] {  // rows per thread and iteration
-        const char *e = getenv("ZKGPU_EVMAP_U");
-        const uint32_t u = e ? (uint32_t)atoi(e) : 2u;
-        return (u == 1 || u == 2 || u == 4) ? u : 2u;
-    }();
+    constexpr uint32_t GW = 4;  // sub-entries per group: accumulator VGPRs vs shared limb work
+    constexpr uint32_t UR = 2;  // rows per thread and iteration
     struct Sub {
         const uint64_t *col;
         uint32_t prime, which, entry;

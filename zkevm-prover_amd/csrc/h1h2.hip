@@ -5,31 +5,21 @@
 // The reference builds a chained hash table of the table column t (each key
 // remembers its LAST row), counts every f value onto that row, and deals the
 // resulting multiset (t[j] repeated 1 + count_j times, in t order) alternately
-// into h1 and h2.  The same mapping, data-parallel:
-//   1. perm = stable radix sort of row indices by the canonical key
-//      (dim 3: three stable LSD passes, component 2 first, so the order is
-//      lexicographic (k0, k1, k2) with equal keys in ascending row order);
-//   2. one thread per f row: upper_bound in the sorted keys, step back one
-//      -> the last table row with that key; atomicAdd on its count
-//      (counts start at 1); a key that is absent records the smallest such
-//      row ("Number not included");
-//   3. exclusive scan of the counts = start position of each t row in the
-//      2N-long multiset;
-//   4. one thread per multiset slot s: j = upper_bound(start, s) - 1,
-//      h_{1 + (s & 1)}[s >> 1] = t[j]  (raw copy, like copyElement).
+// into h1 and h2.  The same mapping, data-parallel (h1h2_hash): an
+// open-addressing table of table ROWS keyed by the canonical value (linear
+// probing, 2^k >= 2N slots of u32): insertion keeps the largest row per key
+// (atomicMax: the reference's "last row wins"), every f row probes and counts
+// onto its row (counts start at 1; an absent key records the smallest such f
+// row, "Number not included"), an exclusive scan of the counts gives each
+// table row its start in the 2N-long multiset, and one thread per table row
+// scatters its 1 + count raw copies (copyElement) alternately into h1 / h2.
 // Columns are column-major: component c of a dim-3 column at ptr + c * ld.
-//
-// Default path (hash, h1h2_hash below): steps 1-2 as an open-addressing table
-// of table ROWS keyed by the canonical value (linear probing, 2^k >= 2N
-// slots of u32): insertion keeps the largest row per key (atomicMax: the
-// reference's "last row wins"), then every f row probes, and step 4 scatters
-// each table row's 1 + count copies from its start.  The sort path stays
-// selectable with ZKGPU_H1H2_SORT=1 (A/B); both are the same mapping.
+// (A stable radix sort of the keys with a two-level upper_bound was the
+// round-2 form: 8.1 against 1.9 ms for two plookups at 2^23.)
 #include <stdlib.h>
 
 #include <vector>
 
-#include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
 #include "gl_device.hpp"
@@ -39,119 +29,10 @@ namespace zk {
 
 static inline uint32_t nblk2(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
 
-__global__ void k_h12_iota(uint32_t *v, uint64_t n)
-{
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) v[i] = (uint32_t)i;
-}
-
-// out[r] = canon(col[perm[r]])  (perm = null: identity)
-__global__ void k_h12_gather(uint64_t *out, const uint64_t *col, const uint32_t *perm, uint64_t n)
-{
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < n) out[r] = gl_canon(col[perm ? perm[r] : r]);
-}
-
 __global__ void k_h12_fill1(uint32_t *c, uint64_t n)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) c[i] = 1;
-}
-
-template <int DIM>
-__device__ __forceinline__ int h12_cmp(const uint64_t *sk, uint64_t n, uint64_t r, const uint64_t *key)
-{
-#pragma unroll
-    for (int c = 0; c < DIM; c++) {
-        const uint64_t v = sk[c * n + r];
-        if (v < key[c]) return -1;
-        if (v > key[c]) return 1;
-    }
-    return 0;
-}
-
-// Two-level upper_bound: the first H12_S levels of the search run on a sample
-// of the sorted first components held in LDS (smp[j] = sk0[r_j], r_j =
-// min((j+1) step, n) - 1), the rest in global memory over one sample
-// interval -- 23 -> ~11 dependent random HBM reads per f row at 2^23.
-constexpr uint32_t H12_S = 4096;
-constexpr uint32_t H12_ROWS = 8;  // f rows per thread (amortises the LDS fill)
-
-__device__ __forceinline__ uint64_t h12_sample_row(uint64_t j, uint64_t step, uint64_t n)
-{
-    const uint64_t r = (j + 1) * step;
-    return (r < n ? r : n) - 1;
-}
-
-__global__ void k_h12_sample(uint64_t *smp, const uint64_t *sk0, uint64_t n, uint64_t step, uint32_t S)
-{
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < S) smp[j] = sk0[h12_sample_row(j, step, n)];
-}
-
-// sk: DIM sorted key columns (ld n); perm: sorted position -> table row
-template <int DIM>
-__global__ void __launch_bounds__(256) k_h12_count(const uint64_t *f, uint64_t f_ld, const uint64_t *sk,
-                                                   const uint32_t *perm, uint64_t n, const uint64_t *smp, uint32_t S,
-                                                   uint64_t step, uint32_t *cnt, unsigned long long *miss)
-{
-    __shared__ uint64_t ls[H12_S];
-    for (uint32_t j = threadIdx.x; j < S; j += blockDim.x) ls[j] = smp[j];
-    __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * blockDim.x * H12_ROWS + threadIdx.x;
-    for (uint32_t q = 0; q < H12_ROWS; q++) {
-        const uint64_t i = base + (uint64_t)q * blockDim.x;
-        if (i >= n) return;
-        uint64_t key[DIM];
-#pragma unroll
-        for (int c = 0; c < DIM; c++) key[c] = gl_canon(f[c * f_ld + i]);
-        // first sample j whose row's key is > key
-        uint32_t a = 0, b = S;
-        while (a < b) {
-            const uint32_t mid = (a + b) >> 1;
-            const uint64_t v = ls[mid];
-            const bool gt = v > key[0] || (v == key[0] && h12_cmp<DIM>(sk, n, h12_sample_row(mid, step, n), key) > 0);
-            if (gt)
-                b = mid;
-            else
-                a = mid + 1;
-        }
-        uint64_t lo = a ? h12_sample_row(a - 1, step, n) + 1 : 0;
-        uint64_t hi = a < S ? h12_sample_row(a, step, n) : n;
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (h12_cmp<DIM>(sk, n, mid, key) <= 0)
-                lo = mid + 1;
-            else
-                hi = mid;
-        }
-        if (lo == 0 || h12_cmp<DIM>(sk, n, lo - 1, key) != 0) {
-            atomicMin(miss, (unsigned long long)i);
-            continue;
-        }
-        atomicAdd(&cnt[perm[lo - 1]], 1u);
-    }
-}
-
-template <int DIM>
-__global__ void k_h12_deal(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint64_t *t, uint64_t t_ld,
-                           const uint32_t *start, uint64_t n)
-{
-    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= 2 * n) return;
-    uint64_t lo = 0, hi = n;  // upper_bound(start, s)
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if ((uint64_t)start[mid] <= s)
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    const uint64_t j = lo - 1;
-    uint64_t *h = (s & 1) ? h2 : h1;
-    const uint64_t ld = (s & 1) ? h2_ld : h1_ld;
-#pragma unroll
-    for (int c = 0; c < DIM; c++) h[c * ld + (s >> 1)] = t[c * t_ld + j];
 }
 
 // ---------------------------------------------------------------- hash path
@@ -313,95 +194,8 @@ static int h1h2_hash(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld,
 int h1h2(uint64_t *h1, uint64_t h1_ld, uint64_t *h2, uint64_t h2_ld, const uint64_t *f, uint64_t f_ld,
          const uint64_t *t, uint64_t t_ld, uint64_t n, uint32_t dim, uint64_t *missing_row, hipStream_t s)
 {
-    static const bool use_sort = [] {
-        const char *e = getenv("ZKGPU_H1H2_SORT");
-        return e && atoi(e) != 0;
-    }();
-    if (!use_sort && n < 0xFFFFFFFFULL)
-        return h1h2_hash(h1, h1_ld, h2, h2_ld, f, f_ld, t, t_ld, n, dim, missing_row, s);
-    // scratch: keys_in, keys_out (n u64 each), sk (dim n u64; sk[0] = keys_out
-    // of the last pass), perm_in, perm_out, cnt (n u32 each), miss (u64)
-    const size_t kb = n * sizeof(uint64_t), pb = n * sizeof(uint32_t);
-    const size_t need = 2 * kb + 2 * kb /* sk[1], sk[2] */ + 3 * pb + 16 + H12_S * 8 /* search sample */;
-    char *w = (char *)workspace(4, need);
-    if (!w) return ZKGPU_ERR_OOM;
-    uint64_t *keys_in = (uint64_t *)w;
-    uint64_t *keys_out = keys_in + n;
-    uint64_t *sk12 = keys_out + n;  // components 1, 2 of the sorted keys
-    uint32_t *perm_in = (uint32_t *)(sk12 + 2 * n);
-    uint32_t *perm_out = perm_in + n;
-    uint32_t *cnt = perm_out + n;
-    unsigned long long *miss = (unsigned long long *)(((uintptr_t)(cnt + n) + 7) & ~(uintptr_t)7);
-
-    // temp storage for the sort and the scan (sized once for both)
-    size_t sort_bytes = 0, scan_bytes = 0;
-    if (rocprim::radix_sort_pairs(nullptr, sort_bytes, keys_in, keys_out, perm_in, perm_out, (unsigned int)n, 0, 64, s) !=
-            hipSuccess ||
-        rocprim::exclusive_scan(nullptr, scan_bytes, cnt, perm_in, 0u, (size_t)n, rocprim::plus<uint32_t>(), s) !=
-            hipSuccess)
-        return set_error(ZKGPU_ERR_HIP, "h1h2: rocprim temp-size query failed");
-    void *tmp = workspace(5, sort_bytes > scan_bytes ? sort_bytes : scan_bytes);
-    if (!tmp) return ZKGPU_ERR_OOM;
-    size_t tmp_bytes = sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
-
-    const uint32_t B = 256;
-    prof_begin(s);
-    hipLaunchKernelGGL(k_h12_iota, dim3(nblk2(n, B)), dim3(B), 0, s, perm_in, n);
-    for (int c = (int)dim - 1; c >= 0; c--) {
-        hipLaunchKernelGGL(k_h12_gather, dim3(nblk2(n, B)), dim3(B), 0, s, keys_in, t + (uint64_t)c * t_ld,
-                           c == (int)dim - 1 ? (const uint32_t *)nullptr : perm_in, n);
-        size_t tb = tmp_bytes;
-        if (rocprim::radix_sort_pairs(tmp, tb, keys_in, keys_out, perm_in, perm_out, (unsigned int)n, 0, 64, s) !=
-            hipSuccess)
-            return set_error(ZKGPU_ERR_HIP, "h1h2: radix sort failed");
-        uint32_t *x = perm_in;
-        perm_in = perm_out;
-        perm_out = x;
-    }
-    // perm_in = sorted position -> table row; keys_out = component 0 sorted
-    for (uint32_t c = 1; c < dim; c++)
-        hipLaunchKernelGGL(k_h12_gather, dim3(nblk2(n, B)), dim3(B), 0, s, sk12 + (uint64_t)(c - 1) * n,
-                           t + (uint64_t)c * t_ld, perm_in, n);
-    // the count kernel indexes components as sk[c * n + r]: lay them out contiguously
-    uint64_t *sk = keys_out;  // keys_out, sk12[0..n), sk12[n..2n) are contiguous (keys_out + n == sk12)
-    hipLaunchKernelGGL(k_h12_fill1, dim3(nblk2(n, B)), dim3(B), 0, s, cnt, n);
-    (void)hipMemsetAsync(miss, 0xFF, 8, s);
-    const uint32_t S = (uint32_t)(n < H12_S ? n : H12_S);
-    const uint64_t step = (n + S - 1) / S;
-    uint64_t *smp = (uint64_t *)(miss + 1);
-    hipLaunchKernelGGL(k_h12_sample, dim3(nblk2(S, B)), dim3(B), 0, s, smp, sk, n, step, S);
-    const uint32_t cblocks = nblk2(n, B * H12_ROWS);
-    if (dim == 1)
-        hipLaunchKernelGGL(k_h12_count<1>, dim3(cblocks), dim3(B), 0, s, f, f_ld, sk, perm_in, n, smp, S, step, cnt,
-                           miss);
-    else
-        hipLaunchKernelGGL(k_h12_count<3>, dim3(cblocks), dim3(B), 0, s, f, f_ld, sk, perm_in, n, smp, S, step, cnt,
-                           miss);
-    uint32_t *start = perm_out;  // free now
-    {
-        size_t tb = tmp_bytes;
-        if (rocprim::exclusive_scan(tmp, tb, cnt, start, 0u, (size_t)n, rocprim::plus<uint32_t>(), s) != hipSuccess)
-            return set_error(ZKGPU_ERR_HIP, "h1h2: scan failed");
-    }
-    unsigned long long mh = 0;
-    if (check_hip(hipMemcpyAsync(&mh, miss, 8, hipMemcpyDeviceToHost, s), "D2H") ||
-        check_hip(hipStreamSynchronize(s), "h1h2 sync"))
-        return ZKGPU_ERR_HIP;
-    if (mh != ~0ULL) {
-        if (missing_row) *missing_row = mh;
-        return set_error(ZKGPU_ERR_ARG, "calculateH1H2: Number not included: w=%llu", mh);
-    }
-    if (missing_row) *missing_row = ~0ULL;
-    if (dim == 1)
-        hipLaunchKernelGGL(k_h12_deal<1>, dim3(nblk2(2 * n, B)), dim3(B), 0, s, h1, h1_ld, h2, h2_ld, t, t_ld, start,
-                           n);
-    else
-        hipLaunchKernelGGL(k_h12_deal<3>, dim3(nblk2(2 * n, B)), dim3(B), 0, s, h1, h1_ld, h2, h2_ld, t, t_ld, start,
-                           n);
-    prof_end("k_h1h2", (double)dim * 8.0 * 4.0 * n, s);
-    return check_launch("h1h2");
+    return h1h2_hash(h1, h1_ld, h2, h2_ld, f, f_ld, t, t_ld, n, dim, missing_row, s);
 }
-
 
 // ---------------------------------------------------------------- row-sharded
 // calculateH1H2 over W ranks, each holding rows [row0, row0 + n) of f and t

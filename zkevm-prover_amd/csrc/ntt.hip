@@ -466,11 +466,7 @@ static std::vector<OtwTable> g_otw;
 
 static const uint64_t *otw_table(Ctx &ctx, int d, uint32_t logm, uint32_t logr, hipStream_t s)
 {
-    static const int enabled = [] {
-        const char *v = getenv("ZKGPU_NTT_OTW");
-        return v ? atoi(v) : 1;
-    }();
-    if (!enabled || logm > OTW_MAX_LOG) return nullptr;
+    if (logm > OTW_MAX_LOG) return nullptr;
     for (const OtwTable &t : g_otw)
         if (t.d == d && t.logm == logm && t.logr == logr) return t.ptr;
     uint64_t *p = nullptr;
@@ -508,18 +504,10 @@ static void launch_pass(const PassArgs &a, uint64_t ncols, int inverse, hipStrea
     constexpr int LOGR = L1 + L2;
     uint64_t units = (1ULL << (a.logn - LOGR)) / 16;
     dim3 grid((uint32_t)(units * ncols));
-    static const bool split = [] {
-        const char *e = getenv("ZKGPU_NTT_SPLIT");
-        return !e || atoi(e) != 0;
-    }();
-    if (inverse && split)
+    if (inverse)
         hipLaunchKernelGGL((k_ntt_pass<L1, L2, true, true>), grid, dim3(16 << L2), 0, s, a);
-    else if (inverse)
-        hipLaunchKernelGGL((k_ntt_pass<L1, L2, true, false>), grid, dim3(16 << L2), 0, s, a);
-    else if (split)
-        hipLaunchKernelGGL((k_ntt_pass<L1, L2, false, true>), grid, dim3(16 << L2), 0, s, a);
     else
-        hipLaunchKernelGGL((k_ntt_pass<L1, L2, false, false>), grid, dim3(16 << L2), 0, s, a);
+        hipLaunchKernelGGL((k_ntt_pass<L1, L2, false, true>), grid, dim3(16 << L2), 0, s, a);
 }
 
 static void dispatch_pass(uint32_t logr, const PassArgs &a, uint64_t ncols, int inverse, hipStream_t s)
@@ -573,11 +561,7 @@ int ntt_columns(Ctx &ctx, uint64_t *dst, uint64_t dst_ld, const uint64_t *src, u
         return check_launch("k_ntt_small");
     }
     PassArgs a;
-    static const bool twr_table = [] {  // A/B switch: omega_R from the table or from the 2-level product
-        const char *e = getenv("ZKGPU_NTT_TWR_TABLE");
-        return !e || atoi(e) != 0;
-    }();
-    a.rt4096 = twr_table ? ctx.rt_small[d] : nullptr;
+    a.rt4096 = ctx.rt_small[d];  // omega_R from the table (+0.6 % against the 2-level product)
     a.tw_lo = ctx.tw_lo[d];
     a.tw_hi = ctx.tw_hi[d];
     a.logn = logn;
@@ -602,11 +586,7 @@ int ntt_columns(Ctx &ctx, uint64_t *dst, uint64_t dst_ld, const uint64_t *src, u
             // zero-padded forward input: exactly the rows j1 >= R1/2 of every
             // sub-DFT (positions (R2 j1 + j2) * n / R) are past src_valid
             const uint32_t l1 = rb / 2;  // launch_pass<L1 = rb/2, L2 = rb - L1>
-            static const bool half_env = [] {  // A/B switch
-                const char *e = getenv("ZKGPU_NTT_HALF");
-                return !e || atoi(e) != 0;
-            }();
-            a.half_zero = (half_env && !inverse && l1 >= 1 && src_valid == (1ULL << (logn - 1))) ? 1u : 0u;
+            a.half_zero = (!inverse && l1 >= 1 && src_valid == (1ULL << (logn - 1))) ? 1u : 0u;
         } else {
             a.src = tmp;
             a.src_ld = tmp_ld;
@@ -695,7 +675,6 @@ struct StridedArgs {
     uint32_t canon;         // 1 = canonical output (P3)
     uint32_t ncols;
     uint32_t units;         // workgroups per column
-    uint32_t xcd;           // 1 = XCD-aware order (below)
 };
 
 // One sub-DFT of size R = 2^LA = 64 * T per group; G = 256 / T groups
@@ -712,21 +691,11 @@ __global__ void __launch_bounds__(SP_THREADS) k_lde_strided(StridedArgs a)
     constexpr int LT = LA - 6, T = 1 << LT, G = SP_THREADS / T, M = 64 / T;
     constexpr int ROW = T * G + (G < 32 ? G : 0);
     __shared__ uint32_t lds[64 * ROW];
-    // xcd: workgroup b runs on XCD b % 8; give each XCD a contiguous range of
-    // (column, unit) with units fastest, so that the workgroups sharing 128-byte
-    // lines (neighbouring units) run at the same time behind the same L2.
-    // Otherwise columns fastest (the outer-twiddle slice of a unit stays in L2).
-    uint32_t col;
-    uint64_t unit;
-    if (a.xcd) {
-        const uint32_t nb = gridDim.x, b = blockIdx.x;
-        const uint32_t lb = (b & 7) * (nb >> 3) + (b >> 3);
-        col = lb / a.units;
-        unit = lb % a.units;
-    } else {
-        col = blockIdx.x % a.ncols;
-        unit = blockIdx.x / a.ncols;
-    }
+    // columns fastest (the outer-twiddle slice of a unit stays in L2; an
+    // XCD-aware order -- each XCD a contiguous range of (column, unit), units
+    // fastest -- measured slower, 46.3 vs 48.0 Gelem/s)
+    const uint32_t col = blockIdx.x % a.ncols;
+    const uint64_t unit = blockIdx.x / a.ncols;
     const uint64_t g0 = unit * G;
     const int tid = threadIdx.x, g = tid % G, t = tid / G;
     const uint64_t rs = a.row_stride;
@@ -974,12 +943,7 @@ static void launch_strided(const StridedArgs &a, uint64_t units, int inverse, hi
 static void dispatch_strided(uint32_t la, StridedArgs a, uint64_t groups, int inverse, hipStream_t s)
 {
     const uint64_t units = groups / (SP_THREADS >> (la - 6));
-    static const int xcd_env = [] {  // measured slower (46.3 vs 48.0 Gelem/s): off unless asked for
-        const char *e = getenv("ZKGPU_LDE3_XCD");
-        return e ? atoi(e) : 0;
-    }();
     a.units = (uint32_t)units;
-    a.xcd = (xcd_env && (units * a.ncols) % 8 == 0) ? 1u : 0u;
     switch (la) {
     case 6: launch_strided<6>(a, units, inverse, s); break;
     case 7: launch_strided<7>(a, units, inverse, s); break;

@@ -775,12 +775,7 @@ extern "C" int zkgpu_zxp_compile(const void *instr, uint32_t n_instr, const void
     // the producer's order, in which each constraint is folded into the
     // accumulator as soon as it is computed (the 2^23 config-4 quotient: 186
     // VGPRs in source order, 512 + spills scheduled).
-    // ZKGPU_ZXP_SCHED = 0 never, 1 always, unset: by that estimate.
-    static const int sched_env = [] {
-        const char *e = getenv("ZKGPU_ZXP_SCHED");
-        return e ? atoi(e) : -1;
-    }();
-    const bool sched_on = sched_env < 0 ? source_peak_live(in, n_instr, op) > 96 : sched_env != 0;
+    const bool sched_on = source_peak_live(in, n_instr, op) > 96;
     Scheduled sp;
     if (sched_on) {
         schedule(in, n_instr, op, n_opnd, n_tmp1, n_tmp3, sp);

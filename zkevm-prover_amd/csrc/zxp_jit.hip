@@ -284,27 +284,19 @@ int rtc_compile(const std::string &src, std::vector<char> &code)
     // each term's limb reads into 16+8-byte loads (-O1 does not run it).
     // Otherwise -O1 (-O2 is no faster there: the scheduler hoists more scalar
     // loads, e.g. step42ns without LDS 14.1 -> 16.7 ms).  Compile time is about
-    // the same.  ZKGPU_ZXP_JIT_OPT overrides.
+    // the same.
     const bool klds = src.find("#define ZKJIT_KL_LDS 1") != std::string::npos;
-    const std::string olev = [&] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_OPT");
-        const int o = e ? atoi(e) : (klds ? 2 : 1);
-        return std::string("-O") + std::to_string(o >= 0 && o <= 3 ? o : 1);
-    }();
+    const char *olev = klds ? "-O2" : "-O1";
     // The GCN scheduler's re-scheduling stages (unclustered high-pressure and
     // clustered low-occupancy) re-run the scheduler over every region and
     // doubled the compile time of the large programs; register pressure is
     // already bounded by the ZXP scheduler (csrc/zxp_compile.cpp), so they
-    // are off unless ZKGPU_ZXP_JIT_RESCHED=1.
+    // are off for them.
     // Small programs keep them: there they lower register pressure (config-4
     // quotient 17.2 -> 15.2 ms, FRI polynomial 10.4 -> 9.1 ms at 2^23) and
     // cost little compile time.
-    static const int resched_env = [] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_RESCHED");
-        return e ? atoi(e) : -1;
-    }();
-    const bool resched = resched_env < 0 ? src.find("#define ZKJIT_SPLIT 1") == std::string::npos : resched_env != 0;
-    std::vector<const char *> opts = {"--offload-arch=gfx950", olev.c_str(), "-std=c++17"};
+    const bool resched = src.find("#define ZKJIT_SPLIT 1") == std::string::npos;
+    std::vector<const char *> opts = {"--offload-arch=gfx950", olev, "-std=c++17"};
     if (!resched) {
         opts.push_back("-mllvm");
         opts.push_back("-amdgpu-disable-unclustered-high-rp-reschedule=1");
@@ -364,9 +356,9 @@ static std::string cache_key(const std::string &src)
     };
     mix(src.data(), src.size());
     char opt[160];
-    snprintf(opt, sizeof(opt), "hiprtc%d.%d hip%d gfx950 opt%s resched%s", major, minor, (int)HIP_VERSION,
-             getenv("ZKGPU_ZXP_JIT_OPT") ? getenv("ZKGPU_ZXP_JIT_OPT") : "-",
-             getenv("ZKGPU_ZXP_JIT_RESCHED") ? getenv("ZKGPU_ZXP_JIT_RESCHED") : "-");
+    // ("opt- resched-": the compile options are a function of the source,
+    // which is hashed above; the text keeps the keys of existing entries)
+    snprintf(opt, sizeof(opt), "hiprtc%d.%d hip%d gfx950 opt- resched-", major, minor, (int)HIP_VERSION);
     mix(opt, strlen(opt));
     char key[64];
     snprintf(key, sizeof(key), "zxp_%016llx%016llx.co", (unsigned long long)h1, (unsigned long long)h2);
@@ -443,37 +435,24 @@ int code_object(const std::string &src, std::vector<char> &code, bool *cached = 
 
 }  // namespace
 
-// ZKGPU_ZXP_JIT_KLDS: 0 never, 1 (default) for limb tables of at least
-// JIT_KL_LDS_MIN words, 2 always.  Measured on the config-4 STARK at 2^23:
+// Limb tables of at least JIT_KL_LDS_MIN words are staged in LDS.  Measured
+// on the config-4 STARK at 2^23:
 // step42ns (4.1 K words) 14.1 -> 12.4 ms; step52ns (0.4 K words) is
 // 9.2 -> 14.4 ms with LDS (its VGPRs go 74 -> 198), so small tables stay on
 // scalar loads.
 constexpr size_t JIT_KL_LDS_MIN = 1024;
 static bool jit_kl_lds(size_t nkl)
 {
-    static const int mode = [] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_KLDS");
-        return e ? atoi(e) : 1;
-    }();
-    if (!mode || !nkl || nkl * 4 > JIT_KL_LDS_MAX) return false;
-    return mode == 2 || nkl >= JIT_KL_LDS_MIN;
+    if (!nkl || nkl * 4 > JIT_KL_LDS_MAX) return false;
+    return nkl >= JIT_KL_LDS_MIN;
 }
 
-// Rows per thread of a compiled kernel (ZKGPU_ZXP_JIT_ROWS 1 / 2 / 4, default
-// 1): with 2 rows each wave-uniform limb read from LDS, column pointer and
-// instruction serves 128 rows and two independent chains hide each other's
-// load latency -- measured equal to 1 row at twice the occupancy on the
-// zkEVM-sized quotient (0.557 vs 0.547 s at 2^24 rows), so it stays an option.
-static uint32_t jit_rows(bool large)
-{
-    static const int env = [] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_ROWS");
-        return e ? atoi(e) : 0;
-    }();
-    if (env == 1 || env == 2 || env == 4) return (uint32_t)env;
-    (void)large;  // measured: 2 rows x 2 waves == 1 row x 4 waves on the zkEVM-sized quotient
-    return 1;
-}
+// Rows per thread of a compiled kernel: one.  (With 2 rows each
+// wave-uniform limb read from LDS, column pointer and instruction serves 128
+// rows and two independent chains hide each other's load latency -- measured
+// equal to 1 row at twice the occupancy on the zkEVM-sized quotient, 0.557 vs
+// 0.547 s at 2^24 rows; the generator keeps the row expansion.)
+static uint32_t jit_rows(bool) { return 1; }
 
 // every line holding a ` is written once per row r (` -> _r, ~ -> r)
 static std::string expand_rows(const std::string &text, uint32_t rows)
@@ -670,12 +649,8 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             }
         }
     }
-    static const bool imm_stores = [] {  // ZKGPU_ZXP_JIT_IMMST=0: every store deferred (the round-2 form)
-        const char *e = getenv("ZKGPU_ZXP_JIT_IMMST");
-        return !e || atoi(e) != 0;
-    }();
     auto store_now = [&](uint32_t sec, uint32_t col) {
-        return imm_stores && sec != ZXP_SEC_SCRATCH && !read_cols.count({sec, col});
+        return sec != ZXP_SEC_SCRATCH && !read_cols.count({sec, col});
     };
     std::map<std::pair<uint32_t, int32_t>, uint32_t> wreg;
     std::vector<std::pair<uint32_t, int32_t>> wcell;  // register -> (slot, shift)
@@ -867,11 +842,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     // instructions before their DOT are streamed.
     // Small programs (< 1,000 compiled instructions: one or two Horner
     // accumulators over the whole program) stream without limit.
-    static const int64_t stream_span_env = [] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_STREAM_SPAN");
-        return (int64_t)(e ? atol(e) : -1);
-    }();
-    const int64_t stream_span = stream_span_env >= 0 ? stream_span_env : (in.n_instr < 1000 ? INT64_MAX / 4 : 24);
+    const int64_t stream_span = in.n_instr < 1000 ? INT64_MAX / 4 : 24;
     {
         uint32_t nt = 0;
         for (uint32_t k = 0; k < in.n_instr; k++)
@@ -879,13 +850,8 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         streamed_term.assign(nt, 0);
     }
     // Large programs (block-split, below) choose per DOT where to open its
-    // accumulators by a register cost (ZKGPU_ZXP_JIT_STREAM=span: the span
-    // rule above for every program)
-    static const int stream_mode_env = [] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_STREAM");
-        return e ? (strcmp(e, "span") ? 1 : 0) : 1;
-    }();
-    const bool cost_stream = stream_mode_env && (in.n_instr >= 1000 || in.force_split);
+    // accumulators by a register cost
+    const bool cost_stream = in.n_instr >= 1000 || in.force_split;
     std::vector<int64_t> last_read(in.n_opnd ? in.n_opnd : 1, -1);  // per SSA operand
     for (uint32_t k = 0; k < in.n_instr; k++) {
         const zxp_instr &I = in.ins[k];
@@ -897,15 +863,10 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             if (I.op != ZXP_COPY && I.b < last_read.size()) last_read[I.b] = k;
         }
     }
-    // Only programs of ZKGPU_ZXP_JIT_SPLIT_MIN (1000) compiled instructions or
-    // more are split: the opaque branch costs registers (config-4 FRI
-    // polynomial: 74 -> 200 VGPRs, 9 -> 57 ms), and small programs compile in
-    // seconds as one block.
-    static const uint32_t split_min = [] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_SPLIT_MIN");
-        return (uint32_t)(e ? atol(e) : 1000);
-    }();
-    const bool split = in.n_instr >= split_min || in.force_split;
+    // Only programs of 1000 compiled instructions or more are split: the
+    // opaque branch costs registers (config-4 FRI polynomial: 74 -> 200
+    // VGPRs, 9 -> 57 ms), and small programs compile in seconds as one block.
+    const bool split = in.n_instr >= 1000 || in.force_split;
     // ---- fused column chains (the FRI polynomial, step52ns) -------------
     // A Horner chain over committed columns compiles to a chain of DOTs of at
     // most max_terms terms, each carrying the previous one as an F_p^3 term;
@@ -921,31 +882,20 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     // Same values (the chain sum is linear; accumulators are reduced every
     // FUSE_PIECE columns).  Measured (A/B on one box): zkEVM-shaped FRI
     // polynomial at 2^23 rows 69.4 -> 38.4 ms with 4 column loads in flight
-    // per iteration, 33.5 ms with 8 (ZKGPU_ZXP_JIT_FUSE_U); the config-4 one
+    // per iteration, 33.5 ms with 8 (FUSE_U); the config-4 one
     // (397 column terms) 9.3 -> 10.4 ms with 4, 8.1 ms with 8.  Small chains
     // inside other programs (config-4 quotient, step3prev: 20-24 columns)
     // ran slower fused, so a program is fused only when its chains hold at
-    // least half of its column terms and ZKGPU_ZXP_JIT_FUSE_MIN (128) or more
-    // -- the FRI polynomials.  ZKGPU_ZXP_JIT_FUSE=0 disables.
+    // least half of its column terms and fuse_min (128) or more -- the FRI
+    // polynomials.
     constexpr int FUSE_MAX = 4;
     constexpr uint32_t FUSE_PIECE = 224;
-    static const int fuse_env = [] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_FUSE");
-        return e ? atoi(e) : 1;
-    }();
-    static const size_t fuse_min = [] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_FUSE_MIN");
-        return (size_t)(e ? atol(e) : 128);
-    }();
-    static const size_t fuse_u = [] {  // column loads in flight per fused-loop iteration
-        const char *e = getenv("ZKGPU_ZXP_JIT_FUSE_U");
-        const long u = e ? atol(e) : 8;
-        return (size_t)(u == 2 || u == 8 || u == 16 ? u : 4);
-    }();
+    constexpr size_t fuse_min = 128;
+    constexpr size_t fuse_u = 8;  // column loads in flight per fused-loop iteration
     std::vector<int32_t> fused(in.n_instr, -1);  // chain of a fused link
     std::vector<std::vector<uint32_t>> fchains;   // links in order, per fused chain
     uint32_t fuse_at = UINT32_MAX;                // where the fused chains are evaluated
-    if (!split && fuse_env) {
+    if (!split) {
         // a link: DOT3 whose terms are column reads (columns the program never
         // writes), constants, and the whole previous link (its only reader)
         std::map<uint32_t, uint32_t> def_at;  // SSA operand -> defining instruction
@@ -1190,7 +1140,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         if (first_use[k] != UINT32_MAX) declare_at[first_use[k]].push_back(k);
     // Compile time: LLVM's instruction selection and machine scheduler are
     // superlinear in basic-block size (a 600-instruction program took ~60 s
-    // as one block).  Every ZKGPU_ZXP_JIT_BLOCK source bytes the body opens a
+    // as one block).  Every `block` (1 KB) of source the body opens a
     // new block behind a uniform branch on an opaque 1 (zk_one(): an
     // s_mov_b32 the optimiser cannot see through, so it cannot merge the
     // blocks back), so each block is compiled on its own.  The block size also
@@ -1198,12 +1148,8 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     // step42ns-shaped program at 2^24 rows, 256 / 512 / 1024 / 4096 bytes ->
     // 184 / 246 / 246 / 512+spills VGPRs, 453 / 359 / 303 / 394 ms, hiprtc
     // 63 / 56 / 80 / 116 s.
-    static const size_t block = [] {  // source bytes per block
-        const char *e = getenv("ZKGPU_ZXP_JIT_BLOCK");
-        const long b = e ? atol(e) : 1024;
-        return (size_t)(b > 0 ? b : 1L << 40);
-    }();
-    // Limb chunks in LDS (ZKGPU_ZXP_JIT_KCHUNK): a split program whose limb
+    constexpr size_t block = 1024;  // source bytes per block
+    // Limb chunks in LDS: a split program whose limb
     // table is too large for LDS reads it from global memory, one wave-uniform
     // 16 + 8-byte vector load pair per term, each taking the texture
     // addresser's full 64-lane path.  In this mode the table is rewritten in
@@ -1212,13 +1158,9 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     // chunk into the other half of an LDS double buffer (one 16-byte load per
     // thread, issued at the block's start) and a barrier closes each block.
     // Quarter-size step42ns-shaped program at 2^24 rows: 251 -> 189 ms
-    // (global vector loads of the limbs 25 K -> 6.7 K per wave).  Default on
-    // for split programs; ZKGPU_ZXP_JIT_KCHUNK=0 disables.
-    static const int kchunk_env = [] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_KCHUNK");
-        return e ? atoi(e) : 1;
-    }();
-    const bool kchunk = split && kchunk_env > 0;
+    // (global vector loads of the limbs 25 K -> 6.7 K per wave).  Every split
+    // program.
+    const bool kchunk = split;
     std::vector<uint32_t> kl2;
     size_t blk_lo = 0, blk_no = 0;
     auto kmap = [&](size_t off, size_t n) -> size_t {  // n words of kl at off, in emission order
@@ -1245,31 +1187,19 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             }
         }
     };
-    // ZKGPU_ZXP_JIT_SYNC=n: a workgroup barrier every n blocks keeps the
-    // workgroup's waves in the same stretch of code, so an instruction-cache
-    // line fetched for one wave serves the others (experiment, default off)
-    static const int sync_every = [] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_SYNC");
-        return e ? atoi(e) : 0;
-    }();
-    // ZKGPU_ZXP_JIT_KSYNC=1: a new limb chunk (and so a workgroup barrier)
-    // at every code block, the round-3 form; default 0: a chunk spans as many
-    // code blocks as its limbs fill (a barrier every ~3-4 blocks instead of
-    // every block)
-    static const int ksync = [] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_KSYNC");
-        return e ? atoi(e) : 0;
-    }();
-    size_t block_start = 0, n_blocks = 0;
+    // A limb chunk spans as many code blocks as its limbs fill (a workgroup
+    // barrier every ~3-4 blocks; a chunk and barrier per block, the round-3
+    // form, measured 43.3 against 45.4 Mrow/s on the zkEVM-sized quotient)
+    size_t block_start = 0;
     auto chunk_head = [&] {  // LDS base of this chunk; the next chunk's start patched in at the end
         appendf(body, "const uint32_t *K = kbuf + %d - %zu; pf_ = kpre(p.kl, @KLO%zu@);\n",
                 (int)(blk_no & 1) * JIT_KCHUNK, blk_lo, blk_no + 1);
     };
     std::vector<size_t> klo_of;  // chunk start of chunk b
     auto maybe_split = [&] {
-        const bool full = kchunk && kl2.size() - blk_lo > JIT_KCHUNK - (ksync ? 512 : 256);
+        const bool full = kchunk && kl2.size() - blk_lo > JIT_KCHUNK - 256;
         if (split && (body.size() - block_start >= block || full)) {
-            if (kchunk && (ksync || full)) {
+            if (full) {
                 appendf(body, "kput(kbuf + %d, pf_);\n}\n__syncthreads();\n", (int)((blk_no + 1) & 1) * JIT_KCHUNK);
                 blk_lo = kl2.size();
                 blk_no++;
@@ -1280,9 +1210,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                 appendf(body, "}\nif (zk_one()) {\nconst uint32_t *K = kbuf + %d - %zu;\n", (int)(blk_no & 1) * JIT_KCHUNK,
                         blk_lo);
             } else {
-                body += "}\n";
-                if (sync_every > 0 && ++n_blocks % sync_every == 0) body += "__syncthreads();\n";
-                body += "if (zk_one()) { ZK_KREFRESH\n";
+                body += "}\nif (zk_one()) { ZK_KREFRESH\n";
             }
             block_start = body.size();
         }
@@ -1530,9 +1458,9 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     }
     // assemble: prelude, params, declarations, body, deferred stores
     // Address space of the wave-uniform tables a kernel reads from global
-    // memory (ZKGPU_ZXP_JIT_KAS: the DOT limb table when not in LDS,
-    // ZKGPU_ZXP_JIT_CPAS: the column pointers; 0 generic = FLAT loads,
-    // 1 global = vector loads, 4 constant = scalar loads).  Block-split
+    // memory (kas: the DOT limb table when not in LDS, cpas: the column
+    // pointers; 0 generic = FLAT loads, 1 global = vector loads, 4 constant
+    // = scalar loads).  Block-split
     // programs hide their limb table base behind an asm copy per block (so it
     // is not provably uniform and was read with FLAT loads, which also count
     // on LGKM_CNT) and loaded every column pointer with a vector load ahead of
@@ -1541,76 +1469,39 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     // 277, global/scalar 251 (default for split programs), scalar/scalar 293
     // (scalar limbs: 106 SGPRs, spills).  Small programs keep the compiler's
     // choice (their limbs already come from scalar loads).
-    static const int kas_env = [] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_KAS");
-        return e ? atoi(e) : -1;
-    }();
-    static const int cpas_env = [] {
-        const char *e = getenv("ZKGPU_ZXP_JIT_CPAS");
-        return e ? atoi(e) : -1;
-    }();
-    const int kas = kas_env < 0 ? (split ? 1 : 0) : kas_env;
-    const int cpas = cpas_env < 0 ? (split ? 4 : 0) : cpas_env;
+    const int kas = split ? 1 : 0;
+    const int cpas = split ? 4 : 0;
     src.clear();
     if ((kas == 1 || kas == 4) && !kchunk && !jit_kl_lds(kl.size()))
         appendf(src, "#define ZK_LIMB_AS __attribute__((address_space(%d)))\n", kas);
     if (cpas == 1 || cpas == 4) appendf(src, "#define ZK_CP_AS __attribute__((address_space(%d)))\n", cpas);
-    {
-        // ZKGPU_ZXP_JIT_RB=1: field add / sub with the rare second correction
-        // behind a wave-uniform branch (gl_device.hpp ZK_RB)
-        static const int rb = [] {
-            const char *e = getenv("ZKGPU_ZXP_JIT_RB");
-            return e ? atoi(e) : 0;
-        }();
-        if (rb) src += "#define ZK_RB 1\n";
-    }
-    {
-        // DOT limb reads (gl_device.hpp Dot3::term_al): explicit 16 + 8-byte
-        // loads for the split programs' LDS chunks (-O1), the struct copy the
-        // -O2 vectorizer merges for the others; ZKGPU_ZXP_JIT_LIMB_STRUCT
-        // forces one form (1 struct, 0 vector) for A/B
-        const char *e = getenv("ZKGPU_ZXP_JIT_LIMB_STRUCT");
-        if (e ? atoi(e) != 0 : !kchunk) src += "#define ZK_LIMB_STRUCT 1\n";
-    }
+    // (field add / sub keep their second correction as a select: with the
+    // wave-uniform branch of gl_device.hpp ZK_RB the branches split the long
+    // straight-line blocks, zkEVM-shaped quotient 39.9 -> 32.8 Mrow/s)
+    // DOT limb reads (gl_device.hpp Dot3::term_al): explicit 16 + 8-byte
+    // loads for the split programs' LDS chunks (-O1), the struct copy the -O2
+    // vectorizer merges for the others
+    if (!kchunk) src += "#define ZK_LIMB_STRUCT 1\n";
     src += k_gl_device_src;
     appendf(src, "#define ZKJIT_KL_LDS %d\n", !kchunk && jit_kl_lds(kl.size()) ? 1 : 0);
     appendf(src, "#define ZKJIT_SPLIT %d\n", split ? 1 : 0);
     appendf(src, "#define ZKJIT_KL_CHUNK %d\n", kchunk ? JIT_KCHUNK : 0);  // large program: compile-time options (rtc_compile)
-    {
-        static const int unroll = [] {  // column terms per loop iteration (loads in flight)
-            const char *e = getenv("ZKGPU_ZXP_JIT_UNROLL");
-            const int u = e ? atoi(e) : 4;
-            return (u == 2 || u == 4 || u == 8 || u == 16) ? u : 4;
-        }();
-        appendf(src, "#define ZKJIT_UNROLL %d\n", unroll);
-    }
+    // column terms per DOT-loop iteration (loads in flight; 8 / 16 measured neutral)
+    src += "#define ZKJIT_UNROLL 4\n";
     if (in.waves_per_eu)
         appendf(src, "#define ZKJIT_WAVES __attribute__((amdgpu_waves_per_eu(%u)))\n", in.waves_per_eu);
     else
         src += "#define ZKJIT_WAVES\n";
     const uint32_t rows = jit_rows(split);
     appendf(src, "#define ZKJIT_ROWS %u\n", rows);
+    // 32-bit column offsets from scalar bases (64-bit addresses, the round-3
+    // form: 44.6 against 46.3 Mrow/s on the zkEVM-sized quotient)
+    src += "#define ZKJIT_SADDR 1\n";
     {
-        // ZKGPU_ZXP_JIT_SADDR=0: 64-bit column addresses (the round-3 form)
-        static const int saddr = [] {
-            const char *e = getenv("ZKGPU_ZXP_JIT_SADDR");
-            return e ? atoi(e) : 1;
-        }();
-        appendf(src, "#define ZKJIT_SADDR %d\n", saddr ? 1 : 0);
-    }
-    {
-        // LDS column cache (lds_column_cache): block-split programs;
-        // ZKGPU_ZXP_JIT_LCACHE slots per lane and row (LDS: 2 KB per slot, row
-        // and workgroup), ZKGPU_ZXP_JIT_LCACHE_GAP reads left to the caches
-        static const int lslots = [] {
-            const char *e = getenv("ZKGPU_ZXP_JIT_LCACHE");
-            const int v = e ? atoi(e) : 12;
-            return v < 0 ? 0 : v > 32 ? 32 : v;
-        }();
-        static const int lgap = [] {
-            const char *e = getenv("ZKGPU_ZXP_JIT_LCACHE_GAP");
-            return e ? atoi(e) : 0;
-        }();
+        // LDS column cache (lds_column_cache): block-split programs, 12
+        // slots per lane and row (LDS: 2 KB per slot, row and workgroup; 16
+        // slots measured +2 % on one box, -5 % on another)
+        constexpr int lslots = 12, lgap = 0;
         // LDS budget of one workgroup (64 KB): the limb double buffer (kbuf)
         // or the whole limb table, then as many cache slots as still fit
         // (none: the uncached source)
@@ -1828,26 +1719,12 @@ int launch_all(std::vector<JitKernel> &ks, const ZxpJitIn &in, hipStream_t s)
     return 0;
 }
 
-// Segments of a large program (csrc/zxp_segment.hpp).  ZKGPU_ZXP_SEGMENTS:
-// 0 never, n > 0 exactly n (programs of >= 2 * n instructions), unset: one
-// segment per ZKGPU_ZXP_SEG_COST of estimated VALU work for programs of
-// >= ZKGPU_ZXP_SEG_MIN (2,000) compiled instructions.
+// Segments of a large program (csrc/zxp_segment.hpp): one per seg_cost of
+// estimated VALU work for programs of >= seg_min compiled instructions.
 uint32_t segments_for(const zxp_compiled &cp)
 {
-    static const int env_n = [] {
-        const char *e = getenv("ZKGPU_ZXP_SEGMENTS");
-        return e ? atoi(e) : -1;
-    }();
-    static const uint64_t seg_cost = [] {
-        const char *e = getenv("ZKGPU_ZXP_SEG_COST");
-        return (uint64_t)(e && atoll(e) > 0 ? atoll(e) : 50000);
-    }();
-    static const uint32_t seg_min = [] {
-        const char *e = getenv("ZKGPU_ZXP_SEG_MIN");
-        return (uint32_t)(e ? atoi(e) : 2000);
-    }();
-    if (env_n == 0) return 1;
-    if (env_n > 0) return cp.n_instr >= 2u * (uint32_t)env_n ? (uint32_t)env_n : 1;
+    constexpr uint64_t seg_cost = 50000;
+    constexpr uint32_t seg_min = 2000;
     if (cp.n_instr < seg_min) return 1;
     uint64_t cost = 0;
     for (uint32_t k = 0; k < cp.n_instr; k++) cost += zxp_instr_cost(cp, k);
@@ -1929,12 +1806,8 @@ int build_kernels(const ZxpJitIn &in, std::vector<JitKernel> &ks, const std::fun
         // lets the scheduler spend registers: FRI polynomial 8.9 -> 9.2 ms),
         // as are block-split programs (registers bounded by their blocks).
         // Decided from the code object's metadata, so the prebuilt cache and
-        // the run agree.  ZKGPU_ZXP_JIT_AUTOWAVES=0 disables.
-        static const bool auto_waves = [] {
-            const char *e = getenv("ZKGPU_ZXP_JIT_AUTOWAVES");
-            return !e || atoi(e) != 0;
-        }();
-        if (auto_waves && in.waves_per_eu == 0 && only <= 0 &&
+        // the run agree.
+        if (in.waves_per_eu == 0 && only <= 0 &&
             ks[0].src.find("#define ZKJIT_SPLIT 1") == std::string::npos) {
             uint32_t w = 0;
             if (!waves_known(ks[0].src, w)) {
@@ -1967,35 +1840,25 @@ int build_kernels(const ZxpJitIn &in, std::vector<JitKernel> &ks, const std::fun
         J.n_opnd = (uint32_t)seg[j].opnd.size();
         J.terms = seg[j].term.data();
         J.force_split = 1;
-        // occupancy target of a segment (ZKGPU_ZXP_SEG_WAVES, default 4 waves
-        // per SIMD = 128 VGPRs): zkEVM-sized quotient at 2^24 rows 0.57 s
-        // with the compiler's choice (~250 VGPRs), 0.55 s at 4 waves
-        // A segment whose code spills more than ZKGPU_ZXP_SEG_SPILL_MAX bytes
-        // per lane (default 300) at that target is compiled again one wave
+        // occupancy target of a segment (seg_waves, 4 waves per SIMD = 128
+        // VGPRs): zkEVM-sized quotient at 2^24 rows 0.57 s with the compiler's
+        // choice (~250 VGPRs), 0.55 s at 4 waves
+        // A segment whose code spills more than spill_max bytes per lane
+        // (300) at that target is compiled again one wave
         // lower (down to 2): the reference's step3 segments spill 324-452
         // bytes at 4 waves, none at 2.  Small spills stay: on the synthetic
         // quotient (<= 272 bytes) 4 waves with spills ran 0.54 s, the
         // spill-free lower targets 0.58 s -- it is HBM-bound, occupancy buys
-        // bandwidth.  ZKGPU_ZXP_SEG_ADAPT=0 keeps the first target.
-        static const uint32_t seg_waves = [] {
-            const char *e = getenv("ZKGPU_ZXP_SEG_WAVES");
-            return (uint32_t)(e ? atoi(e) : 4);
-        }();
-        static const bool adapt = [] {
-            const char *e = getenv("ZKGPU_ZXP_SEG_ADAPT");
-            return !e || atoi(e) != 0;
-        }();
-        static const uint64_t spill_max = [] {
-            const char *e = getenv("ZKGPU_ZXP_SEG_SPILL_MAX");
-            return (uint64_t)(e ? atoll(e) : 300);
-        }();
+        // bandwidth.
+        constexpr uint32_t seg_waves = 4;
+        constexpr uint64_t spill_max = 300;
         const bool fixed = J.waves_per_eu != 0;
         J.scratch = scr;
         J.scratch_ld = dom;
         uint32_t w = fixed ? J.waves_per_eu : seg_waves;
         J.waves_per_eu = w;
         if ((rc = prepare(J, ks[j]))) return rc;  // 1: unsupported shape -> interpreter for the whole program
-        if (!fixed && adapt && (only < 0 || (size_t)only == j)) {
+        if (!fixed && (only < 0 || (size_t)only == j)) {
             const std::string first = ks[j].src;
             uint32_t wk = 0;
             if (waves_known(first, wk)) {
@@ -2074,10 +1937,10 @@ extern "C" int zkgpu_zxp_jit_source(const void *instr, uint32_t n_instr, const v
     J.publics = publics;
     J.evals = evals;
     J.n_opnd = cp.n_opnd;
-    // the same environment overrides as zkgpu_zxp_eval_dev (api.hip), so the
-    // sources (and cache keys) match
-    J.dot_loop_min = getenv("ZKGPU_ZXP_JIT_DOTLOOP") ? (uint32_t)atoi(getenv("ZKGPU_ZXP_JIT_DOTLOOP")) : 8;
-    J.waves_per_eu = getenv("ZKGPU_ZXP_JIT_WAVES") ? (uint32_t)atoi(getenv("ZKGPU_ZXP_JIT_WAVES")) : 0;
+    // the same settings as zkgpu_zxp_eval_dev (api.hip), so the sources (and
+    // cache keys) match
+    J.dot_loop_min = 8;
+    J.waves_per_eu = 0;
     std::vector<JitKernel> ks;
     static uint64_t dummy_scratch;
     const char *only_env = getenv("ZKGPU_ZXP_JIT_ONLY");

@@ -596,6 +596,43 @@ def h1h2_dev(h1, h1_ld, h2, h2_ld, f, f_ld, t, t_ld, n, dim):
     return None
 
 
+# calculateH1H2 over row-sharded f / t (include/zkgpu.h zkgpu_h1h2_shard_*;
+# host/sharded_starks.hpp h1h2_sharded runs the same steps with exchanges)
+def h1h2_shard_route(recs, cap, f, f_ld, t, t_ld, nrows, row0, dim, world):
+    """-> (n_t, n_f): the rank's bucket sizes per owner"""
+    nt = np.zeros(world, np.uint32)
+    nf = np.zeros(world, np.uint32)
+    _check(lib().zkgpu_h1h2_shard_route(_addr(recs), cap, nt.ctypes.data, nf.ctypes.data, _addr(f), f_ld, _addr(t),
+                                        t_ld, nrows, row0, dim, world), "zkgpu_h1h2_shard_route")
+    return nt, nf
+
+
+def h1h2_shard_owner(ret, recs, nrec, dim):
+    """-> the smallest f row without a table row, or None"""
+    miss = ctypes.c_uint64(0)
+    _check(lib().zkgpu_h1h2_shard_owner(_addr(ret), _addr(recs), nrec, dim, ctypes.byref(miss)),
+           "zkgpu_h1h2_shard_owner")
+    return None if miss.value == (1 << 64) - 1 else miss.value
+
+
+def h1h2_shard_counts(start, cnt, sent, ret, nsent, nrows, row0):
+    """-> the rank's multiset total"""
+    tot = ctypes.c_uint64(0)
+    _check(lib().zkgpu_h1h2_shard_counts(_addr(start), _addr(cnt), ctypes.byref(tot), _addr(sent), _addr(ret), nsent,
+                                         nrows, row0), "zkgpu_h1h2_shard_counts")
+    return tot.value
+
+
+def h1h2_shard_deal(seg, seg_ld, t, t_ld, start, cnt, nrows, dim):
+    _check(lib().zkgpu_h1h2_shard_deal(_addr(seg), seg_ld, _addr(t), t_ld, _addr(start), _addr(cnt), nrows, dim),
+           "zkgpu_h1h2_shard_deal")
+
+
+def h1h2_shard_place(h1, h1_ld, h2, h2_ld, buf, buf_ld, pos0, length, row0, dim):
+    _check(lib().zkgpu_h1h2_shard_place(_addr(h1), h1_ld, _addr(h2), h2_ld, _addr(buf), buf_ld, pos0, length, row0,
+                                        dim), "zkgpu_h1h2_shard_place")
+
+
 def qsplit_dev(qq2, ld2, qq1, ld1, n, q_deg, shift_in):
     _check(lib().zkgpu_qsplit_dev(_addr(qq2), ld2, _addr(qq1), ld1, n, q_deg, shift_in), "zkgpu_qsplit_dev")
 

@@ -26,12 +26,12 @@ FAMILIES = {
 }
 # environment settings that change a family's kernels
 ENV = {
-    "lde": ["ZKGPU_LDE3", "ZKGPU_NTT_RB"],
+    "lde": ["ZKGPU_LDE3"],
     "poseidon": [],
-    # (ZKGPU_ZXP_JIT, interpreter vs compiled, is not one: the profiled
-    # workloads pick the compiled kernels themselves, bench.py --s42-jit)
-    "zxp": ["ZKGPU_ZXP_JIT_LCACHE", "ZKGPU_ZXP_JIT_LCACHE_GAP", "ZKGPU_ZXP_JIT_KCHUNK",
-            "ZKGPU_ZXP_JIT_KLDS", "ZKGPU_ZXP_JIT_ROWS", "ZKGPU_ZXP_JIT_RB", "ZKGPU_ZXP_JIT_UNROLL"],
+    # the compiler's fusion / term cap change the compiled programs (ZKGPU_ZXP_JIT,
+    # interpreter vs compiled, is not one: the profiled workloads pick the
+    # compiled kernels themselves, bench.py --s42-jit)
+    "zxp": ["ZKGPU_ZXP_FUSE", "ZKGPU_ZXP_MAX_TERMS"],
 }
 
 
