@@ -62,8 +62,8 @@ def _sharded_run(cfg, world, comm):
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    for p, (_, err) in zip(procs, outs):
-        assert p.returncode == 0, err
+    bad = [(r, p.returncode, err) for r, (p, (_, err)) in enumerate(zip(procs, outs)) if p.returncode != 0]
+    assert not bad, "\n".join("rank %d exit %s: %s" % b for b in bad)
     return [err for _, err in outs]
 
 
