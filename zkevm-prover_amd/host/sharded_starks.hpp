@@ -274,9 +274,17 @@ public:
         return (uint64_t)info.n_cm1 + info.n_cm2 + info.n_cm3 + info.n_cm4 + info.n_const + 20ULL * info.n_bits_ext;
     }
 
+    // Collective: every rank calls it at the same point of the proof, with
+    // whatever it has to send and receive -- possibly nothing (a rank whose
+    // multiset segment is all its own rows, calculateH1H2): the host exchange
+    // is a barrier per call, so a rank that skipped an empty exchange would
+    // pair its next one with the others' current one.
     int exchange()
     {
-        if (ops.empty()) return 0;
+        if (W == 1) {
+            ops.clear();
+            return 0;
+        }
         max_ops = std::max(max_ops, (uint32_t)ops.size());
         if (ops.size() > 2ULL * (W - 1)) {
             // still enter the collective exchange, with nothing posted: the
@@ -287,8 +295,11 @@ public:
             (void)comm.exchange(comm.ctx, ops.data(), 0);
             return fail("exchange of %zu operations: more than one send and one receive per peer", n);
         }
-        if (comm.exchange(comm.ctx, ops.data(), (uint32_t)ops.size()))
-            return fail("zkgpu_comm exchange of %zu operations failed (rank %u of %u)", ops.size(), R, W);
+        if (comm.exchange(comm.ctx, ops.data(), (uint32_t)ops.size())) {
+            const std::string why = last_error_text();
+            return fail("zkgpu_comm exchange of %zu operations failed (rank %u of %u): %s", ops.size(), R, W,
+                        why.c_str());
+        }
         uint64_t sent = 0;
         for (const zkgpu_comm_op &o : ops)
             if (o.send) sent += o.bytes;

@@ -35,6 +35,9 @@ static int fail(const char *fmt, ...)
     va_end(ap);
     return -1;
 }
+// the message of the last fail() on this thread (e.g. a communicator's, before
+// the prover's own wraps it)
+static std::string last_error_text() { return g_err; }
 #define CK(x)                                                                                                  \
     do {                                                                                                       \
         int _rc = (x);                                                                                         \
