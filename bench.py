@@ -148,6 +148,12 @@ def _threads():
 
 
 # ---------------------------------------------------------------- CPU baselines (oracle = checker only)
+# what the CPU baseline is: the checker, not the reference's CPU path
+PORT_NOTE = ("oracle port (scalar C + OpenMP, the textbook dense 12x12 MDS in every Poseidon round), not the "
+             "reference's AVX2 Goldilocks path (absent submodule, unbuildable here): a GPU/CPU ratio against it "
+             "overstates the lead over the reference")
+
+
 def cpu_baseline_stark(sample_bits, blow, ncols, n_queries):
     """Oracle STARK prover (C/OpenMP kernels + numpy driver) on the same
     instance shape at 2^sample_bits rows."""
@@ -162,7 +168,7 @@ def cpu_baseline_stark(sample_bits, blow, ncols, n_queries):
     t0 = time.perf_counter()
     o.prove()
     dt = time.perf_counter() - t0
-    return {"value": round(dt, 3), "unit": "s/proof", "cores": threads, "kind": "port",
+    return {"value": round(dt, 3), "unit": "s/proof", "cores": threads, "kind": "port", "what": PORT_NOTE,
             "sample": "oracle genProof (oracle/stark_prover.py over oracle/*.c) of the config-4 instance shape at "
                       "2^%d rows (%d cm1 cols, %d queries), %.1f s, %d threads (%s)"
                       % (sample_bits, ncols, n_queries, dt, threads, _cpu_model())}
@@ -184,7 +190,8 @@ def cpu_baseline_zkevm(sample_bits, n_queries):
     t0 = time.perf_counter()
     o.prove()
     dt = time.perf_counter() - t0
-    return {"value": round(dt, 3), "unit": "s/proof", "cores": threads, "kind": "port", "rows": 1 << sample_bits,
+    return {"value": round(dt, 3), "unit": "s/proof", "cores": threads, "kind": "port", "what": PORT_NOTE,
+            "rows": 1 << sample_bits,
             "sample": "oracle genProof of the zkEVM-shaped instance (751/168/408/6 committed, 234 constants, the five "
                       "zkEVM-shaped programs, 1,973 evaluations) at 2^%d rows, %d queries, %.1f s, %d threads (%s)"
                       % (sample_bits, n_queries, dt, threads, _cpu_model())}
