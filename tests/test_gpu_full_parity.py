@@ -4,7 +4,9 @@
   trace, 100/26/27/6 committed columns, 128 queries) == the oracle's proof of
   the same instance, field by field: tests/golden/config4_2p23_proof.json,
   written in the build container by tests/golden/make_config4_fixture.py
-  (per-field SHA-256 of the canonical JSON, roots / evals / finalPol verbatim).
+  (per-field SHA-256 of the canonical JSON, roots / evals / finalPol
+  verbatim); likewise the zkEVM-shaped instance at 2^20 rows
+  (zkevm_shaped_2p20_proof.json).
 * The compiled zkEVM-shaped step42ns (constraint quotient, starks.cpp:241) and
   step52ns (FRI polynomial, starks.cpp:371) kernels at their real 2^24-row
   extended domain -- the segment kernels, carries and scratch columns bench.py
@@ -27,13 +29,19 @@ P = 0xFFFFFFFF00000001
 SEC_CONST_2NS, SEC_Q_2NS, SEC_F_2NS = 9, 10, 11
 
 
-def test_config4_2p23_proof_equals_oracle_fixture(zkgpu):
+@pytest.mark.parametrize("fixture", ["config4_2p23_proof.json", "zkevm_shaped_2p20_proof.json"])
+def test_full_size_proof_equals_oracle_fixture(zkgpu, fixture):
+    """config4_2p23: the headline instance at its benchmarked size;
+    zkevm_shaped_2p20: the fork-9 widths with the five zkEVM-shaped programs
+    (the sharded_one_proof.fork9_zkevm_shaped workload) at the largest size
+    whose oracle run fits the build container"""
     import bench
     from zkgpu.stark import GpuStark
     from golden.make_config4_fixture import summarize
-    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "config4_2p23_proof.json")))
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", fixture)))
     i = fx["instance"]
-    inst = bench.stark_instance(i["log_n"], i["blowup_bits"], i["ncols"], i["queries"])
+    kind = "zkevm" if i.get("kind") == "zkevm" else False
+    inst = bench.stark_instance(i["log_n"], i["blowup_bits"], i["ncols"], i["queries"], kind)
     assert [inst.n_cm1, inst.n_cm2, inst.n_cm3, inst.n_cm4] == i["n_cm"] and inst.n_const == i["n_const"]
     g = GpuStark(inst)
     try:
