@@ -11,7 +11,7 @@ for r in 1 2; do
     for v in A B; do
         if [ $v = B ]; then export ZKGPU_LIB_DIR=$PWD/zkevm-prover_amd/lib_ab; else unset ZKGPU_LIB_DIR; fi
         timeout -k 10 300 python bench.py --no-cpu "$@" > gpurun_out/ab_${L}_$v$r.json 2> gpurun_out/ab_${L}_$v$r.err || exit $?
-        echo "$L $v run $r: $(python -c "import json;d=json.load(open('gpurun_out/ab_${L}_$v$r.json'));print(d['value'],d['unit'],(d.get('lde') or {}).get('value',''))")"
+        echo "$L $v run $r: $(python -c "import json;d=json.loads(open('gpurun_out/ab_${L}_$v$r.json').read().strip().splitlines()[-1]);print(d['value'],d['unit'],(d.get('lde') or {}).get('value',''))")"
     done
 done
 unset ZKGPU_LIB_DIR

@@ -30,6 +30,8 @@
 #include <cstring>
 #include <unordered_map>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "../../include/zkgpu.h"
@@ -729,6 +731,75 @@ uint32_t source_peak_live(const zxp_instr *in, uint32_t n, const zxp_operand *op
     return (uint32_t)peak;
 }
 
+// The register-pressure decision and the schedule depend only on the source
+// program's structure (instructions, operand table, temporary pools), never on
+// the challenge / public / eval values -- and a prover compiles the same stage
+// programs every proof (18 ms of the zkEVM-shaped quotient's ~40 ms host
+// compile).  They are kept per process, keyed by the program's bytes (compared
+// in full on a hit), at most SCHED_MEMO entries.
+struct SchedMemo {
+    std::vector<zxp_instr> in;
+    std::vector<zxp_operand> op;
+    uint32_t n_tmp1 = 0, n_tmp3 = 0;
+    bool sched_on = false;
+    Scheduled sp;
+};
+constexpr size_t SCHED_MEMO = 32;
+
+static uint64_t program_hash(const zxp_instr *in, uint32_t n_in, const zxp_operand *op, uint32_t n_opnd)
+{
+    uint64_t h = 0x9E3779B97F4A7C15ULL ^ ((uint64_t)n_in << 32 | n_opnd);
+    auto mix = [&](const void *p, size_t bytes) {
+        const uint8_t *b = (const uint8_t *)p;
+        size_t k = 0;
+        for (; k + 8 <= bytes; k += 8) {
+            uint64_t w;
+            memcpy(&w, b + k, 8);
+            h = (h ^ w) * 0xBF58476D1CE4E5B9ULL;
+            h ^= h >> 31;
+        }
+        for (; k < bytes; k++) h = (h ^ b[k]) * 0x100000001B3ULL;
+    };
+    mix(in, (size_t)n_in * sizeof(zxp_instr));
+    mix(op, (size_t)n_opnd * sizeof(zxp_operand));
+    return h;
+}
+
+static std::shared_ptr<const SchedMemo> scheduled_program(const zxp_instr *in, uint32_t n_in, const zxp_operand *op,
+                                                          uint32_t n_opnd, uint32_t n_tmp1, uint32_t n_tmp3)
+{
+    static std::mutex mu;
+    static std::unordered_map<uint64_t, std::shared_ptr<const SchedMemo>> memo;
+    const uint64_t key = program_hash(in, n_in, op, n_opnd) ^ ((uint64_t)n_tmp1 << 20) ^ ((uint64_t)n_tmp3 << 40);
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = memo.find(key);
+        if (it != memo.end()) {
+            const SchedMemo &m = *it->second;
+            if (m.in.size() == n_in && m.op.size() == n_opnd && m.n_tmp1 == n_tmp1 && m.n_tmp3 == n_tmp3 &&
+                !memcmp(m.in.data(), in, (size_t)n_in * sizeof(zxp_instr)) &&
+                !memcmp(m.op.data(), op, (size_t)n_opnd * sizeof(zxp_operand)))
+                return it->second;
+        }
+    }
+    auto m = std::make_shared<SchedMemo>();
+    m->in.assign(in, in + n_in);
+    m->op.assign(op, op + n_opnd);
+    m->n_tmp1 = n_tmp1;
+    m->n_tmp3 = n_tmp3;
+    // reschedule for register pressure when the source order keeps more than
+    // 96 temporary words live (the zkEVM's bytecode: ~1,200); otherwise keep
+    // the producer's order, in which each constraint is folded into the
+    // accumulator as soon as it is computed (the 2^23 config-4 quotient: 186
+    // VGPRs in source order, 512 + spills scheduled).
+    m->sched_on = source_peak_live(in, n_in, op) > 96;
+    if (m->sched_on) schedule(in, n_in, op, n_opnd, n_tmp1, n_tmp3, m->sp);
+    std::lock_guard<std::mutex> lk(mu);
+    if (memo.size() >= SCHED_MEMO) memo.clear();
+    memo[key] = m;
+    return m;
+}
+
 }  // namespace
 
 extern "C" int zkgpu_zxp_compile(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd,
@@ -770,15 +841,10 @@ extern "C" int zkgpu_zxp_compile(const void *instr, uint32_t n_instr, const void
         if (dk != ZXP_TMP1 && dk != ZXP_TMP3 && dk != ZXP_COL && dk != ZXP_COL3)
             return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u writes a read-only operand", k);
     }
-    // reschedule for register pressure when the source order keeps more than
-    // 96 temporary words live (the zkEVM's bytecode: ~1,200); otherwise keep
-    // the producer's order, in which each constraint is folded into the
-    // accumulator as soon as it is computed (the 2^23 config-4 quotient: 186
-    // VGPRs in source order, 512 + spills scheduled).
-    const bool sched_on = source_peak_live(in, n_instr, op) > 96;
-    Scheduled sp;
-    if (sched_on) {
-        schedule(in, n_instr, op, n_opnd, n_tmp1, n_tmp3, sp);
+    // the schedule (structure only, kept per process: scheduled_program)
+    const std::shared_ptr<const SchedMemo> memo = scheduled_program(in, n_instr, op, n_opnd, n_tmp1, n_tmp3);
+    if (memo->sched_on) {
+        const Scheduled &sp = memo->sp;
         in = sp.instr.data();
         n_instr = (uint32_t)sp.instr.size();
         op = sp.opnd.data();

@@ -1832,7 +1832,12 @@ int build_kernels(const ZxpJitIn &in, std::vector<JitKernel> &ks, const std::fun
     if (!scr) return ZKGPU_ERR_OOM;
     const uint64_t dom = 1ULL << in.log_dom;
     ks.resize(seg.size());
-    for (size_t j = 0; j < seg.size(); j++) {
+    // The segments are independent: their sources are generated (and their
+    // occupancy decided) in parallel threads -- on the zkEVM-shaped quotient
+    // ~10 ms of host work per segment, 8 segments, each proof (the GPU waits
+    // for it).  The occupancy memo and the disk cache are thread-safe.
+    auto one = [&](size_t j) -> int {
+        int rc;
         ZxpJitIn J = in;
         J.ins = seg[j].instr.data();
         J.n_instr = (uint32_t)seg[j].instr.size();
@@ -1883,7 +1888,20 @@ int build_kernels(const ZxpJitIn &in, std::vector<JitKernel> &ks, const std::fun
             }
         }
         ks[j].bytes = in.bytes / seg.size() + 8.0 * (seg[j].carry_in + seg[j].carry_out) * (double)dom;
-    }
+        return 0;
+    };
+    std::vector<int> rcs(seg.size(), 0);
+    std::atomic<size_t> next{0};
+    auto work = [&] {
+        for (size_t j; (j = next++) < seg.size();) rcs[j] = one(j);
+    };
+    std::vector<std::thread> th;
+    const size_t nthr = std::min<size_t>(seg.size(), std::max(1u, std::min(8u, std::thread::hardware_concurrency())));
+    for (size_t t = 1; t < nthr; t++) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+    for (int r : rcs)
+        if (r) return r;  // the first failing segment in order (1: unsupported shape -> the interpreter)
     return 0;
 }
 
