@@ -32,8 +32,10 @@
 //       layout), the W sub-roots are all-gathered, the top log2 W levels
 //       hashed on every rank.
 //   stage 4  the quotient program on the rank's 2n rows (x_i = 7 w^(rB+i),
-//       halo rows); q (2n x 3) is gathered, the INTT / split / NTT
-//       (starks.cpp:255-296) run on every rank, each commits its rows.
+//       halo rows); the split (starks.cpp:255-296) by column owners: q column
+//       j goes to rank j mod W, which interpolates it over the whole domain,
+//       splits it into the q_deg pieces and evaluates them; every rank gets
+//       its row blocks of all pieces back and commits its rows.
 //   stage 5  LEv / LpEv (closed form) and evmap on the rank's n-domain rows,
 //       partial sums all-gathered and added mod p; xDivXSub and the FRI
 //       program on the rank's 2n rows.
