@@ -42,10 +42,15 @@ def test_zkevm_shaped_proof_bit_exact(zkgpu, zkevm_case, monkeypatch, jit):
         assert got[k] == ref[k], k
 
 
-def test_zkevm_shaped_repeat_is_deterministic(zkgpu, zkevm_case):
+@pytest.mark.parametrize("jit", ["0", "2"], ids=["interpreter", "compiled"])
+def test_zkevm_shaped_repeat_is_deterministic(zkgpu, zkevm_case, monkeypatch, jit):
     """a second proof by the same prover object (the bench's timed loop)
-    equals the first: nothing reads a column left over from the last proof"""
+    equals the first: nothing reads a column left over from the last proof.
+    Compiled: from the second evaluation of a segmented program on, its
+    segments are launched as they are prepared (csrc/zxp_jit.hip
+    zxp_jit_run, per-segment staging), so this checks that path too."""
     from zkgpu.stark import GpuStark
+    monkeypatch.setenv("ZKGPU_ZXP_JIT", jit)
     inst, ref = zkevm_case
     g = GpuStark(inst)
     g.witness()
