@@ -7,6 +7,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -933,6 +935,27 @@ static void zxp_alloc_slots(const zxp_instr *in, uint32_t n_instr, std::vector<z
 
 // log_dom: rows evaluated (2^log_dom); log_omega: x_i = x_start * w_{2^log_omega}^i and zhInv's N =
 // 2^(log_omega - extend_bits); wrap: shifted reads wrap mod 2^log_dom, else halo rows follow the block
+// zhInv tables (<= 64 words) on the device, one per (log omega, extend
+// bits), uploaded once: the compiled expression kernels read them and need
+// no per-call upload (and no stream sync for a pageable source)
+static const uint64_t *zh_table(uint32_t log_omega, uint32_t eb, const uint64_t *zhv, size_t n)
+{
+    static std::mutex mu;
+    static std::map<std::pair<uint32_t, uint32_t>, uint64_t *> tabs;
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_pair(log_omega, eb);
+    auto it = tabs.find(key);
+    if (it != tabs.end()) return it->second;
+    uint64_t *d = nullptr;
+    if (check_hip(hipMalloc((void **)&d, 64 * 8), "zxp: zhInv table")) return nullptr;
+    if (check_hip(hipMemcpy(d, zhv, n * 8, hipMemcpyHostToDevice), "zxp: zhInv table")) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    tabs[key] = d;
+    return d;
+}
+
 static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, uint32_t n_opnd, uint32_t n_tmp1,
                          uint32_t n_tmp3, const zkgpu_sections *sections, uint32_t log_dom, uint32_t log_omega,
                          int wrap, const uint64_t *challenges, const uint64_t *publics, uint32_t n_publics,
@@ -1026,12 +1049,6 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
     const uint32_t n_logz = extend_bits;
     const size_t zh = (size_t)1 << n_logz;
     if (zh > 64) return set_error(ZKGPU_ERR_ARG, "zxp: extend bits > 6");
-    size_t off_prog = 0;
-    size_t off_terms = off_prog + (size_t)std::max<uint32_t>(n_instr, 1) * sizeof(ZOp);
-    size_t off_zh = off_terms + (size_t)n_dot_terms * sizeof(ZTerm);
-    size_t total = off_zh + zh * 8 + 16;
-    char *p = param_buf(total);
-    if (!p) return set_error(ZKGPU_ERR_OOM, "param buffer");
     // zhInv[j] = 1/(7^N * W[eb]^j - 1)  (zhInv.cpp:7-31), N = 2^(log_dom - eb)
     uint64_t zhv[64];
     {
@@ -1043,6 +1060,76 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
             w = h_mul(w, we);
         }
     }
+    for (uint32_t k = 0; k < n_opnd; k++)
+        if ((op[k].kind == ZXP_COL || op[k].kind == ZXP_COL3) && sections->ld[op[k].a] > 0xFFFFFFFFULL)
+            return set_error(ZKGPU_ERR_ARG, "zxp: section %u stride exceeds 2^32", op[k].a);
+    hipStream_t s = g_ctx.stream;
+    // algorithmic bytes: every distinct column operand read once per row + written columns
+    double alg_bytes = 0;
+    for (uint32_t k = 0; k < n_opnd; k++) {
+        const uint32_t kind = op[k].kind;
+        alg_bytes += kind == ZXP_COL ? 1 : (kind == ZXP_COL3 || kind == ZXP_XDIV || kind == ZXP_XDIVW) ? 3 : 0;
+    }
+    alg_bytes *= 8.0 * (double)(1ULL << log_dom);
+    if (use_jit) {
+        // the compiled kernels take their own tables (csrc/zxp_jit.hip): no
+        // interpreter records, no upload or stream sync here, so the host
+        // prepares them while earlier work still runs on the stream
+        for (uint32_t k = 0; k < n_instr; k++) {
+            const zxp_instr &I = pin[k];
+            if (I.op == ZXP_DOT1 || I.op == ZXP_DOT3) {
+                for (uint32_t t = I.a; t < I.a + I.b; t++) {
+                    if (terms[t].src == ZXP_TERM_ONE) continue;
+                    const uint32_t kind = opv[terms[t].src].kind;
+                    if (kind != ZXP_COL && kind != ZXP_TMP1 && kind != ZXP_TMP3)
+                        return set_error(ZKGPU_ERR_ARG, "zxp: DOT term source kind %u", kind);
+                }
+            }
+            const uint32_t dk = opv[I.dst].kind;
+            if (dk != ZXP_TMP1 && dk != ZXP_TMP3 && dk != ZXP_COL && dk != ZXP_COL3)
+                return set_error(ZKGPU_ERR_ARG, "zxp: instruction %u writes a read-only operand", k);
+        }
+        const uint64_t *zh_dev = zh_table(log_omega, extend_bits, zhv, zh);
+        if (!zh_dev) return -1;
+        ZxpJitIn J;
+        J.ins = pin;
+        J.n_instr = n_instr;
+        J.opnd = opv.data();
+        J.n_opnd = (uint32_t)opv.size();
+        J.terms = terms;
+        J.csts = csts;
+        J.n_tmp1 = n_tmp1;
+        J.n_tmp3 = n_tmp3;
+        J.sections = sections;
+        J.log_dom = log_dom;
+        J.log_omega = log_omega;
+        J.wrap = wrap ? 1u : 0u;
+        J.challenges = challenges;
+        J.publics = publics;
+        J.evals = evals;
+        J.xdiv = xdiv;
+        J.xdivw = xdivw;
+        J.zh_dev = zh_dev;
+        J.zmask = (uint32_t)(zh - 1);
+        J.x_start = x_start % HP;
+        J.bytes = alg_bytes;
+        J.dot_loop_min = 8;  // (zxp_jit.hip zkgpu_zxp_jit_source uses the same settings)
+        J.waves_per_eu = 0;
+        J.force_split = 0;
+        J.scratch = nullptr;
+        J.scratch_ld = 0;
+        rc = zxp_jit_run(J, s);
+        if (rc <= 0) return rc;  // launched, or an error
+        // 1 = shape unsupported: compile for the interpreter instead
+        return zxp_eval_impl(instr, n_instr0, opnd0, n_opnd, n_tmp1_0, n_tmp3_0, sections, log_dom, log_omega, wrap,
+                             challenges, publics, n_publics, evals, n_evals, xdiv, xdivw, extend_bits, x_start, 1);
+    }
+    size_t off_prog = 0;
+    size_t off_terms = off_prog + (size_t)std::max<uint32_t>(n_instr, 1) * sizeof(ZOp);
+    size_t off_zh = off_terms + (size_t)n_dot_terms * sizeof(ZTerm);
+    size_t total = off_zh + zh * 8 + 16;
+    char *p = param_buf(total);
+    if (!p) return set_error(ZKGPU_ERR_OOM, "param buffer");
     const uint64_t *zh_dev = (const uint64_t *)(p + off_zh);
     // pre-decode: resolve every operand to (kind, pointer, shift/slot, stride, immediate)
     std::vector<ZOp> prog(n_instr);
@@ -1145,10 +1232,6 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
         if (slots * 64 * 8 > 160 * 1024)
             return set_error(ZKGPU_ERR_ARG, "zxp: %llu temp slots exceed LDS", (unsigned long long)slots);
     }
-    for (uint32_t k = 0; k < n_opnd; k++)
-        if ((op[k].kind == ZXP_COL || op[k].kind == ZXP_COL3) && sections->ld[op[k].a] > 0xFFFFFFFFULL)
-            return set_error(ZKGPU_ERR_ARG, "zxp: section %u stride exceeds 2^32", op[k].a);
-    hipStream_t s = g_ctx.stream;
     if ((rc = check_hip(hipMemcpyAsync(p + off_prog, prog.data(), n_instr * sizeof(ZOp), hipMemcpyHostToDevice, s),
                         "H2D")) ||
         (zterms.size() &&
@@ -1181,47 +1264,7 @@ static int zxp_eval_impl(const void *instr, uint32_t n_instr, const void *opnd, 
     L.zhinv = zh_dev;
     L.zhinv_mask = (uint32_t)(zh - 1);
     L.x_start = x_start % HP;
-    // algorithmic bytes: every distinct column operand read once per row + written columns
-    double cols = 0;
-    for (uint32_t k = 0; k < n_opnd; k++)
-        if (op[k].kind == ZXP_COL) cols += 1;
-        else if (op[k].kind == ZXP_COL3) cols += 3;
-        else if (op[k].kind == ZXP_XDIV || op[k].kind == ZXP_XDIVW) cols += 3;
-    L.bytes = 8.0 * cols * (double)(1ULL << log_dom);
-    if (use_jit) {
-        ZxpJitIn J;
-        J.ins = pin;
-        J.n_instr = n_instr;
-        J.opnd = opv.data();
-        J.n_opnd = (uint32_t)opv.size();
-        J.terms = terms;
-        J.csts = csts;
-        J.n_tmp1 = n_tmp1;
-        J.n_tmp3 = n_tmp3;
-        J.sections = sections;
-        J.log_dom = log_dom;
-        J.log_omega = log_omega;
-        J.wrap = wrap ? 1u : 0u;
-        J.challenges = challenges;
-        J.publics = publics;
-        J.evals = evals;
-        J.xdiv = xdiv;
-        J.xdivw = xdivw;
-        J.zh_dev = zh_dev;
-        J.zmask = (uint32_t)(zh - 1);
-        J.x_start = x_start % HP;
-        J.bytes = L.bytes;
-        J.dot_loop_min = 8;  // (zxp_jit.hip zkgpu_zxp_jit_source uses the same settings)
-        J.waves_per_eu = 0;
-        J.force_split = 0;
-        J.scratch = nullptr;
-        J.scratch_ld = 0;
-        rc = zxp_jit_run(J, s);
-        if (rc <= 0) return rc;  // launched, or an error
-        // 1 = shape unsupported: compile for the interpreter instead
-        return zxp_eval_impl(instr, n_instr0, opnd0, n_opnd, n_tmp1_0, n_tmp3_0, sections, log_dom, log_omega, wrap,
-                             challenges, publics, n_publics, evals, n_evals, xdiv, xdivw, extend_bits, x_start, 1);
-    }
+    L.bytes = alg_bytes;
     return zxp_eval(L, s);
 }
 

@@ -26,6 +26,7 @@
 
 #include <chrono>
 #include <cctype>
+#include <charconv>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -244,6 +245,41 @@ void appendf(std::string &s, const char *fmt, ...)
     }
 }
 
+// decimal text without the printf machinery (the per-term lines below are
+// ~10 K appends per segment: vsnprintf was ~60 % of a segment's source time)
+inline void app_num(std::string &s, uint64_t v)
+{
+    char b[24];
+    const auto r = std::to_chars(b, b + sizeof(b), v);
+    s.append(b, r.ptr);
+}
+
+// one DOT term's line: D<dot>_j`.term_al(<val>, K + <kt + 8 j>) for the
+// components of the accumulator (the same text appendf wrote)
+inline void app_term(std::string &s, const std::string &val, uint32_t dot, size_t kt, bool three)
+{
+    if (three) {
+        s += "{ const uint64_t v_ = ";
+        s += val;
+        for (int j = 0; j < 3; j++) {
+            s += j ? " D" : "; D";
+            app_num(s, dot);
+            s += j == 0 ? "_0`.term_al(v_, K + " : j == 1 ? "_1`.term_al(v_, K + " : "_2`.term_al(v_, K + ";
+            app_num(s, kt + 8 * (size_t)j);
+            s += ");";
+        }
+        s += " }\n";
+    } else {
+        s += 'D';
+        app_num(s, dot);
+        s += "_0`.term_al(";
+        s += val;
+        s += ", K + ";
+        app_num(s, kt);
+        s += ");\n";
+    }
+}
+
 struct Expr {
     std::string e;
     int dim;
@@ -259,12 +295,14 @@ Cache &cache()
     return c;
 }
 
-// grow-only device buffer for the per-launch tables
-char *jit_buf(size_t bytes)
+// grow-only device buffer for the per-launch tables (in_use: the event after
+// the last kernels that read it)
+char *jit_buf(size_t bytes, hipEvent_t in_use)
 {
     static char *buf = nullptr;
     static size_t cap = 0;
     if (bytes > cap) {
+        if (in_use) (void)hipEventSynchronize(in_use);
         if (buf) (void)hipFree(buf);
         buf = nullptr;
         cap = 0;
@@ -509,7 +547,9 @@ static size_t lds_column_cache(std::string &body, int slots, int gap)
     };
     std::vector<Rd> rd;
     std::set<uint32_t> stored;
-    auto ident = [](char c) { return isalnum((unsigned char)c) || c == '_'; };
+    auto ident = [](char c) {
+        return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_';
+    };
     auto num = [&](size_t &q, int64_t &v) {
         const char *b = body.c_str() + q;
         char *e;
@@ -519,13 +559,16 @@ static size_t lds_column_cache(std::string &body, int slots, int gap)
         return true;
     };
     uint32_t line = 0;
-    for (size_t q = 0; q < body.size(); q++) {
-        const char ch = body[q];
+    const char *bp = body.data();
+    const size_t bn = body.size();
+    for (size_t q = 0; q < bn; q++) {
+        const char ch = bp[q];
         if (ch == '\n') {
             line++;
             continue;
         }
-        if (q > 0 && ident(body[q - 1])) continue;
+        if (ch != 'C' && ch != 'Z') continue;
+        if (q > 0 && ident(bp[q - 1])) continue;
         if (ch == 'C' && body.compare(q, 2, "C(") == 0) {
             size_t t = q + 2;
             int64_t j, sh;
@@ -542,7 +585,8 @@ static size_t lds_column_cache(std::string &body, int slots, int gap)
     const uint64_t INF = ~0ULL;
     std::vector<uint64_t> nx(rd.size(), INF);
     {
-        std::map<uint64_t, size_t> last;
+        std::unordered_map<uint64_t, size_t> last;
+        last.reserve(rd.size());
         for (size_t r = rd.size(); r-- > 0;) {
             auto it = last.find(rd[r].key);
             if (it != last.end()) nx[r] = it->second;
@@ -550,7 +594,7 @@ static size_t lds_column_cache(std::string &body, int slots, int gap)
         }
     }
     std::vector<uint64_t> slot_key(slots, INF), slot_nu(slots, INF);
-    std::map<uint64_t, int> where;
+    std::unordered_map<uint64_t, int> where;
     std::vector<int> act(rd.size(), -1), hit(rd.size(), 0);
     std::vector<uint32_t> pinned_line(slots, UINT32_MAX);
     size_t hits = 0;
@@ -596,10 +640,17 @@ static size_t lds_column_cache(std::string &body, int slots, int gap)
     for (size_t r = 0; r < rd.size(); r++) {
         if (act[r] < 0) continue;
         out.append(body, at, rd[r].pos - at);
-        if (hit[r])  // (~: the row of the line, expand_rows)
-            appendf(out, "LC(%d,~)", act[r]);
-        else
-            appendf(out, "CS(%s,%d,~)", body.substr(rd[r].pos + 2, rd[r].len - 3).c_str(), act[r]);
+        if (hit[r]) {  // (~: the row of the line, expand_rows)
+            out += "LC(";
+            app_num(out, (uint64_t)act[r]);
+            out += ",~)";
+        } else {
+            out += "CS(";
+            out.append(body, rd[r].pos + 2, rd[r].len - 3);
+            out += ',';
+            app_num(out, (uint64_t)act[r]);
+            out += ",~)";
+        }
         at = rd[r].pos + rd[r].len;
     }
     out.append(body, at, std::string::npos);
@@ -1224,13 +1275,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         for (const Stream &st : stream[at]) {
             maybe_split();
             const size_t kt = kmap(st.kt, st.three ? 24 : 8);
-            if (st.three)
-                appendf(body,
-                        "{ const uint64_t v_ = %s; D%u_0`.term_al(v_, K + %zu); D%u_1`.term_al(v_, K + %zu); "
-                        "D%u_2`.term_al(v_, K + %zu); }\n",
-                        st.val.c_str(), st.dot, kt, st.dot, kt + 8, st.dot, kt + 16);
-            else
-                appendf(body, "D%u_0`.term_al(%s, K + %zu);\n", st.dot, st.val.c_str(), kt);
+            app_term(body, st.val, st.dot, kt, st.three);
         }
     };
     // the fused chains (above), where their first link stood
@@ -1359,13 +1404,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                                               ? "a" + std::to_string(tm.src) + "`"
                                               : "b" + std::to_string(tm.src) + "`.v[" + std::to_string(tm.comp) + "]";
                     const size_t kt = kmap(limbs6x3(tm.coef), three ? 24 : 8);
-                    if (three)
-                        appendf(body,
-                                "{ const uint64_t v_ = %s; D%u_0`.term_al(v_, K + %zu); D%u_1`.term_al(v_, K + %zu); "
-                                "D%u_2`.term_al(v_, K + %zu); }\n",
-                                v.c_str(), k, kt, k, kt + 8, k, kt + 16);
-                    else
-                        appendf(body, "D%u_0`.term_al(%s, K + %zu);\n", k, v.c_str(), kt);
+                    app_term(body, v, k, kt, three);
                     continue;
                 }
                 if (loop && memcol(tm)) continue;
@@ -1373,13 +1412,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
                 std::string e;
                 if (col_read(o.a, o.b, (int32_t)o.c, e)) return 1;
                 const size_t kt = kmap(limbs6x3(tm.coef), three ? 24 : 8);
-                if (three)
-                    appendf(body,
-                            "{ const uint64_t v_ = %s; D%u_0`.term_al(v_, K + %zu); D%u_1`.term_al(v_, K + %zu); "
-                            "D%u_2`.term_al(v_, K + %zu); }\n",
-                            e.c_str(), k, kt, k, kt + 8, k, kt + 16);
-                else
-                    appendf(body, "D%u_0`.term_al(%s, K + %zu);\n", k, e.c_str(), kt);
+                app_term(body, e, k, kt, three);
             }
             char fin[128];
             if (three)
@@ -1667,18 +1700,39 @@ int launch_all(std::vector<JitKernel> &ks, const ZxpJitIn &in, hipStream_t s)
         total = (K.end + 15) & ~(size_t)15;
         K.klds = jit_kl_lds(K.kl.size()) && K.src.find("#define ZKJIT_KL_CHUNK 0") != std::string::npos;
     }
-    char *buf = jit_buf(total);
-    if (!buf) return set_error(ZKGPU_ERR_OOM, "zxp jit: table buffer");
-    std::vector<char> h(total, 0);
-    for (JitKernel &K : ks) {
-        memcpy(h.data() + K.off, K.zt.data(), K.zt.size() * sizeof(JitTerm));
-        memcpy(h.data() + K.off_cp, K.cp.data(), K.cp.size() * 8);
-        memcpy(h.data() + K.off_kc, K.kc.data(), K.kc.size() * 8);
-        memcpy(h.data() + K.off_kl, K.kl.data(), K.kl.size() * 4);
-    }
+    // The tables go through a pinned staging buffer, so the upload is
+    // asynchronous and the host does not wait for the stream's earlier work
+    // (a stage's kernels queued before this program): the staging buffer is
+    // rewritten only after its last upload has landed (event), and the
+    // device buffer after the last kernels that read it (stream order, or an
+    // event if the stream changed).
+    static hipEvent_t up = nullptr, use = nullptr;
+    static char *pin = nullptr;
+    static size_t pin_cap = 0;
     int rc;
-    if ((rc = check_hip(hipMemcpyAsync(buf, h.data(), total, hipMemcpyHostToDevice, s), "zxp jit: H2D"))) return rc;
-    if ((rc = check_hip(hipStreamSynchronize(s), "zxp jit: table upload"))) return rc;  // pageable source
+    if (!up && ((rc = check_hip(hipEventCreateWithFlags(&up, hipEventDisableTiming), "zxp jit: event")) ||
+                (rc = check_hip(hipEventCreateWithFlags(&use, hipEventDisableTiming), "zxp jit: event"))))
+        return rc;
+    if ((rc = check_hip(hipEventSynchronize(up), "zxp jit: staging"))) return rc;
+    if (total > pin_cap) {
+        if (pin) (void)hipHostFree(pin);
+        pin = nullptr;
+        pin_cap = 0;
+        if ((rc = check_hip(hipHostMalloc((void **)&pin, total), "zxp jit: staging buffer"))) return rc;
+        pin_cap = total;
+    }
+    char *buf = jit_buf(total, use);
+    if (!buf) return set_error(ZKGPU_ERR_OOM, "zxp jit: table buffer");
+    memset(pin, 0, total);
+    for (JitKernel &K : ks) {
+        memcpy(pin + K.off, K.zt.data(), K.zt.size() * sizeof(JitTerm));
+        memcpy(pin + K.off_cp, K.cp.data(), K.cp.size() * 8);
+        memcpy(pin + K.off_kc, K.kc.data(), K.kc.size() * 8);
+        memcpy(pin + K.off_kl, K.kl.data(), K.kl.size() * 4);
+    }
+    if ((rc = check_hip(hipStreamWaitEvent(s, use, 0), "zxp jit: table order"))) return rc;
+    if ((rc = check_hip(hipMemcpyAsync(buf, pin, total, hipMemcpyHostToDevice, s), "zxp jit: H2D"))) return rc;
+    if ((rc = check_hip(hipEventRecord(up, s), "zxp jit: event"))) return rc;
     Ctx &c = ctx();
     const uint64_t dom = 1ULL << in.log_dom;
     for (JitKernel &K : ks)
@@ -1716,7 +1770,7 @@ int launch_all(std::vector<JitKernel> &ks, const ZxpJitIn &in, hipStream_t s)
         prof_end(name, K.bytes, s);
         if (rc) return rc;
     }
-    return 0;
+    return check_hip(hipEventRecord(use, s), "zxp jit: event");
 }
 
 // Segments of a large program (csrc/zxp_segment.hpp): one per seg_cost of
