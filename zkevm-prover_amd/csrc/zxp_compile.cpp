@@ -248,6 +248,17 @@ struct Compiler {
         }
     }
 
+    // source operand k's value without copying a stored temporary's form
+    // (scratch holds the value of any other operand)
+    const Form &load_ref(uint32_t k, Form &scratch)
+    {
+        const zxp_operand &o = op[k];
+        if (o.kind == ZXP_TMP1 && set1[o.a]) return st1[o.a];
+        if (o.kind == ZXP_TMP3 && set3[o.a]) return st3[o.a];
+        scratch = load(k);
+        return scratch;
+    }
+
     static void project1(Form &f)
     {
         if (f.dim == 1) return;
@@ -407,11 +418,11 @@ struct Compiler {
         for (uint32_t k = 0; k < n_in; k++) {
             const zxp_instr &I = in[k];
             const zxp_operand &D = op[I.dst];
-            Form A = load(I.a);
+            Form sa, sb;
+            const Form &A = load_ref(I.a, sa);
             Form R;
             bool opaque = false;
-            Form B;
-            if (I.op != ZXP_COPY) B = load(I.b);
+            const Form &B = I.op != ZXP_COPY ? load_ref(I.b, sb) : sb;
             if (I.op == ZXP_COPY) {
                 R = A;
             } else if (I.op == ZXP_ADD || I.op == ZXP_SUB) {
@@ -431,7 +442,7 @@ struct Compiler {
             const bool to_col = D.kind == ZXP_COL || D.kind == ZXP_COL3;
             if (opaque) {
                 // realise the operands in place (temps keep the realised form)
-                const uint32_t ra = realize_src(I.a, A), rb = realize_src(I.b, B);
+                const uint32_t ra = realize_src(I.a, sa), rb = realize_src(I.b, sb);
                 const int dim = std::max(A.dim, B.dim);
                 if (to_col) {
                     const int sd = (D.kind == ZXP_COL || dim == 1) ? 1 : 3;
@@ -476,22 +487,15 @@ struct Compiler {
         return 0;
     }
 
-    // realise operand k's value; for temps, the state entry is updated so
-    // later reads reuse the materialised value
-    uint32_t realize_src(uint32_t k, Form &f)
+    // realise operand k's value; for temps, the state entry is updated (in
+    // place: a reference from load_ref sees the realised form) so later reads
+    // reuse the materialised value; any other operand's value is in scratch
+    uint32_t realize_src(uint32_t k, Form &scratch)
     {
         const zxp_operand &o = op[k];
-        if (o.kind == ZXP_TMP1 && set1[o.a]) {
-            const uint32_t r = realize(st1[o.a]);
-            f = st1[o.a];
-            return r;
-        }
-        if (o.kind == ZXP_TMP3 && set3[o.a]) {
-            const uint32_t r = realize(st3[o.a]);
-            f = st3[o.a];
-            return r;
-        }
-        return realize(f);
+        if (o.kind == ZXP_TMP1 && set1[o.a]) return realize(st1[o.a]);
+        if (o.kind == ZXP_TMP3 && set3[o.a]) return realize(st3[o.a]);
+        return realize(scratch);
     }
 
     // store SSA temporary t (dimension td) into column operand D (row shift
