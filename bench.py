@@ -94,6 +94,9 @@ def parse():
                     help="stark workload: skip the oracle's zkEVM-shaped sample (cpu_baseline.zkevm_shaped, 2^16 rows, ~20 s)")
     ap.add_argument("--cpu-sample-bits", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_BITS", "18")))
     ap.add_argument("--cpu-sample-cols", type=int, default=int(os.environ.get("ZKGPU_CPU_SAMPLE_COLS", "4")))
+    ap.add_argument("--comm", choices=["rccl", "shm"], default="rccl",
+                    help="stark-sharded: the exchange -- RCCL over xGMI, or host shared memory (zkgpu_comm_host, the "
+                         "fallback the default bench retries with when the RCCL run fails)")
     ap.add_argument("--rank-probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-full", action="store_true",
                     help="only time the oracle STARK prover at the full size (minutes of CPU); prints one JSON line "
@@ -405,7 +408,7 @@ def timed(step, steps, warmup, world, dist, torch):
 
 
 def max_over_ranks(x, world, dist, torch, dev):
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64, device=_coll_dev(dist) if world > 1 else dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -688,6 +691,23 @@ def handoff_measure(n, C, dev, torch, zkgpu, s_per_proof):
     return res
 
 
+def shm_outbox_bytes(inst, args, world):
+    """Outbox of the host-staged exchange (bytes per rank and exchange): the
+    largest message set a rank posts is a commit's return of its column share
+    of the widest section, (W-1)/W of C 2N / W words, or its n-domain block
+    (W-1)/W of C N / W words; with a quarter of margin, at least 256 MiB."""
+    n = 1 << args.log_n
+    widest = max(inst.n_cm1, inst.n_cm2, inst.n_cm3, inst.n_cm4, inst.n_const)
+    share = -(-widest // world)
+    words = max(share * (n << args.blowup_bits), widest * (n // world))
+    return max(256 << 20, int(words * 8 * (world - 1) / world * 1.25))
+
+
+def _coll_dev(dist):
+    """device of the small tensors the bench's own collectives carry"""
+    return "cpu" if dist.get_backend() == "gloo" else "cuda"
+
+
 def _free_port():
     import socket
     s = socket.socket()
@@ -705,65 +725,94 @@ def sharded_children(args, world, rank, local, dist, torch):
     the replica measurement above with it: a child that fails or outlives
     --sharded-timeout is killed and reported.  Runs: the config-4 instance at
     every world size, and the fork-9 widths (751/168/408/6): 2^23 rows from
-    W = 4 (190 GB per rank; 120 GB at W = 8), 2^22 rows on 1-2 ranks.  Returns
-    rank 0's summary."""
-    import signal
-    import subprocess
+    W = 4 (190 GB per rank; 120 GB at W = 8), 2^22 rows on 1-2 ranks.  If the
+    config-4 run over RCCL fails at N > 1, it runs again over the host-staged
+    exchange (zkgpu_comm_host through /dev/shm), which then carries the
+    headline with the line saying so, and the fork-9 runs are skipped.
+    Returns rank 0's summary."""
     # fork-9 widths: 2^23 rows from W = 4 (plan 190 GB per rank), 2^22 rows
     # below it (2^23 needs 386 GB on one GPU, 317 GB per rank at W = 2)
     small = ["--log-n", "22"] if world < 4 and args.log_n > 22 else []
     runs = [("config4", []), ("fork9", ["--fork9"] + small), ("fork9_zkevm_shaped", ["--zkevm-shaped"] + small)]
     out = {}
-    failed = False
     for name, extra in runs:
-        if failed:  # the same code path again: do not spend another timeout on it
+        ok, rec = _sharded_child(args, world, rank, local, dist, torch, extra, "rccl")
+        if rank == 0:
+            out[name] = rec
+        if ok:
+            continue
+        if name == "config4" and world > 1:
+            # the RCCL run failed: the headline one-proof run again over the
+            # host-staged exchange -- slower, but a real proof over the N GPUs
+            ok2, rec2 = _sharded_child(args, world, rank, local, dist, torch, extra, "shm")
             if rank == 0:
-                out[name] = {"error": "skipped after a failed run"}
-            continue
-        port = _free_port() if rank == 0 else 0
-        if world > 1:
-            t = torch.tensor([port], dtype=torch.int64, device="cuda")
-            dist.broadcast(t, 0)
-            port = int(t.item())
-        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(local), WORLD_SIZE=str(world),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--workload", "stark-sharded",
-               "--steps", "3", "--warmup",
-               "1", "--no-cpu", "--log-n", str(args.log_n), "--blowup-bits", str(args.blowup_bits), "--ncols",
-               str(args.ncols), "--queries", str(args.queries)] + extra  # (a later --log-n wins)
-        t0 = time.time()
-        p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
-                             start_new_session=True)
-        try:
-            so, se = p.communicate(timeout=args.sharded_timeout)
-            rc = p.returncode
-        except subprocess.TimeoutExpired:
-            os.killpg(p.pid, signal.SIGKILL)
-            so, se = p.communicate()
-            rc = "timeout"
-        if world > 1:  # every rank learns whether any child failed
-            f = torch.tensor([0 if rc == 0 else 1], dtype=torch.int64, device="cuda")
-            dist.all_reduce(f)
-            failed = int(f.item()) > 0
-        else:
-            failed = rc != 0
-        if rank != 0:
-            continue
-        line = next((ln for ln in reversed(so.splitlines()) if ln.startswith('{"metric"')), None)
-        if rc != 0 or line is None:
-            out[name] = {"error": "exit %s" % rc, "stderr_tail": se[-600:], "wall_s": round(time.time() - t0, 1)}
-            continue
-        d = json.loads(line)
-        st = d.get("stages_ms") or {}
-        out[name] = {"value": d["value"], "unit": d["unit"], "n_gpus": d["n_gpus"], "ms_per_step": d["ms_per_step"],
-                     "scaling": "strong", "workload": d["config"]["workload"],
-                     "exchange_ms": round(sum(v for k, v in st.items() if "EXCHANGE" in k and not k.startswith("COUNT_")),
-                                          3),
-                     "stages_ms": {k: v for k, v in st.items() if not k.startswith("COUNT_COMM")},
-                     "wall_s": round(time.time() - t0, 1)}
-        if d.get("comm"):
-            out[name]["comm"] = d["comm"]
+                out[name] = dict(rec2, rccl_run=rec) if ok2 else {"error": "RCCL and host-staged runs failed",
+                                                                  "rccl_run": rec, "shm_run": rec2}
+                if ok2:
+                    out[name]["exchange"] = "host shared memory (zkgpu_comm_host): the RCCL run failed"
+        # the same code path again would fail the same way: no more runs
+        if rank == 0:
+            for later, _ in runs[runs.index((name, extra)) + 1:]:
+                out[later] = {"error": "skipped after the failed %s run" % name}
+        break
     return out if rank == 0 else None
+
+
+def _sharded_child(args, world, rank, local, dist, torch, extra, comm):
+    """One `--workload stark-sharded` run as a child process per rank (own
+    rendezvous, --sharded-timeout).  Returns (every rank's child succeeded,
+    rank 0's record)."""
+    import signal
+    import subprocess
+    port = _free_port() if rank == 0 else 0
+    if world > 1:
+        t = torch.tensor([port], dtype=torch.int64, device=_coll_dev(dist))
+        dist.broadcast(t, 0)
+        port = int(t.item())
+    # ZKGPU_RUN_ID: the tag the host-staged exchange's ranks match their shared
+    # segment on (host/comm_host.hpp; by default the launcher's pid, but each
+    # rank's child here has its own parent)
+    env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(local), WORLD_SIZE=str(world),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ZKGPU_RUN_ID="bench-%d" % port)
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--workload", "stark-sharded",
+           "--steps", "3", "--warmup", "1", "--no-cpu", "--log-n", str(args.log_n), "--blowup-bits",
+           str(args.blowup_bits), "--ncols", str(args.ncols), "--queries", str(args.queries),
+           "--comm", comm] + extra  # (a later --log-n wins)
+    t0 = time.time()
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        so, se = p.communicate(timeout=args.sharded_timeout)
+        rc = p.returncode
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        so, se = p.communicate()
+        rc = "timeout"
+    line = next((ln for ln in reversed(so.splitlines()) if ln.startswith('{"metric"')), None)
+    mine = rc == 0 and (line is not None or rank != 0)
+    if world > 1:  # every rank learns whether any child failed
+        f = torch.tensor([0 if mine else 1], dtype=torch.int64, device=_coll_dev(dist))
+        dist.all_reduce(f)
+        ok = int(f.item()) == 0
+    else:
+        ok = mine
+    if rank != 0:
+        return ok, None
+    if not mine:
+        return ok, {"error": "exit %s" % rc, "comm": comm, "stderr_tail": se[-600:],
+                    "wall_s": round(time.time() - t0, 1)}
+    if not ok:
+        return ok, {"error": "another rank's child failed", "comm": comm, "wall_s": round(time.time() - t0, 1)}
+    d = json.loads(line)
+    st = d.get("stages_ms") or {}
+    rec = {"value": d["value"], "unit": d["unit"], "n_gpus": d["n_gpus"], "ms_per_step": d["ms_per_step"],
+           "scaling": "strong", "workload": d["config"]["workload"],
+           "exchange_ms": round(sum(v for k, v in st.items() if "EXCHANGE" in k and not k.startswith("COUNT_")), 3),
+           "stages_ms": {k: v for k, v in st.items() if not k.startswith("COUNT_COMM")},
+           "wall_s": round(time.time() - t0, 1)}
+    if d.get("comm"):
+        rec["comm"] = d["comm"]
+    return ok, rec
 
 
 def launch_ranks(args):
@@ -869,8 +918,14 @@ def main():
     import torch.distributed as dist
     import zkgpu
 
+    # ZKGPU_BENCH_SHARE_GPU=1 (tests only, tests/test_gpu_bench_ranks.py):
+    # every rank on device 0 with a gloo group -- the multi-rank bench on the
+    # one-GPU test box, where RCCL refuses two ranks on one device
+    share = os.environ.get("ZKGPU_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group("gloo" if share else "nccl", init_method="env://")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     zkgpu.init(local)
@@ -901,10 +956,16 @@ def main():
             def step():
                 gs.prove_raw()
         elif args.workload == "stark-sharded":
-            # the C++ row-sharded prover (host/sharded_starks.hpp) over RCCL
-            from zkgpu.stark import GpuStark, RcclComm
+            # the C++ row-sharded prover (host/sharded_starks.hpp) over RCCL,
+            # or over host shared memory (--comm shm: outboxes sized for the
+            # instance's largest exchange, named after this run's rendezvous)
+            from zkgpu.stark import GpuStark, RcclComm, ShmComm
             inst = stark_instance(args.log_n, args.blowup_bits, C, args.queries, _kind(args))
-            comm = RcclComm()
+            if args.comm == "shm":
+                comm = ShmComm("/zkgpu_bench_%s" % os.environ.get("MASTER_PORT", "0"), world, rank,
+                               shm_outbox_bytes(inst, args, world))
+            else:
+                comm = RcclComm()
             gs = GpuStark(inst, comm=comm)
             gs.witness()
 
@@ -997,9 +1058,11 @@ def main():
                         "independent proof per GPU"
                         % (args.log_n, args.blowup_bits, inst.n_cm1, inst.n_cm2, inst.n_cm3, inst.n_cm4, inst.n_const,
                            inst.fri_steps, args.queries))
+            one = (sharded or {}).get("config4") or {}
             parallelism = ("replicas x%d (one independent proof per GPU)" % world if world == 1 or scaling == "weak"
-                           else "ONE proof row-sharded x%d (sharded_one_proof.config4: C++ prover, RCCL exchange of "
-                                "packed column/row blocks per commit); replicas in the `replicas` block" % world)
+                           else "ONE proof row-sharded x%d (sharded_one_proof.config4: C++ prover, %s exchange of "
+                                "packed column/row blocks per commit); replicas in the `replicas` block"
+                                % (world, "host shared memory (the RCCL run failed)" if one.get("exchange") else "RCCL"))
         elif args.workload == "stark-sharded":
             workload = ("ONE %s STARK proof (2^%d trace, cm1/cm2/cm3/cm4 = %d/%d/%d/%d, %d constants, %d queries) "
                         "row-sharded over %d rank(s): n and 2n domains by rows, NTT-transpose all-to-all per commit"

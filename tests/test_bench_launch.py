@@ -67,3 +67,20 @@ def test_comm_summary_checks_world():
     assert bench.comm_summary({"STARK_TOTAL": 1.0}, 1) is None
     with pytest.raises(SystemExit):
         bench.comm_summary(st, 8)
+
+
+def test_shm_outbox_covers_the_largest_exchange():
+    """bench.py --comm shm sizes each rank's outbox for its largest message set:
+    a commit's return of its column share over the extended rows, or its
+    n-domain block of the widest section (the capacities
+    tests/test_gpu_sharded_full.py ran the config-4 and zkEVM-shaped proofs with)"""
+    import types
+    import bench
+    args = types.SimpleNamespace(log_n=23, blowup_bits=1)
+    c4 = types.SimpleNamespace(n_cm1=100, n_cm2=26, n_cm3=27, n_cm4=6, n_const=30)
+    for w, need in ((2, 50 * 2**24 * 8 // 2), (8, 13 * 2**24 * 8 * 7 // 8)):
+        b = bench.shm_outbox_bytes(c4, args, w)
+        assert need <= b <= 1.3 * need, (w, b, need)
+    zk = types.SimpleNamespace(n_cm1=751, n_cm2=168, n_cm3=408, n_cm4=6, n_const=234)
+    args20 = types.SimpleNamespace(log_n=20, blowup_bits=1)
+    assert bench.shm_outbox_bytes(zk, args20, 8) <= 2 << 30 and bench.shm_outbox_bytes(zk, args20, 2) <= 4 << 30
