@@ -23,6 +23,7 @@ namespace zkgpu_host {
 
 struct HostCommHeader {
     std::atomic<uint32_t> ready;
+    std::atomic<uint32_t> arrived;  // ranks that have mapped the segment (creation)
     uint32_t world;
     uint64_t capacity;
     uint64_t run;                 // this run's tag (run_tag_hash): a stale segment never matches
@@ -185,6 +186,7 @@ static int host_comm_create(zkgpu_comm *comm, const char *name, uint32_t world, 
         h->capacity = capacity;
         h->run = run;
         for (auto &e : h->error) e.store(0);
+        h->arrived.store(0);
         h->ready.store(1, std::memory_order_release);
     } else {
         // wait (up to 60 s) for rank 0's segment of THIS run: a segment left
@@ -215,11 +217,22 @@ static int host_comm_create(zkgpu_comm *comm, const char *name, uint32_t world, 
         }
         c->base = (uint8_t *)m;
     }
-    // every rank has mapped the segment: its name is no longer needed
-    if (c->wait()) {
-        munmap(m, c->size);
-        delete c;
-        return -1;
+    // every rank has mapped the segment (counted, with a time limit: a rank
+    // that never arrives fails the others here instead of leaving them in a
+    // barrier), then its name is no longer needed
+    {
+        HostCommHeader *h = c->hdr();
+        h->arrived.fetch_add(1);
+        bool all = false;
+        for (int t = 0; t < 12000 && !(all = h->arrived.load() >= world); t++)
+            std::this_thread::sleep_for(std::chrono::milliseconds(5));
+        if (!all) {
+            const uint32_t n = h->arrived.load();
+            if (rank == 0) shm_unlink(name);
+            munmap(m, c->size);
+            delete c;
+            return fail("zkgpu_comm_host_create: %u of %u ranks arrived within 60 s", n, world);
+        }
     }
     if (rank == 0) shm_unlink(name);
     comm->rank = rank;
