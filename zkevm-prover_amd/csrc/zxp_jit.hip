@@ -505,18 +505,19 @@ static std::string expand_rows(const std::string &text, uint32_t rows)
         if (memchr(text.data() + pos, '`', len) == nullptr) {
             out.append(text, pos, len);
         } else {
-            for (uint32_t r = 0; r < rows; r++)
-                for (size_t k = pos; k <= eol; k++) {
-                    const char ch = text[k];
-                    if (ch == '`') {
-                        out += '_';
-                        out += (char)('0' + r);
-                    } else if (ch == '~') {
-                        out += (char)('0' + r);
-                    } else {
-                        out += ch;
-                    }
+            for (uint32_t r = 0; r < rows; r++) {
+                // runs between the marks appended whole (a line is ~50-100 chars)
+                size_t k = pos;
+                while (k <= eol) {
+                    size_t e = k;
+                    while (e <= eol && text[e] != '`' && text[e] != '~') e++;
+                    out.append(text, k, e - k);
+                    if (e > eol) break;
+                    if (text[e] == '`') out += '_';
+                    out += (char)('0' + r);
+                    k = e + 1;
                 }
+            }
         }
         pos = eol + 1;
     }
@@ -845,11 +846,21 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         }
         switch (d.kind) {
         case ZXP_TMP1:
-            appendf(body, "a%u` = %s%s;\n", didx, r.e.c_str(), r.dim == 3 ? ".v[0]" : "");
+            body += 'a';
+            app_num(body, didx);
+            body += "` = ";
+            body += r.e;
+            if (r.dim == 3) body += ".v[0]";
+            body += ";\n";
             return 0;
         case ZXP_TMP3:
-            if (r.dim == 3)
-                appendf(body, "b%u` = %s;\n", didx, r.e.c_str());
+            if (r.dim == 3) {
+                body += 'b';
+                app_num(body, didx);
+                body += "` = ";
+                body += r.e;
+                body += ";\n";
+            }
             else
                 appendf(body, "b%u` = gl3{{%s, 0, 0}};\n", didx, r.e.c_str());
             return 0;
@@ -1561,8 +1572,11 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             const uint32_t d = in.ins[k].dst;
             if (d >= in.n_opnd || seen[d]) continue;
             seen[d] = 1;
-            if (in.opnd[d].kind == ZXP_TMP1) appendf(decl, "uint64_t a%u`;\n", d);
-            if (in.opnd[d].kind == ZXP_TMP3) appendf(decl, "gl3 b%u`;\n", d);
+            if (in.opnd[d].kind == ZXP_TMP1 || in.opnd[d].kind == ZXP_TMP3) {
+                decl += in.opnd[d].kind == ZXP_TMP1 ? "uint64_t a" : "gl3 b";
+                app_num(decl, d);
+                decl += "`;\n";
+            }
         }
     }
     for (uint32_t r = 0; r < wcell.size(); r++) appendf(decl, "uint64_t w%u` = 0;\n", r);
