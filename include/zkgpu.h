@@ -367,6 +367,23 @@ int zkgpu_cols3_to_interleaved_dev(uint64_t *out, const uint64_t *cols, uint64_t
 int zkgpu_gl_merkle_open_rows_dev(uint64_t *vals_out, uint64_t *sibs_out, const uint64_t *nodes, const uint64_t *src,
                                   uint64_t ncols, uint64_t nrows, const uint64_t *idx, uint64_t nq);
 
+/* The query phase's openings of several trees in one round trip
+ * (friProve.cpp:195-232 -- every tree's getGroupProof at its query indices):
+ * request k is zkgpu_gl_merkle_open_dev (rows = 0: src column-major, ld) or
+ * zkgpu_gl_merkle_open_rows_dev (rows = 1: src row-major, ld ignored) with the
+ * same arguments and output layout; one index upload, the n kernels, one
+ * download, one synchronisation.  Every index is checked before anything is
+ * queued. */
+typedef struct zkgpu_open_req {
+    uint64_t *vals_out, *sibs_out;
+    const uint64_t *nodes, *src;
+    uint64_t ld, ncols, nrows;
+    const uint64_t *idx;
+    uint64_t nq;
+    uint32_t rows;
+} zkgpu_open_req;
+int zkgpu_gl_merkle_open_many(const zkgpu_open_req *req, uint32_t n);
+
 /* ---- arithmetic self-test hook -----------------------------------------------
  * Runs one device field operation elementwise on arbitrary u64 inputs
  * (including non-canonical values >= p) and stores canonical results:

@@ -56,3 +56,18 @@ def test_calls_fail_loudly_without_init():
     import numpy as np
     with pytest.raises(zkgpu.ZkgpuError):
         zkgpu.ntt(np.arange(16, dtype=np.uint64))
+
+
+def test_host_permutation_vs_oracle(oracle):
+    """The transcript's host permutation (zkgpu_gl_poseidon_full_host: full
+    rounds + the sparse partial rounds of poseidon_gl_sparse.h) equals the
+    oracle's textbook permutation, non-canonical inputs included.  CPU only."""
+    import numpy as np
+    import zkgpu
+    P = 0xFFFFFFFF00000001
+    rng = np.random.default_rng(77)
+    cases = [np.zeros(12, np.uint64), np.full(12, P - 1, np.uint64), np.full(12, 2**64 - 1, np.uint64),
+             np.arange(12, dtype=np.uint64) + np.uint64(P - 6)]
+    cases += [rng.integers(0, 2**64 - 1, 12, dtype=np.uint64, endpoint=True) for _ in range(200)]
+    for x in cases:
+        assert np.array_equal(zkgpu.poseidon_full_host(x), oracle.poseidon_full(x % np.uint64(P))), x

@@ -143,6 +143,45 @@ def test_merkletree_rows_dev(oracle, zkgpu):
     assert np.array_equal(zkgpu.from_device(nodes), oracle.merkletree(src))
 
 
+def test_merkle_open_many_vs_oracle(oracle, zkgpu):
+    """The query phase's one-round-trip openings (zkgpu_gl_merkle_open_many):
+    a column-major tree, a row-major tree, an empty request and a width-0
+    tree, each equal to the oracle's getGroupProof; a bad index anywhere fails
+    the whole call before anything is queued."""
+    import torch
+    rng = np.random.default_rng(23)
+    trees = []
+    for nrows, ncols, rows in [(1 << 11, 13, False), (1 << 9, 24, True), (1 << 10, 0, False)]:
+        src = rand_gl(rng, (nrows, ncols))
+        nodes = torch.zeros(zkgpu.merkle_num_elements(nrows), dtype=torch.int64, device="cuda:0")
+        dsrc = zkgpu.to_device(src if rows else np.ascontiguousarray(src.T)) if ncols else nodes
+        if rows:
+            zkgpu.merkletree_rows_dev(nodes, dsrc, ncols, nrows)
+        else:
+            zkgpu.merkletree_dev(nodes, dsrc, nrows, ncols, nrows)
+        torch.cuda.synchronize()
+        trees.append((src, nodes, dsrc, nrows, ncols, rows))
+    reqs, idxs = [], []
+    for k, (src, nodes, dsrc, nrows, ncols, rows) in enumerate(trees):
+        idx = rng.integers(0, nrows, 9 + k, dtype=np.uint64)
+        idx[0], idx[-1] = 0, nrows - 1
+        idxs.append(idx)
+        reqs.append((nodes, dsrc, nrows, ncols, nrows, idx, rows))
+    reqs.insert(1, (trees[0][1], trees[0][2], trees[0][3], trees[0][4], trees[0][3], np.zeros(0, np.uint64), False))
+    got = zkgpu.merkle_open_many(reqs)
+    del got[1]
+    for (src, nodes, _, nrows, ncols, _), idx, (vals, sibs) in zip(trees, idxs, got):
+        ref_nodes = oracle.merkletree(src)
+        for q, i in enumerate(idx):
+            v, s = oracle.merkle_group_proof(ref_nodes, src, int(i))
+            assert np.array_equal(vals[q], v)
+            assert np.array_equal(sibs[q], s)
+    bad = list(reqs)
+    bad[-1] = bad[-1][:5] + (np.array([0, bad[-1][4]], np.uint64),) + bad[-1][6:]
+    with pytest.raises(zkgpu.ZkgpuError, match="index"):
+        zkgpu.merkle_open_many(bad)
+
+
 # ------------------------------------------------------------------ FRI
 @pytest.mark.parametrize("pol_bits,out_bits", [(6, 2), (10, 6), (12, 9), (16, 12), (20, 16), (11, 11), (13, 8)])
 def test_fri_fold_vs_oracle(oracle, zkgpu, pol_bits, out_bits):

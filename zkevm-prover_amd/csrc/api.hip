@@ -16,6 +16,7 @@
 #include "gl_device.hpp"
 #include "zkgpu_internal.hpp"
 #include "poseidon_gl_constants.h"
+#include "poseidon_gl_sparse.h"
 
 namespace zk {
 
@@ -64,7 +65,20 @@ uint64_t *workspace(int i, size_t bytes)
 
 // ---- host scalar field (setup constants only)
 static const uint64_t HP = 0xFFFFFFFF00000001ULL;
-uint64_t h_mul(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) % HP); }
+// (a b) mod p by the Goldilocks folding 2^64 = 2^32 - 1, 2^96 = -1 (no 128-bit
+// division: the expression kernels' limb tables take ~10^5 of these per proof)
+uint64_t h_mul(uint64_t a, uint64_t b)
+{
+    const unsigned __int128 x = (unsigned __int128)a * b;
+    const uint64_t lo = (uint64_t)x, hi = (uint64_t)(x >> 64), eps = 0xFFFFFFFFULL;
+    const uint64_t hh = hi >> 32, hl = hi & eps;
+    uint64_t t0 = lo - hh;
+    if (lo < hh) t0 -= eps;  // borrow: 2^64 == eps
+    const uint64_t t1 = (hl << 32) - hl;
+    uint64_t r = t0 + t1;
+    if (r < t1) r += eps;  // carry: no second one
+    return r >= HP ? r - HP : r;
+}
 uint64_t h_pow(uint64_t a, uint64_t e)
 {
     uint64_t r = 1;
@@ -416,53 +430,65 @@ static int poseidon_one(uint64_t *out, const uint64_t *in, int full)
 
 int zkgpu_gl_poseidon_full(uint64_t out[12], const uint64_t in[12]) { return poseidon_one(out, in, 1); }
 
-// Host permutation for the transcript (PoseidonGoldilocks::hash_full_result
-// on the CPU, transcript.cpp:18-24): textbook rounds
-// (poseidon_g_executor.cpp:201-231): add constants, x^7 on all lanes
-// (rounds 0-3, 26-29) or lane 0, then M[i][j] = MCIRC[(j - i) mod 12] +
-// (i == j == 0) * 8.  Needs no GPU and no zkgpu_init.
-static uint64_t hp_mul(uint64_t a, uint64_t b)
+static uint64_t hp_add(uint64_t a, uint64_t b)  // a, b < p
 {
-    const unsigned __int128 x = (unsigned __int128)a * b;
-    const uint64_t lo = (uint64_t)x, hi = (uint64_t)(x >> 64);
-    const uint64_t hh = hi >> 32, hl = hi & 0xFFFFFFFFULL;
-    uint64_t t0 = lo - hh;
-    if (lo < hh) t0 -= 0xFFFFFFFFULL;  // borrow: 2^64 == 2^32 - 1
-    const uint64_t t1 = (hl << 32) - hl;
-    uint64_t r = t0 + t1;
-    if (r < t1) r += 0xFFFFFFFFULL;
-    return r >= HP ? r - HP : r;
+    const uint64_t s = a + b;
+    return (s < a || s >= HP) ? s - HP : s;
 }
-
-int zkgpu_gl_poseidon_full_host(uint64_t out[12], const uint64_t in[12])
+static uint64_t hp_pow7(uint64_t x)
+{
+    const uint64_t x2 = h_mul(x, x), x3 = h_mul(x2, x), x4 = h_mul(x2, x2);
+    return h_mul(x3, x4);
+}
+// full round r: constants, x^7 on every lane, M[i][j] = MCIRC[(j - i) mod 12] +
+// (i == j == 0) * 8 (an MDS row: 13 products of a canonical lane and a
+// constant < 2^6, < 2^74, one fold of 2^64)
+static void hp_full_round(uint64_t st[12], int r)
 {
     static const uint32_t MC[12] = {17, 15, 41, 16, 2, 28, 13, 13, 39, 18, 34, 20};
+    for (int i = 0; i < 12; i++) st[i] = hp_pow7(hp_add(st[i], ZKGPU_POSEIDON_RC[r * 12 + i]));
+    uint64_t t[12];
+    for (int i = 0; i < 12; i++) {
+        unsigned __int128 acc = (i == 0) ? (unsigned __int128)st[0] * 8 : 0;
+        for (int j = 0; j < 12; j++) acc += (unsigned __int128)st[j] * MC[j >= i ? j - i : j + 12 - i];
+        const uint64_t lo = (uint64_t)acc, hi = (uint64_t)(acc >> 64);  // hi < 2^10
+        const uint64_t hv = (hi << 32) - hi;                            // hi * 2^64 mod p
+        uint64_t v = lo + hv;
+        if (v < hv) v += 0xFFFFFFFFULL;
+        t[i] = v >= HP ? v - HP : v;
+    }
+    memcpy(st, t, sizeof t);
+}
+
+// Host permutation for the transcript (PoseidonGoldilocks::hash_full_result
+// on the CPU, transcript.cpp:18-24; the rounds of
+// poseidon_g_executor.cpp:201-231): 4 full rounds, the 22 partial rounds in
+// the sparse form the device uses (poseidon_gl_sparse.h, perm_sparse in
+// csrc/poseidon_perm.hpp: 27 products per round instead of a 12x12 MDS),
+// 4 full rounds.  Needs no GPU and no zkgpu_init.
+int zkgpu_gl_poseidon_full_host(uint64_t out[12], const uint64_t in[12])
+{
     uint64_t st[12];
     for (int i = 0; i < 12; i++) st[i] = in[i] % HP;
-    for (int r = 0; r < 30; r++) {
-        const bool full = r < 4 || r >= 26;
-        for (int i = 0; i < 12; i++) {
-            uint64_t x = st[i] + ZKGPU_POSEIDON_RC[r * 12 + i];
-            if (x < st[i] || x >= HP) x -= HP;
-            if (full || i == 0) {
-                const uint64_t x2 = hp_mul(x, x), x3 = hp_mul(x2, x), x4 = hp_mul(x2, x2);
-                x = hp_mul(x3, x4);
-            }
-            st[i] = x;
+    for (int r = 0; r < 4; r++) hp_full_round(st, r);
+    {
+        uint64_t v[11];
+        for (int j = 0; j < 11; j++) v[j] = hp_add(st[1 + j], ZKGPU_PSP_PRE[1 + j]);
+        st[0] = hp_add(st[0], ZKGPU_PSP_PRE[0]);
+        for (int i = 0; i < 11; i++) {
+            uint64_t acc = 0;
+            for (int j = 0; j < 11; j++) acc = hp_add(acc, h_mul(v[j], ZKGPU_PSP_D0[i * 11 + j]));
+            st[1 + i] = acc;
         }
-        uint64_t t[12];
-        for (int i = 0; i < 12; i++) {
-            // an MDS row: 13 products of a canonical lane and a constant < 2^6 -> < 2^74
-            unsigned __int128 acc = (i == 0) ? (unsigned __int128)st[0] * 8 : 0;
-            for (int j = 0; j < 12; j++) acc += (unsigned __int128)st[j] * MC[(j - i + 12) % 12];
-            const uint64_t lo = (uint64_t)acc, hi = (uint64_t)(acc >> 64);  // hi < 2^10
-            const uint64_t hv = (hi << 32) - hi;                            // hi * 2^64 mod p
-            uint64_t v = lo + hv;
-            if (v < hv) v += 0xFFFFFFFFULL;
-            t[i] = v >= HP ? v - HP : v;
-        }
-        memcpy(st, t, sizeof t);
     }
+    for (int k = 0; k < 22; k++) {
+        const uint64_t s0 = hp_add(hp_pow7(st[0]), ZKGPU_PSP_POST[k]);
+        uint64_t acc = h_mul(s0, 25);
+        for (int j = 0; j < 11; j++) acc = hp_add(acc, h_mul(st[1 + j], ZKGPU_PSP_W[k * 11 + j]));
+        for (int j = 0; j < 11; j++) st[1 + j] = hp_add(st[1 + j], h_mul(s0, ZKGPU_PSP_V[k * 11 + j]));
+        st[0] = acc;
+    }
+    for (int r = 26; r < 30; r++) hp_full_round(st, r);
     memcpy(out, st, sizeof st);
     return 0;
 }
@@ -1576,6 +1602,67 @@ int zkgpu_gl_merkle_open_rows_dev(uint64_t *vals_out, uint64_t *sibs_out, const 
     if (nv && (rc = check_hip(hipMemcpyAsync(vals_out, dv, nv * 8, hipMemcpyDeviceToHost, c.stream), "D2H"))) return rc;
     if (ns && (rc = check_hip(hipMemcpyAsync(sibs_out, ds, ns * 8, hipMemcpyDeviceToHost, c.stream), "D2H"))) return rc;
     return check_hip(hipStreamSynchronize(c.stream), "merkle_open_rows sync");
+}
+
+// all query openings of a proof in one round trip: [indices of every request |
+// vals, sibs of every request] in workspace 2, mirrored in a page-locked host
+// buffer so that the upload and the download are one copy each
+int zkgpu_gl_merkle_open_many(const zkgpu_open_req *req, uint32_t n)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    Ctx &c = g_ctx;
+    uint64_t ni = 0, no = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        const zkgpu_open_req &r = req[k];
+        if (r.nrows == 0 || (r.nrows & (r.nrows - 1)))
+            return set_error(ZKGPU_ERR_ARG, "merkle_open_many: request %u: nrows %llu is not a power of two", k,
+                             (unsigned long long)r.nrows);
+        for (uint64_t q = 0; q < r.nq; q++)
+            if (r.idx[q] >= r.nrows)
+                return set_error(ZKGPU_ERR_ARG, "merkle_open_many: request %u: index %llu >= nrows", k,
+                                 (unsigned long long)r.idx[q]);
+        ni += r.nq;
+        no += r.nq * (r.ncols + log2u(r.nrows) * 4ULL);
+    }
+    if (!ni) return 0;
+    static uint64_t *pin = nullptr;
+    static uint64_t pin_words = 0;
+    if (pin_words < ni + no) {
+        if (pin) (void)hipHostFree(pin);
+        pin = nullptr;
+        pin_words = 0;
+        if ((rc = check_hip(hipHostMalloc((void **)&pin, (ni + no) * 8, hipHostMallocDefault), "open_many pin")))
+            return rc;
+        pin_words = ni + no;
+    }
+    uint64_t *d = workspace(2, (ni + no) * 8);
+    if (!d) return ZKGPU_ERR_OOM;
+    for (uint32_t k = 0, i = 0; k < n; i += req[k].nq, k++) memcpy(pin + i, req[k].idx, req[k].nq * 8);
+    if ((rc = check_hip(hipMemcpyAsync(d, pin, ni * 8, hipMemcpyHostToDevice, c.stream), "open_many H2D"))) return rc;
+    uint64_t io = 0, oo = ni;
+    for (uint32_t k = 0; k < n; k++) {
+        const zkgpu_open_req &r = req[k];
+        if (!r.nq) continue;
+        uint64_t *dv = d + oo, *ds = dv + r.nq * r.ncols;
+        rc = r.rows ? merkle_open_strided(dv, ds, r.nodes, r.src, r.ncols, r.nrows, r.ncols, 1, d + io, r.nq, c.stream)
+                    : merkle_open_cols(dv, ds, r.nodes, r.src, r.ncols, r.nrows, r.ld, d + io, r.nq, c.stream);
+        if (rc) return rc;
+        io += r.nq;
+        oo += r.nq * (r.ncols + log2u(r.nrows) * 4ULL);
+    }
+    if ((rc = check_hip(hipMemcpyAsync(pin + ni, d + ni, no * 8, hipMemcpyDeviceToHost, c.stream), "open_many D2H")))
+        return rc;
+    if ((rc = check_hip(hipStreamSynchronize(c.stream), "open_many sync"))) return rc;
+    oo = ni;
+    for (uint32_t k = 0; k < n; k++) {
+        const zkgpu_open_req &r = req[k];
+        const uint64_t nv = r.nq * r.ncols, ns = r.nq * log2u(r.nrows) * 4ULL;
+        if (nv) memcpy(r.vals_out, pin + oo, nv * 8);
+        if (ns) memcpy(r.sibs_out, pin + oo + nv, ns * 8);
+        oo += nv + ns;
+    }
+    return 0;
 }
 
 // ---------------------------------------------------------------- FRI

@@ -667,13 +667,25 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         if (sec == ZXP_SEC_SCRATCH) return in.scratch + (uint64_t)col * in.scratch_ld;
         return S->sec[sec] + (uint64_t)col * S->ld[sec];
     };
-    std::map<std::pair<uint32_t, uint32_t>, uint32_t> slot;  // (section, col) -> cp slot
-    auto col_slot = [&](uint32_t sec, uint32_t col) {
+    // (section, col) -> cp slot: a flat table per section (a segment looks up
+    // ~10^4 column reads), a map for out-of-table indices
+    std::vector<std::vector<uint32_t>> slot_of(ZXP_SEC_SCRATCH + 1);
+    std::map<std::pair<uint32_t, uint32_t>, uint32_t> slot_far;
+    auto col_slot = [&](uint32_t sec, uint32_t col) -> uint32_t {
+        if (sec <= ZXP_SEC_SCRATCH && col < (1u << 20)) {
+            std::vector<uint32_t> &v = slot_of[sec];
+            if (col >= v.size()) v.resize(col + 1, UINT32_MAX);
+            if (v[col] == UINT32_MAX) {
+                cp.push_back(col_ptr(sec, col));
+                v[col] = (uint32_t)cp.size() - 1;
+            }
+            return v[col];
+        }
         auto key = std::make_pair(sec, col);
-        auto it = slot.find(key);
-        if (it != slot.end()) return it->second;
+        auto it = slot_far.find(key);
+        if (it != slot_far.end()) return it->second;
         cp.push_back(col_ptr(sec, col));
-        return slot[key] = (uint32_t)cp.size() - 1;
+        return slot_far[key] = (uint32_t)cp.size() - 1;
     };
     // Columns the program reads (any shift): a written column it never reads
     // is stored where the value is assigned (the compiled program forwards
@@ -733,7 +745,12 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             }
             if (sh != 0) return 1;  // cross-row read of a written column: interpreter
         }
-        e = "C(" + std::to_string(j) + "," + std::to_string(sh) + ",i`)";
+        e.assign("C(", 2);
+        app_num(e, j);
+        e += ',';
+        if (sh < 0) e += '-';
+        app_num(e, (uint64_t)(sh < 0 ? -(int64_t)sh : sh));
+        e += ",i`)";
         return 0;
     };
     auto kconst = [&](const uint64_t *v, int dim) {
@@ -1062,7 +1079,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
             const uint64_t s = a + b;
             return (s < a || s >= P) ? s - P : s;
         };
-        auto fmul = [](uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) % P); };
+        auto fmul = [](uint64_t a, uint64_t b) { return h_mul(a, b); };
         std::map<std::pair<uint32_t, int32_t>, size_t> fidx;
         for (size_t g = 0; g < fchains.size(); g++)
             for (uint32_t x : fchains[g])
@@ -1840,6 +1857,39 @@ static void waves_remember(const std::string &src, uint32_t w)
     g_waves[src] = w;
 }
 
+// The same decision of a whole (unsegmented) program keyed by its structure
+// -- instructions, operands, the DOT terms' sources, the launch shape; never
+// the coefficient or constant values -- so that a program evaluated every
+// proof is generated once per evaluation instead of twice (first source, then
+// the source at the chosen occupancy; config-4 quotient).  A key shared by two
+// programs can only cost one of them its occupancy target, never a result.
+static uint64_t structure_key(const ZxpJitIn &in)
+{
+    uint64_t h = 0x9E3779B97F4A7C15ULL;
+    auto mix = [&](uint64_t w) {
+        h = (h ^ w) * 0xBF58476D1CE4E5B9ULL;
+        h ^= h >> 31;
+    };
+    for (uint32_t k = 0; k < in.n_instr; k++) {
+        const zxp_instr &I = in.ins[k];
+        mix((uint64_t)I.op << 32 | I.dst);
+        mix((uint64_t)I.a << 32 | I.b);
+        if (I.op == ZXP_DOT1 || I.op == ZXP_DOT3)
+            for (uint32_t t = I.a; t < I.a + I.b; t++) mix((uint64_t)in.terms[t].src << 32 | in.terms[t].comp);
+    }
+    for (uint32_t k = 0; k < in.n_opnd; k++) {
+        const zxp_operand &o = in.opnd[k];
+        mix((uint64_t)o.kind << 32 | o.a);
+        mix((uint64_t)o.b << 32 | o.c);
+    }
+    mix((uint64_t)in.n_instr << 32 | in.n_opnd);
+    mix((uint64_t)in.n_tmp1 << 32 | in.n_tmp3);
+    mix((uint64_t)in.log_dom << 40 | (uint64_t)in.log_omega << 20 | in.wrap);
+    mix((uint64_t)in.dot_loop_min << 32 | in.force_split);
+    return h;
+}
+static std::unordered_map<uint64_t, uint32_t> g_waves_fp;
+
 // may_compile = false (source / cache queries): the occupancy decisions use
 // only code objects already on disk, and stop where one is missing
 int build_kernels(const ZxpJitIn &in, std::vector<JitKernel> &ks, const std::function<uint64_t *(uint32_t)> &scratch,
@@ -1865,6 +1915,23 @@ int build_kernels(const ZxpJitIn &in, std::vector<JitKernel> &ks, const std::fun
     if (nseg <= 1) {
         ks.resize(1);
         ks[0].bytes = in.bytes;
+        const bool decide = in.waves_per_eu == 0 && only <= 0;
+        const uint64_t fp = decide ? structure_key(in) : 0;
+        if (decide) {
+            uint32_t w = 0;
+            bool hit;
+            {
+                std::lock_guard<std::mutex> lk(g_waves_mu);
+                auto it = g_waves_fp.find(fp);
+                hit = it != g_waves_fp.end();
+                if (hit) w = it->second;
+            }
+            if (hit) {
+                ZxpJitIn in2 = in;
+                in2.waves_per_eu = w;
+                return prepare(in2, ks[0]);
+            }
+        }
         if ((rc = prepare(in, ks[0]))) return rc;
         // A kernel the compiler leaves at 169-256 registers runs 2 waves per
         // SIMD and is latency-bound: compiled again with an occupancy target
@@ -1875,15 +1942,18 @@ int build_kernels(const ZxpJitIn &in, std::vector<JitKernel> &ks, const std::fun
         // as are block-split programs (registers bounded by their blocks).
         // Decided from the code object's metadata, so the prebuilt cache and
         // the run agree.
-        if (in.waves_per_eu == 0 && only <= 0 &&
-            ks[0].src.find("#define ZKJIT_SPLIT 1") == std::string::npos) {
+        if (decide) {
             uint32_t w = 0;
-            if (!waves_known(ks[0].src, w)) {
+            if (ks[0].src.find("#define ZKJIT_SPLIT 1") == std::string::npos && !waves_known(ks[0].src, w)) {
                 std::vector<char> code;
-                if ((rc = object(ks[0].src, code))) return rc < 0 ? rc : 0;
+                if ((rc = object(ks[0].src, code))) return rc < 0 ? rc : 0;  // (query mode: undecided)
                 const uint64_t regs = co_note(code, ".vgpr_count") + co_note(code, ".agpr_count");
                 w = regs > 256 ? 2 : regs > 168 ? 3 : 0;
                 waves_remember(ks[0].src, w);
+            }
+            {
+                std::lock_guard<std::mutex> lk(g_waves_mu);
+                g_waves_fp[fp] = w;
             }
             if (w) {
                 ZxpJitIn in2 = in;

@@ -775,25 +775,24 @@ public:
         tstart();
         std::vector<uint64_t> ys(q());
         tr.get_permutations(ys.data(), q(), fri_steps[0]);
+        pend.clear();
+        pend_idx.clear();
         // FRI layers si >= 1: root, vals, siblings
         std::vector<uint64_t> yq = ys;
         for (size_t si = 0; si < fri_steps.size(); si++) {
-            if (si > 0) {
+            if (si > 0) {  // root, then the openings written in place (at flush_opens at the latest)
                 uint64_t ngroups = 1ULL << fri_steps[si];
                 uint64_t width = (3ULL << fri_steps[si - 1]) / ngroups;
-                std::vector<uint64_t> vals(q() * width), sibs((uint64_t)q() * fri_steps[si] * 4);
-                if (fri_open(si, ngroups, width, yq, vals.data(), sibs.data())) return -1;
                 memcpy(w, &fri_roots[4 * si], 32);
                 w += 4;
-                memcpy(w, vals.data(), vals.size() * 8);
-                w += vals.size();
-                memcpy(w, sibs.data(), sibs.size() * 8);
-                w += sibs.size();
+                uint64_t *vals = w, *sibs = w + q() * width;
+                w = sibs + (uint64_t)q() * fri_steps[si] * 4;
+                if (fri_open(si, ngroups, width, yq, vals, sibs)) return -1;
             }
             if (si < fri_steps.size() - 1)
                 for (auto &y : yq) y %= (1ULL << fri_steps[si + 1]);
         }
-        if (open_s0(ys, w)) return -1;
+        if (open_s0(ys, w) || flush_opens()) return -1;
         memcpy(w, final_pol.data(), final_pol.size() * 8);
         w += final_pol.size();
         if (tstop("STARK_STEP_FRI_QUERIES")) return -1;
@@ -827,32 +826,43 @@ public:
         return 0;
     }
     // its openings at groups yq (vals q x width, siblings q x log2(ngroups) x 4)
+    // (queued: written by flush_opens, all of a proof's openings in one round trip)
     virtual int fri_open(size_t si, uint64_t ngroups, uint64_t width, const std::vector<uint64_t> &yq, uint64_t *vals,
                          uint64_t *sibs)
     {
-        CK(zkgpu_gl_merkle_open_rows_dev(vals, sibs, fri_nodes[si], fri_aux[si], width, ngroups, yq.data(), q()));
+        pend_idx.emplace_back(yq);
+        pend.push_back({vals, sibs, fri_nodes[si], fri_aux[si], 0, width, ngroups, pend_idx.back().data(), q(), 1});
         return 0;
     }
 
     // s0: the 4 stage trees + the constant tree at the original indices
+    // (queued like fri_open): vals of the 5 trees, then their siblings
     virtual int open_s0(const std::vector<uint64_t> &ys, uint64_t *&w)
     {
         const uint32_t secs[5] = {SEC_CM1_2NS, SEC_CM2_2NS, SEC_CM3_2NS, SEC_CM4_2NS, SEC_CONST_2NS};
         const uint32_t widths[5] = {info.n_cm1, info.n_cm2, info.n_cm3, info.n_cm4, info.n_const};
         uint64_t *trees[5] = {nodes[0], nodes[1], nodes[2], nodes[3], const_nodes};
-        std::vector<std::vector<uint64_t>> sib_all(5);
+        uint64_t *sib = w;
+        for (int t = 0; t < 5; t++) sib += (uint64_t)q() * widths[t];
+        pend_idx.emplace_back(ys);
         for (int t = 0; t < 5; t++) {
-            std::vector<uint64_t> vals((uint64_t)q() * widths[t] + 1);
-            sib_all[t].resize((uint64_t)q() * info.n_bits_ext * 4);
-            CK(zkgpu_gl_merkle_open_dev(vals.data(), sib_all[t].data(), trees[t], S.sec[secs[t]], NE, widths[t], NE,
-                                        ys.data(), q()));
-            memcpy(w, vals.data(), (uint64_t)q() * widths[t] * 8);
+            pend.push_back({w, sib, trees[t], S.sec[secs[t]], NE, widths[t], NE, pend_idx.back().data(), q(), 0});
             w += (uint64_t)q() * widths[t];
+            sib += (uint64_t)q() * info.n_bits_ext * 4;
         }
-        for (int t = 0; t < 5; t++) {
-            memcpy(w, sib_all[t].data(), sib_all[t].size() * 8);
-            w += sib_all[t].size();
-        }
+        w = sib;
+        return 0;
+    }
+
+    // the queued openings (fri_open / open_s0 of this class)
+    std::vector<zkgpu_open_req> pend;
+    std::vector<std::vector<uint64_t>> pend_idx;
+    int flush_opens()
+    {
+        const int rc = pend.empty() ? 0 : zkgpu_gl_merkle_open_many(pend.data(), (uint32_t)pend.size());
+        pend.clear();
+        pend_idx.clear();
+        CK(rc);
         return 0;
     }
 };

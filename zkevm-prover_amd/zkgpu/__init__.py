@@ -106,6 +106,7 @@ _SIGS = {
     "zkgpu_h1h2_shard_deal": (ctypes.c_int, [vp, u64, vp, u64, vp, vp, u64, u32]),
     "zkgpu_h1h2_shard_place": (ctypes.c_int, [vp, u64, vp, u64, vp, u64, u64, u64, u64, u32]),
     "zkgpu_gl_merkle_open_rows_dev": (ctypes.c_int, [vp, vp, vp, vp, u64, u64, vp, u64]),
+    "zkgpu_gl_merkle_open_many": (ctypes.c_int, [vp, u32]),
     "zkgpu_prof_enable": (ctypes.c_int, [ctypes.c_int]),
     "zkgpu_prof_reset": (ctypes.c_int, []),
     "zkgpu_prof_query": (ctypes.c_int, [ctypes.c_char_p, pu64, ctypes.POINTER(ctypes.c_double),
@@ -127,6 +128,12 @@ def build():
     return LIB_PATH
 
 
+def _absent(name):
+    def call(*_):
+        raise ZkgpuError("%s is not exported by %s (an older build)" % (name, LIB_PATH))
+    return call
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -144,7 +151,10 @@ def lib():
             pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
-            f = getattr(L, name)
+            f = getattr(L, name, None)
+            if f is None:  # an older build (A/B runs, ZKGPU_LIB_DIR): the entry point fails when called
+                setattr(L, name, _absent(name))
+                continue
             f.restype = res
             f.argtypes = args
         _lib = L
@@ -582,6 +592,32 @@ def merkle_open_rows_dev(nodes, src, ncols, nrows, idx):
     _check(lib().zkgpu_gl_merkle_open_rows_dev(vals.ctypes.data, sibs.ctypes.data, _addr(nodes), _addr(src), ncols,
                                                nrows, idx.ctypes.data, nq), "zkgpu_gl_merkle_open_rows_dev")
     return vals, sibs
+
+
+class OpenReq(ctypes.Structure):
+    """zkgpu_open_req (include/zkgpu.h)"""
+    _fields_ = [("vals_out", vp), ("sibs_out", vp), ("nodes", vp), ("src", vp), ("ld", u64), ("ncols", u64),
+                ("nrows", u64), ("idx", vp), ("nq", u64), ("rows", u32)]
+
+
+def merkle_open_many(reqs):
+    """Several trees' openings in one round trip (zkgpu_gl_merkle_open_many).
+    reqs: (nodes, src, ld, ncols, nrows, idx, rows) per tree -- rows=False is
+    merkle_open_dev's column-major source (ld), rows=True merkle_open_rows_dev's
+    row-major one.  Returns [(vals, sibs)] in request order."""
+    out, keep = [], []
+    arr = (OpenReq * max(1, len(reqs)))()
+    for k, (nodes, src, ld, ncols, nrows, idx, rows) in enumerate(reqs):
+        idx = np.ascontiguousarray(_np(idx).reshape(-1))
+        nlev = max(0, int(nrows).bit_length() - 1)
+        vals = np.zeros((idx.size, ncols), np.uint64)
+        sibs = np.zeros((idx.size, nlev, 4), np.uint64)
+        keep.append(idx)
+        out.append((vals, sibs))
+        arr[k] = OpenReq(vals.ctypes.data, sibs.ctypes.data, _addr(nodes), _addr(src), ld, ncols, nrows,
+                         idx.ctypes.data, idx.size, 1 if rows else 0)
+    _check(lib().zkgpu_gl_merkle_open_many(arr, len(reqs)), "zkgpu_gl_merkle_open_many")
+    return out
 
 
 def h1h2_dev(h1, h1_ld, h2, h2_ld, f, f_ld, t, t_ld, n, dim):
