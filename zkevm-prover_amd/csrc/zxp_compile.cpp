@@ -73,21 +73,30 @@ struct F3 {
 inline F3 f3(uint64_t a, uint64_t b = 0, uint64_t c = 0) { return F3{{a, b, c}}; }
 inline F3 add3(const F3 &a, const F3 &b) { return f3(fadd(a.v[0], b.v[0]), fadd(a.v[1], b.v[1]), fadd(a.v[2], b.v[2])); }
 inline F3 sub3(const F3 &a, const F3 &b) { return f3(fsub(a.v[0], b.v[0]), fsub(a.v[1], b.v[1]), fsub(a.v[2], b.v[2])); }
-// F_p[x]/(x^3 - x - 1), polinomial.hpp:195-205
-inline F3 mul3(const F3 &a, const F3 &b)
-{
-    if (b.base()) return f3(fmul(a.v[0], b.v[0]), fmul(a.v[1], b.v[0]), fmul(a.v[2], b.v[0]));
-    if (a.base()) return f3(fmul(b.v[0], a.v[0]), fmul(b.v[1], a.v[0]), fmul(b.v[2], a.v[0]));
-    uint64_t c[5] = {0, 0, 0, 0, 0};
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) c[i + j] = fadd(c[i + j], fmul(a.v[i], b.v[j]));
-    // x^4 = x^2 + x, x^3 = x + 1
-    c[2] = fadd(c[2], c[4]);
-    c[1] = fadd(c[1], c[4]);
-    c[1] = fadd(c[1], c[3]);
-    c[0] = fadd(c[0], c[3]);
-    return f3(c[0], c[1], c[2]);
-}
+// F_p[x]/(x^3 - x - 1), polinomial.hpp:195-205.  A multiplier with its
+// pairwise sums precomputed: the product in 6 base multiplications
+// (Karatsuba: c1 = (a0+a1)(b0+b1) - a0b0 - a1b1, ...) instead of 9 -- a
+// compiled program scales ~10^5 coefficients by the same constant (scale)
+struct Mul3 {
+    uint64_t b0, b1, b2, b01, b02, b12;
+    bool base;
+    explicit Mul3(const F3 &b)
+        : b0(b.v[0]), b1(b.v[1]), b2(b.v[2]), b01(fadd(b.v[0], b.v[1])), b02(fadd(b.v[0], b.v[2])),
+          b12(fadd(b.v[1], b.v[2])), base(b.base())
+    {
+    }
+    F3 operator()(const F3 &a) const
+    {
+        if (base) return f3(fmul(a.v[0], b0), fmul(a.v[1], b0), fmul(a.v[2], b0));
+        if (a.base()) return f3(fmul(b0, a.v[0]), fmul(b1, a.v[0]), fmul(b2, a.v[0]));
+        const uint64_t p0 = fmul(a.v[0], b0), p1 = fmul(a.v[1], b1), p2 = fmul(a.v[2], b2);
+        const uint64_t c1 = fsub(fsub(fmul(fadd(a.v[0], a.v[1]), b01), p0), p1);
+        const uint64_t c2 = fadd(fsub(fsub(fmul(fadd(a.v[0], a.v[2]), b02), p0), p2), p1);
+        const uint64_t c3 = fsub(fsub(fmul(fadd(a.v[1], a.v[2]), b12), p1), p2);
+        // x^4 = x^2 + x, x^3 = x + 1
+        return f3(fadd(p0, c3), fadd(fadd(c1, p2), c3), fadd(c2, p2));
+    }
+};
 
 enum { FK_CONST = 0, FK_LIN = 1, FK_SPECIAL = 2 };
 
@@ -121,7 +130,9 @@ struct Form {
     int32_t alias = -1;  // output operand holding exactly this value, or -1
     F3 cst = f3(0);
     std::vector<Term> t;  // sorted by key, no zero coefficients
+    uint64_t cols = 0;    // Bloom bits (col_bit) of the columns its terms read: a superset
 };
+inline uint64_t col_bit(uint32_t sec, uint32_t col) { return 1ULL << ((col * 0x9E37u + sec * 31u) & 63u); }
 
 struct Compiler {
     const zxp_instr *in;
@@ -140,6 +151,18 @@ struct Compiler {
     uint32_t n_ssa1 = 0, n_ssa3 = 0;
     std::vector<Form> st1, st3;  // current value of every source temporary
     std::vector<uint8_t> set1, set3;
+    // output operand of a source COL operand (k) / of COL3 component j (3k + j):
+    // intern's answer, kept (a program reads its columns ~10^4 times)
+    std::vector<uint32_t> col_out;
+    uint32_t col_operand(uint32_t k, uint32_t j)
+    {
+        const zxp_operand &o = op[k];
+        if (col_out.empty()) col_out.assign(3ULL * n_src_opnd, UINT32_MAX);
+        uint32_t &r = col_out[3ULL * k + j];
+        if (r == UINT32_MAX) r = intern(ZXP_COL, o.a, o.b + j, o.c);
+        return r;
+    }
+    uint32_t n_src_opnd = 0;
     std::unordered_map<OKey, Form, OKeyHash> fwd;  // {sec, col, shift, 0} -> value this row stored there
 
     uint32_t intern(uint32_t kind, uint32_t a, uint32_t b = 0, uint32_t c = 0)
@@ -198,18 +221,23 @@ struct Compiler {
         case ZXP_TMP1: return set1[o.a] ? st1[o.a] : constant(f3(0), 1, -1);
         case ZXP_TMP3: return set3[o.a] ? st3[o.a] : constant(f3(0), 3, -1);
         case ZXP_COL: {
-            auto it = fwd.find(OKey{{o.a, o.b, o.c, 0}});
-            if (it != fwd.end()) return it->second;
-            return identity(intern(ZXP_COL, o.a, o.b, o.c), 1);
+            if (!fwd.empty()) {
+                auto it = fwd.find(OKey{{o.a, o.b, o.c, 0}});
+                if (it != fwd.end()) return it->second;
+            }
+            Form f = identity(col_operand(k, 0), 1);
+            f.cols = col_bit(o.a, o.b);
+            return f;
         }
         case ZXP_COL3: {
             bool any = false;
-            for (uint32_t j = 0; j < 3; j++) any |= fwd.count(OKey{{o.a, o.b + j, o.c, 0}}) != 0;
+            for (uint32_t j = 0; j < 3 && !fwd.empty(); j++) any |= fwd.count(OKey{{o.a, o.b + j, o.c, 0}}) != 0;
             if (any) {  // sum_j X^j * component j (forwarded or read)
                 Form f = constant(f3(0), 3, -1);
                 for (uint32_t j = 0; j < 3; j++) {
                     auto it = fwd.find(OKey{{o.a, o.b + j, o.c, 0}});
-                    const Form c = it != fwd.end() ? it->second : identity(intern(ZXP_COL, o.a, o.b + j, o.c), 1);
+                    Form c = it != fwd.end() ? it->second : identity(col_operand(k, j), 1);
+                    if (it == fwd.end()) c.cols = col_bit(o.a, o.b + j);
                     F3 e = f3(0);
                     e.v[j] = 1;
                     f = combine(f, scale(c, e, 3), false);
@@ -225,9 +253,11 @@ struct Compiler {
             for (uint32_t j = 0; j < 3; j++) {
                 F3 e = f3(0);
                 e.v[j] = 1;
-                f.t.push_back(Term{intern(ZXP_COL, o.a, o.b + j, o.c) * 4, e});
+                f.t.push_back(Term{col_operand(k, j) * 4, e});
+                f.cols |= col_bit(o.a, o.b + j);
             }
-            std::sort(f.t.begin(), f.t.end(), [](const Term &x, const Term &y) { return x.key < y.key; });
+            for (int a = 1; a < 3; a++)  // (three keys: insertion sort)
+                for (int b = a; b > 0 && f.t[b].key < f.t[b - 1].key; b--) std::swap(f.t[b], f.t[b - 1]);
             return f;
         }
         case ZXP_LIT: return constant(f3(((uint64_t)o.a | ((uint64_t)o.b << 32)) % P), 1, intern(ZXP_LIT, o.a, o.b));
@@ -279,6 +309,7 @@ struct Compiler {
         Form r;
         r.dim = std::max(a.dim, b.dim);
         r.cst = sub ? sub3(a.cst, b.cst) : add3(a.cst, b.cst);
+        r.cols = a.cols | b.cols;
         r.t.reserve(a.t.size() + b.t.size());
         size_t i = 0, j = 0;
         while (i < a.t.size() || j < b.t.size()) {
@@ -302,10 +333,12 @@ struct Compiler {
     {
         Form r;
         r.dim = (uint8_t)dim;
-        r.cst = mul3(a.cst, s);
+        const Mul3 ms(s);
+        r.cst = ms(a.cst);
+        r.cols = a.cols;
         if (!s.zero()) {
             r.t.reserve(a.t.size());
-            for (const Term &t : a.t) r.t.push_back(Term{t.key, mul3(t.c, s)});
+            for (const Term &t : a.t) r.t.push_back(Term{t.key, ms(t.c)});
         }
         r.kind = r.t.empty() ? FK_CONST : FK_LIN;
         return r;
@@ -397,13 +430,15 @@ struct Compiler {
     // before storing columns [c0, c1) of sec: materialise the pending forms reading them
     void column_hazard(uint32_t sec, uint32_t c0, uint32_t c1)
     {
+        uint64_t mask = 0;  // (a form whose Bloom bits miss the stored columns reads none of them)
+        for (uint32_t c = c0; c < c1; c++) mask |= col_bit(sec, c);
         for (size_t k = 0; k < st1.size(); k++)
-            if (set1[k] && reads_cols(st1[k], sec, c0, c1)) {
+            if (set1[k] && (st1[k].cols & mask) && reads_cols(st1[k], sec, c0, c1)) {
                 st1[k].alias = -1;
                 realize(st1[k]);
             }
         for (size_t k = 0; k < st3.size(); k++)
-            if (set3[k] && reads_cols(st3[k], sec, c0, c1)) {
+            if (set3[k] && (st3[k].cols & mask) && reads_cols(st3[k], sec, c0, c1)) {
                 st3[k].alias = -1;
                 realize(st3[k]);
             }
@@ -865,6 +900,7 @@ extern "C" int zkgpu_zxp_compile(const void *instr, uint32_t n_instr, const void
     c.evals = evals;
     c.max_terms = max_terms;
     c.n_src_tmp1 = n_tmp1;
+    c.n_src_opnd = n_opnd;
     c.n_src_tmp3 = n_tmp3;
     c.run();
     uint32_t t1 = 1, t3 = 1;
