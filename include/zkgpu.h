@@ -305,6 +305,19 @@ int zkgpu_calculate_z_dev(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint6
  * total == 1. */
 int zkgpu_calculate_z_block_dev(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,
                                 uint64_t den_ld, uint64_t n, const uint64_t z0[3], uint64_t total[3]);
+/* Every grand product of a stage (starks.cpp:165-189: calculateZ per
+ * permutation / plookup / connection context) in one round trip: request k is
+ * zkgpu_calculate_z_dev's (z, z_ld, num, num_ld, den, den_ld) over the same n;
+ * closes[k] as there.  One read-back of the nz totals instead of nz. */
+typedef struct zkgpu_z_req {
+    uint64_t *z;
+    uint64_t z_ld;
+    const uint64_t *num;
+    uint64_t num_ld;
+    const uint64_t *den;
+    uint64_t den_ld;
+} zkgpu_z_req;
+int zkgpu_calculate_z_many_dev(const zkgpu_z_req *req, uint32_t nz, uint64_t n, int *closes);
 
 /* Starks::evmap (starks.cpp:556-669): evals[e] = sum_{k<n} L(k) * pol_e[k << extend_bits],
  * L = lev or lpev (device, 3 columns of ld l_ld).  cols = host array of device
@@ -417,6 +430,16 @@ int zkgpu_prof_reset(void);
 int zkgpu_prof_query(const char *kernel, uint64_t *launches, double *total_ms, double *total_bytes);
 /* names of kernels seen since the last reset, '\n'-separated, into buf */
 int zkgpu_prof_kernels(char *buf, uint64_t buflen);
+
+/* Stream marks (no reference counterpart: the reference times its stages on
+ * the CPU, TimerStart / TimerStopAndLog around synchronous code): the host
+ * prover's stage timers without a device synchronisation per stage.
+ * zkgpu_mark records event `slot` (< ZKGPU_MARKS) on the library stream;
+ * zkgpu_mark_elapsed waits for event b and returns the milliseconds from
+ * event a to event b. */
+#define ZKGPU_MARKS 256
+int zkgpu_mark(uint32_t slot);
+int zkgpu_mark_elapsed(uint32_t a, uint32_t b, double *ms);
 
 #ifdef __cplusplus
 }

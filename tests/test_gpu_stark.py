@@ -211,6 +211,15 @@ def test_calculate_z_dev(oracle, zkgpu):
     den2[5, 0] ^= 3
     dden2 = zkgpu.to_device(np.ascontiguousarray(den2.T))
     assert not zkgpu.calculate_z_dev(dz, n, dnum, n, dden2, n, n)
+    # the batched form (one read-back for a stage's grand products): the same
+    # columns and verdicts, a failing product between closing ones
+    dzs = [torch.zeros((3, n), dtype=torch.int64, device="cuda:0") for _ in range(3)]
+    got = zkgpu.calculate_z_many_dev([(dzs[0], n, dnum, n, dden, n), (dzs[1], n, dnum, n, dden2, n),
+                                      (dzs[2], n, dnum, n, dden, n)], n)
+    assert got == [True, False, True]
+    assert np.array_equal(zkgpu.from_device(dzs[0]).T, zref)
+    assert np.array_equal(zkgpu.from_device(dzs[2]).T, zref)
+    assert np.array_equal(zkgpu.from_device(dzs[1]), zkgpu.from_device(dz))
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])

@@ -1332,6 +1332,34 @@ int zkgpu_calculate_z_block_dev(uint64_t *z, uint64_t z_ld, const uint64_t *num,
     return check_hip(hipStreamSynchronize(g_ctx.stream), "calculateZ sync");
 }
 
+int zkgpu_calculate_z_many_dev(const zkgpu_z_req *req, uint32_t nz, uint64_t n, int *closes)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!nz) return 0;
+    if (!req || !closes) return set_error(ZKGPU_ERR_ARG, "calculate_z_many: null argument");
+    if (!n) {
+        for (uint32_t k = 0; k < nz; k++) closes[k] = 1;  // an empty product
+        return 0;
+    }
+    // the requests run in stream order on one scratch; each keeps its total
+    const size_t words = calculate_z_scratch_words(n);
+    uint64_t *scr = workspace(2, (words + 3ULL * nz + 8) * sizeof(uint64_t));
+    if (!scr) return ZKGPU_ERR_OOM;
+    uint64_t *tot = scr + words;
+    const uint64_t one[3] = {1, 0, 0};
+    for (uint32_t k = 0; k < nz; k++)
+        if ((rc = calculate_z(req[k].z, req[k].z_ld, req[k].num, req[k].num_ld, req[k].den, req[k].den_ld, n, one, scr,
+                              tot + 3ULL * k, g_ctx.stream)))
+            return rc;
+    std::vector<uint64_t> t(3ULL * nz);
+    if ((rc = check_hip(hipMemcpyAsync(t.data(), tot, t.size() * 8, hipMemcpyDeviceToHost, g_ctx.stream), "D2H")))
+        return rc;
+    if ((rc = check_hip(hipStreamSynchronize(g_ctx.stream), "calculateZ sync"))) return rc;
+    for (uint32_t k = 0; k < nz; k++) closes[k] = (t[3 * k] == 1 && t[3 * k + 1] == 0 && t[3 * k + 2] == 0) ? 1 : 0;
+    return 0;
+}
+
 int zkgpu_calculate_z_dev(uint64_t *z, uint64_t z_ld, const uint64_t *num, uint64_t num_ld, const uint64_t *den,
                           uint64_t den_ld, uint64_t n, int *closes)
 {
@@ -1790,6 +1818,27 @@ int zkgpu_prof_kernels(char *buf, uint64_t buflen)
     size_t n = out.size() < buflen - 1 ? out.size() : buflen - 1;
     memcpy(buf, out.data(), n);
     buf[n] = 0;
+    return 0;
+}
+// stream marks for the host prover's stage timers (no synchronisation)
+static hipEvent_t g_marks[ZKGPU_MARKS];
+int zkgpu_mark(uint32_t slot)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (slot >= ZKGPU_MARKS) return set_error(ZKGPU_ERR_ARG, "mark: slot %u >= %d", slot, ZKGPU_MARKS);
+    if (!g_marks[slot] && (rc = check_hip(hipEventCreate(&g_marks[slot]), "mark event"))) return rc;
+    return check_hip(hipEventRecord(g_marks[slot], g_ctx.stream), "mark record");
+}
+int zkgpu_mark_elapsed(uint32_t a, uint32_t b, double *ms)
+{
+    int rc;
+    if (a >= ZKGPU_MARKS || b >= ZKGPU_MARKS || !g_marks[a] || !g_marks[b] || !ms)
+        return set_error(ZKGPU_ERR_ARG, "mark_elapsed: slots %u / %u not recorded", a, b);
+    if ((rc = check_hip(hipEventSynchronize(g_marks[b]), "mark sync"))) return rc;
+    float t = 0;
+    if ((rc = check_hip(hipEventElapsedTime(&t, g_marks[a], g_marks[b]), "mark elapsed"))) return rc;
+    *ms = t;
     return 0;
 }
 }  // extern "C"

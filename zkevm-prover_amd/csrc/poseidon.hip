@@ -184,6 +184,32 @@ __global__ void __launch_bounds__(256) k_merkle_level_lp(uint64_t *dst, const ui
     if (c.x < 4) dst[4 * i + c.x] = gl_canon(s);
 }
 
+// A tree's last levels (<= LP_TAIL nodes: one 16-lane group per node in one
+// 1024-thread workgroup) in one launch, a workgroup barrier between levels:
+// each level still costs one lane-parallel permutation's latency, but not a
+// dependent launch's ~10 us (per-dispatch trace: 7 such levels per tree, ~9
+// trees per config-4 proof)
+constexpr uint64_t LP_TAIL = 64;
+__global__ void __launch_bounds__(1024) k_merkle_tail_lp(uint64_t *lvl, uint64_t pending)
+{
+    __shared__ uint64_t lds[1024];
+    LpCtx c;
+    lp_init(c, lds);
+    const uint64_t i = threadIdx.x / LP_LANES;
+    while (pending > 1) {
+        const uint64_t next = pending / 2;
+        uint64_t *dst = lvl + 4 * pending;
+        if (i < next) {  // whole 16-lane groups
+            uint64_t s = c.x < 8 ? lvl[8 * i + c.x] : 0;
+            s = lp_perm(c, s);
+            if (c.x < 4) dst[4 * i + c.x] = gl_canon(s);
+        }
+        __syncthreads();  // this level's nodes stored before the next level reads them (one workgroup)
+        lvl = dst;
+        pending = next;
+    }
+}
+
 // leaf digests (linear_hash) of a row-major source, 16 lanes per row
 __global__ void __launch_bounds__(256) k_leaves_rows_lp(uint64_t *digests, const uint64_t *__restrict__ src,
                                                        uint64_t ncols, uint64_t nrows)
@@ -294,6 +320,12 @@ int merkle_levels(uint64_t *nodes, uint64_t nrows, hipStream_t s)
     uint64_t off = 0, pending = nrows;
     while (pending > 1) {
         uint64_t next = pending / 2;
+        if (next <= LP_TAIL) {  // the remaining levels in one launch
+            prof_begin(s);
+            hipLaunchKernelGGL(k_merkle_tail_lp, dim3(1), dim3(1024), 0, s, nodes + off, pending);
+            prof_end("k_merkle_level", 96.0 * (double)(pending - 1), s);
+            break;
+        }
         prof_begin(s);
         if (next <= LP_MAX_PERMS)
             hipLaunchKernelGGL(k_merkle_level_lp, dim3(blocks_for(next * LP_LANES, 256)), dim3(256), 0, s,

@@ -1060,6 +1060,8 @@ public:
     int prove_sharded(uint64_t *out)
     {
         timers.clear();
+        pend_t.clear();
+        n_marks = 0;
         n_exch = sent_bytes = max_sent = 0;
         auto tall = clk::now();
         Transcript tr;

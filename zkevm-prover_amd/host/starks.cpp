@@ -513,13 +513,42 @@ public:
         return L;
     }
 
+    // Stage timers (the reference's TimerStart / TimerStopAndLog) between
+    // stream marks, resolved once at the end of the proof (flush_timers): a
+    // stage boundary costs no device synchronisation (config-4: ~20 per
+    // proof, each a dependent launch's gap); the synchronous form only when
+    // the mark pool is spent
     using clk = std::chrono::steady_clock;
     clk::time_point t0;
-    void tstart() { t0 = clk::now(); }
+    uint32_t t0_mark = UINT32_MAX, n_marks = 0;
+    std::vector<std::pair<size_t, std::pair<uint32_t, uint32_t>>> pend_t;  // timer index, marks
+    void tstart()
+    {
+        t0 = clk::now();
+        t0_mark = UINT32_MAX;
+        if (n_marks + 1 < ZKGPU_MARKS && !zkgpu_mark(n_marks)) t0_mark = n_marks++;
+    }
     int tstop(const char *name)
     {
+        if (t0_mark != UINT32_MAX && n_marks < ZKGPU_MARKS && !zkgpu_mark(n_marks)) {
+            pend_t.push_back({timers.size(), {t0_mark, n_marks++}});
+            timers.emplace_back(name, 0.0);
+            return 0;
+        }
         CK(zkgpu_synchronize());
         timers.emplace_back(name, std::chrono::duration<double, std::milli>(clk::now() - t0).count());
+        return 0;
+    }
+    int flush_timers()
+    {
+        for (const auto &p : pend_t) {
+            double ms = 0;
+            CK(zkgpu_mark_elapsed(p.second.first, p.second.second, &ms));
+            timers[p.first].second = ms;
+        }
+        pend_t.clear();
+        n_marks = 0;
+        t0_mark = UINT32_MAX;
         return 0;
     }
 
@@ -549,6 +578,8 @@ public:
     int prove_body(uint64_t *out)
     {
         timers.clear();
+        pend_t.clear();
+        n_marks = 0;
         auto tall = clk::now();
         Transcript tr;
         tr.put(verkey, 4);
@@ -654,13 +685,14 @@ public:
     // calculateZ of every grand product (starks.cpp:165-189), n domain
     virtual int z_all()
     {
-        for (uint32_t z = 0; z < info.n_zctx; z++) {
-            int closes = 0;
-            CK(zkgpu_calculate_z_dev(S.sec[SEC_CM3_N] + (uint64_t)zctx[3 * z + 2] * N, N,
-                                     S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * z] * N, N,
-                                     S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * z + 1] * N, N, N, &closes));
-            if (!closes) return fail("calculateZ: grand product %u does not close", z);
-        }
+        std::vector<zkgpu_z_req> req(info.n_zctx);
+        for (uint32_t z = 0; z < info.n_zctx; z++)
+            req[z] = {S.sec[SEC_CM3_N] + (uint64_t)zctx[3 * z + 2] * N, N, S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * z] * N, N,
+                      S.sec[SEC_TMP_N] + (uint64_t)zctx[3 * z + 1] * N, N};
+        std::vector<int> closes(info.n_zctx + 1, 0);
+        CK(zkgpu_calculate_z_many_dev(req.data(), info.n_zctx, N, closes.data()));
+        for (uint32_t z = 0; z < info.n_zctx; z++)
+            if (!closes[z]) return fail("calculateZ: grand product %u does not close", z);
         return 0;
     }
 
@@ -795,7 +827,7 @@ public:
         if (open_s0(ys, w) || flush_opens()) return -1;
         memcpy(w, final_pol.data(), final_pol.size() * 8);
         w += final_pol.size();
-        if (tstop("STARK_STEP_FRI_QUERIES")) return -1;
+        if (tstop("STARK_STEP_FRI_QUERIES") || flush_timers()) return -1;
         if (tr.err) return fail("transcript hashing failed: %s", zkgpu_last_error());
         if ((uint64_t)(w - out) != proof_len()) return fail("proof length mismatch");
         timers.emplace_back("STARK_TOTAL", std::chrono::duration<double, std::milli>(clk::now() - tall).count());

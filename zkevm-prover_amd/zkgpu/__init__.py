@@ -107,11 +107,14 @@ _SIGS = {
     "zkgpu_h1h2_shard_place": (ctypes.c_int, [vp, u64, vp, u64, vp, u64, u64, u64, u64, u32]),
     "zkgpu_gl_merkle_open_rows_dev": (ctypes.c_int, [vp, vp, vp, vp, u64, u64, vp, u64]),
     "zkgpu_gl_merkle_open_many": (ctypes.c_int, [vp, u32]),
+    "zkgpu_calculate_z_many_dev": (ctypes.c_int, [vp, u32, u64, vp]),
     "zkgpu_prof_enable": (ctypes.c_int, [ctypes.c_int]),
     "zkgpu_prof_reset": (ctypes.c_int, []),
     "zkgpu_prof_query": (ctypes.c_int, [ctypes.c_char_p, pu64, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_double)]),
     "zkgpu_prof_kernels": (ctypes.c_int, [ctypes.c_char_p, u64]),
+    "zkgpu_mark": (ctypes.c_int, [u32]),
+    "zkgpu_mark_elapsed": (ctypes.c_int, [u32, u32, ctypes.POINTER(ctypes.c_double)]),
     # include/zkgpu_parser.h (bindings in zkgpu/parser.py)
     "zkgpu_parser_convert": (ctypes.c_int, [u32, vp, u64, vp, u64, vp, u32, u32, u32, vp]),
     "zkgpu_steps_parser_eval": (ctypes.c_int, [u32, vp, u64, vp, u64, vp, u32, u32, u32, vp]),
@@ -404,6 +407,22 @@ def calculate_z_dev(z, z_ld, num, num_ld, den, den_ld, n):
                                        ctypes.byref(closes)), "zkgpu_calculate_z_dev")
     return bool(closes.value)
 
+
+
+class ZReq(ctypes.Structure):
+    """zkgpu_z_req (include/zkgpu.h)"""
+    _fields_ = [("z", vp), ("z_ld", u64), ("num", vp), ("num_ld", u64), ("den", vp), ("den_ld", u64)]
+
+
+def calculate_z_many_dev(reqs, n):
+    """Several grand products in one round trip (zkgpu_calculate_z_many_dev):
+    reqs = [(z, z_ld, num, num_ld, den, den_ld)]; returns [closes] per request."""
+    arr = (ZReq * max(1, len(reqs)))()
+    for k, (z, z_ld, num, num_ld, den, den_ld) in enumerate(reqs):
+        arr[k] = ZReq(_addr(z), z_ld, _addr(num), num_ld, _addr(den), den_ld)
+    closes = (ctypes.c_int * max(1, len(reqs)))()
+    _check(lib().zkgpu_calculate_z_many_dev(arr, len(reqs), n, closes), "zkgpu_calculate_z_many_dev")
+    return [bool(closes[k]) for k in range(len(reqs))]
 
 
 def calculate_z_block_dev(z, z_ld, num, num_ld, den, den_ld, n, z0=(1, 0, 0)):
