@@ -180,6 +180,28 @@ def test_merkle_open_many_vs_oracle(oracle, zkgpu):
     bad[-1] = bad[-1][:5] + (np.array([0, bad[-1][4]], np.uint64),) + bad[-1][6:]
     with pytest.raises(zkgpu.ZkgpuError, match="index"):
         zkgpu.merkle_open_many(bad)
+    bad[-1] = bad[-1][:4] + (bad[-1][4] - 1, np.zeros(1, np.uint64)) + bad[-1][6:]
+    with pytest.raises(zkgpu.ZkgpuError, match="power of two"):
+        zkgpu.merkle_open_many(bad)
+    assert zkgpu.merkle_open_many([]) == []
+
+
+def test_stream_marks(zkgpu):
+    """zkgpu_mark / zkgpu_mark_elapsed (the host prover's stage timers): the
+    time between two marks around queued work, and the argument checks."""
+    import ctypes
+    import torch
+    L = zkgpu.lib()
+    nodes = torch.zeros(zkgpu.merkle_num_elements(1 << 12), dtype=torch.int64, device="cuda:0")
+    src = zkgpu.to_device(np.ascontiguousarray(rand_gl(np.random.default_rng(5), (1 << 12, 9)).T))
+    assert L.zkgpu_mark(200) == 0
+    zkgpu.merkletree_dev(nodes, src, 1 << 12, 9, 1 << 12)
+    assert L.zkgpu_mark(201) == 0
+    ms = ctypes.c_double(-1.0)
+    assert L.zkgpu_mark_elapsed(200, 201, ctypes.byref(ms)) == 0
+    assert 0.0 < ms.value < 1000.0
+    assert L.zkgpu_mark(256) != 0  # (ZKGPU_MARKS slots)
+    assert L.zkgpu_mark_elapsed(200, 255, ctypes.byref(ms)) != 0  # never recorded
 
 
 # ------------------------------------------------------------------ FRI

@@ -220,6 +220,8 @@ def test_calculate_z_dev(oracle, zkgpu):
     assert np.array_equal(zkgpu.from_device(dzs[0]).T, zref)
     assert np.array_equal(zkgpu.from_device(dzs[2]).T, zref)
     assert np.array_equal(zkgpu.from_device(dzs[1]), zkgpu.from_device(dz))
+    assert zkgpu.calculate_z_many_dev([], n) == []
+    assert zkgpu.calculate_z_many_dev([(dzs[0], n, dnum, n, dden2, n)], 0) == [True]  # an empty product
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
