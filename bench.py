@@ -383,23 +383,45 @@ def stark_valu(kernel, ms_per_proof, launches_per_proof, family="poseidon"):
 
 
 # ---------------------------------------------------------------- timing helpers
-def timed(step, steps, warmup, world, dist, torch):
+def timed(step, steps, warmup, world, dist, torch, prepare=None):
+    """K steps bracketed by a barrier + synchronize on both sides.  With
+    `prepare` (a step that consumes its input: the lean-plan prover extends
+    the trace in place), each step gets its own bracket and prepare() runs
+    between them, outside the timing; elapsed = the sum of the brackets."""
     for _ in range(warmup):
+        if prepare:
+            prepare()
         step()
     torch.cuda.synchronize()
     import zkgpu
     zkgpu.prof_reset()
-    zkgpu.prof_enable(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    if prepare is None:
+        zkgpu.prof_enable(True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+    else:
+        elapsed = 0.0
+        for _ in range(steps):
+            prepare()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            zkgpu.prof_enable(True)
+            t0 = time.perf_counter()
+            step()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            elapsed += time.perf_counter() - t0
+            zkgpu.prof_enable(False)
     zkgpu.prof_enable(False)
     kernels = {}
     for k in zkgpu.prof_kernels():
@@ -604,7 +626,8 @@ def quotient_measure(args, dev, torch, world, dist):
            "what": "step42ns-shaped synthetic program (zkgpu/synthetic_bytecode.py seed 1, the reference step42ns's "
                    "opcode histogram / temporaries / fork-9 map, tests/golden/zkevm_bytecode_shape.json) -> product "
                    "converter -> ZXP compile -> segment kernels; 2^24-row extended domain, sections resident in HBM; "
-                   "parity: tests/test_gpu_parser.py (full size, 2^16 rows, vs the oracle parser)"}
+                   "parity: tests/test_gpu_full_parity.py (these segment kernels at the 2^24-row domain on ~1,000 "
+                   "sampled rows, incl. the wrap rows, vs the oracle's case-table interpreter)"}
     f, d, why = _stamped("*_s42_pmc.json", "zxp")
     if roof is not None:
         roof["traffic_stamp"] = why
@@ -730,13 +753,17 @@ def sharded_children(args, world, rank, local, dist, torch):
     exchange (zkgpu_comm_host through /dev/shm), which then carries the
     headline with the line saying so, and the fork-9 runs are skipped.
     Returns rank 0's summary."""
-    # fork-9 widths: 2^23 rows from W = 4 (plan 190 GB per rank), 2^22 rows
-    # below it (2^23 needs 386 GB on one GPU, 317 GB per rank at W = 2)
-    small = ["--log-n", "22"] if world < 4 and args.log_n > 22 else []
-    runs = [("config4", []), ("fork9", ["--fork9"] + small), ("fork9_zkevm_shaped", ["--zkevm-shaped"] + small)]
+    # fork-9 widths at 2^23 rows: on one GPU the single-GPU prover under the
+    # lean HBM plan (271 GB; the row-sharded prover at W = 1 would hold every
+    # section: 419 GB); from W = 4 the row-sharded prover (217 GB per rank at
+    # W = 4); at W = 2 it needs 369 GB per rank, so 2^22 rows there
+    small = ["--log-n", "22"] if world == 2 and args.log_n > 22 else []
+    single = world == 1  # the fork-9 runs through `--workload stark` (one GPU, AUTO plan -> lean)
+    runs = [("config4", [], False), ("fork9", ["--fork9"] + small, single),
+            ("fork9_zkevm_shaped", ["--zkevm-shaped"] + small, single)]
     out = {}
-    for name, extra in runs:
-        ok, rec = _sharded_child(args, world, rank, local, dist, torch, extra, "rccl")
+    for name, extra, one_gpu in runs:
+        ok, rec = _sharded_child(args, world, rank, local, dist, torch, extra, "rccl", one_gpu)
         if rank == 0:
             out[name] = rec
         if ok:
@@ -752,16 +779,17 @@ def sharded_children(args, world, rank, local, dist, torch):
                     out[name]["exchange"] = "host shared memory (zkgpu_comm_host): the RCCL run failed"
         # the same code path again would fail the same way: no more runs
         if rank == 0:
-            for later, _ in runs[runs.index((name, extra)) + 1:]:
+            for later, _, _ in runs[runs.index((name, extra, one_gpu)) + 1:]:
                 out[later] = {"error": "skipped after the failed %s run" % name}
         break
     return out if rank == 0 else None
 
 
-def _sharded_child(args, world, rank, local, dist, torch, extra, comm):
+def _sharded_child(args, world, rank, local, dist, torch, extra, comm, one_gpu=False):
     """One `--workload stark-sharded` run as a child process per rank (own
-    rendezvous, --sharded-timeout).  Returns (every rank's child succeeded,
-    rank 0's record)."""
+    rendezvous, --sharded-timeout); one_gpu (world 1): `--workload stark`, the
+    single-GPU prover.  Returns (every rank's child succeeded, rank 0's
+    record)."""
     import signal
     import subprocess
     port = _free_port() if rank == 0 else 0
@@ -774,10 +802,12 @@ def _sharded_child(args, world, rank, local, dist, torch, extra, comm):
     # rank's child here has its own parent)
     env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(local), WORLD_SIZE=str(world),
                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ZKGPU_RUN_ID="bench-%d" % port)
-    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--workload", "stark-sharded",
-           "--steps", "3", "--warmup", "1", "--no-cpu", "--log-n", str(args.log_n), "--blowup-bits",
-           str(args.blowup_bits), "--ncols", str(args.ncols), "--queries", str(args.queries),
-           "--comm", comm] + extra  # (a later --log-n wins)
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(world), "--workload",
+           "stark" if one_gpu else "stark-sharded", "--steps", "3", "--warmup", "1", "--no-cpu", "--log-n",
+           str(args.log_n), "--blowup-bits", str(args.blowup_bits), "--ncols", str(args.ncols), "--queries",
+           str(args.queries), "--comm", comm] + extra  # (a later --log-n wins)
+    if one_gpu:
+        cmd += ["--no-lde", "--no-handoff", "--no-s42", "--no-sharded"]
     t0 = time.time()
     p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                          start_new_session=True)
@@ -806,7 +836,8 @@ def _sharded_child(args, world, rank, local, dist, torch, extra, comm):
     d = json.loads(line)
     st = d.get("stages_ms") or {}
     rec = {"value": d["value"], "unit": d["unit"], "n_gpus": d["n_gpus"], "ms_per_step": d["ms_per_step"],
-           "scaling": "strong", "workload": d["config"]["workload"],
+           "scaling": "strong", "workload": d["config"]["workload"], "log_n": d["config"]["log_n"],
+           "prover": "single-GPU (zkgpu_stark_create)" if one_gpu else "row-sharded (zkgpu_stark_create_sharded)",
            "exchange_ms": round(sum(v for k, v in st.items() if "EXCHANGE" in k and not k.startswith("COUNT_")), 3),
            "stages_ms": {k: v for k, v in st.items() if not k.startswith("COUNT_COMM")},
            "wall_s": round(time.time() - t0, 1)}
@@ -887,6 +918,19 @@ def comm_summary(stages, world):
            "rank0_bytes_sent_per_exchange": int(sent / n) if n else 0,
            "rank0_largest_exchange_bytes": int(stages.get("COUNT_COMM_MAX_BYTES_SENT", 0)),
            "max_ops_per_exchange": int(stages.get("COUNT_COMM_MAX_OPS", 0))}
+    # the device time inside the exchanges (stream marks around each one: the
+    # transfers plus any wait for a slower peer) -> the achieved egress rate
+    # of rank 0, against its W - 1 xGMI links (~153 GB/s each, 7 per MI355X)
+    xms = stages.get("COUNT_COMM_EXCHANGE_MS")
+    if xms:
+        res["exchange_ms_per_proof"] = round(xms, 3)
+        res["achieved_GBps"] = round(sent / (xms * 1e-3) / 1e9, 1)
+        big = stages.get("COUNT_COMM_LARGEST_EXCHANGE_MS")
+        if big:
+            res["largest_exchange_ms"] = round(big, 3)
+            res["largest_exchange_GBps"] = round(res["rank0_largest_exchange_bytes"] / (big * 1e-3) / 1e9, 1)
+        res["link_peak_GBps"] = round(153.0 * (world - 1), 1)
+        res["link_peak_note"] = "(W - 1) xGMI links x ~153 GB/s per direction (task brief figure; 7 links per GPU)"
     if res["comm_world"] != world:
         raise SystemExit("bench.py: the prover's communicator has world %d, the job %d" % (res["comm_world"], world))
     return res
@@ -937,6 +981,7 @@ def main():
     C = args.ncols
     res = {"metric": METRIC}
     gs = inst = None
+    prepare = None
     sharded = None
     lde = roof = handoff = quotient = None
     if args.workload == "lde":
@@ -952,6 +997,10 @@ def main():
             inst = stark_instance(args.log_n, args.blowup_bits, C, args.queries, _kind(args))
             gs = GpuStark(inst)  # setup: constants, constant LDE + tree (untimed; files in the reference)
             gs.witness()         # executor stand-in: committed trace cm1 in HBM (untimed)
+            if gs.memory_mode() == "lean":
+                # the lean HBM plan (include/zkgpu_stark.h) extends the trace in
+                # place: every proof gets a fresh one, loaded outside its timing
+                prepare = gs.witness
 
             def step():
                 gs.prove_raw()
@@ -979,7 +1028,7 @@ def main():
 
             def step():
                 zkgpu.merkletree_dev(nodes, src, n, C, n)
-        elapsed, kernels = timed(step, args.steps, args.warmup, world, dist, torch)
+        elapsed, kernels = timed(step, args.steps, args.warmup, world, dist, torch, prepare)
         elapsed = max_over_ranks(elapsed, world, dist, torch, dev)
         if args.workload in ("stark", "stark-sharded"):
             total = (world if args.workload == "stark" else 1) * args.steps
@@ -992,7 +1041,7 @@ def main():
         stages = gs.timers() if gs is not None else None
         if args.workload == "stark" and not args.no_lde:
             lde, roof = lde_measure(args, dev, torch, world, dist)
-        if args.workload == "stark" and world == 1 and not args.no_handoff:
+        if args.workload == "stark" and world == 1 and not args.no_handoff and prepare is None:
             handoff = handoff_measure(n, inst.n_cm1, dev, torch, zkgpu, value)
             handoff["pipelined"] = handoff_pipelined(gs, value)
         if args.workload == "stark" and world == 1 and args.log_n == 23 and not args.no_s42:
@@ -1038,26 +1087,33 @@ def main():
                     z = cpu_baseline_zkevm(16, args.queries)
                     g = ((sharded or {}).get("fork9_zkevm_shaped") or {})
                     if g.get("value"):
-                        rows = 1 << (args.log_n - 1 if args.log_n > 22 else args.log_n)
+                        rows = 1 << g.get("log_n", args.log_n)
                         z["gpu_same_instance"] = {"s_per_proof": g["value"], "rows": rows,
                                                   "source": "sharded_one_proof.fork9_zkevm_shaped (1 GPU)"}
                         z["per_row_ratio"] = round((z["value"] / z["rows"]) / (g["value"] / rows), 1)
                         z["per_row_ratio_note"] = ("CPU seconds per trace row at 2^16 / GPU seconds per row at 2^%d: a "
                                                    "throughput ratio of the same proof, not an extrapolated full-size "
                                                    "time (the CPU's per-row cost still falls with size: FRI and queries "
-                                                   "are a fixed cost)" % (args.log_n - 1 if args.log_n > 22 else args.log_n))
+                                                   "are a fixed cost)" % g.get("log_n", args.log_n))
                     cpu["zkevm_shaped"] = z
             elif args.workload == "lde":
                 cpu = cpu_baseline_lde(args.log_n, args.blowup_bits, args.cpu_sample_cols)
             elif args.workload == "merkle":
                 cpu = cpu_baseline_merkle(args.log_n, C)
         if args.workload == "stark":
-            workload = ("full STARK proof (genProof stages 1-5 + FRI + queries, starks.cpp:9-404), synthetic config-4 "
-                        "instance: 2^%d trace, blowup 2^%d, cm1/cm2/cm3/cm4 = %d/%d/%d/%d, %d constants, 2 plookups "
-                        "(dim 3 + dim 1), post-Z step3, FRI steps %s, %d queries; trace resident in HBM; one "
-                        "independent proof per GPU"
-                        % (args.log_n, args.blowup_bits, inst.n_cm1, inst.n_cm2, inst.n_cm3, inst.n_cm4, inst.n_const,
-                           inst.fri_steps, args.queries))
+            kind = _kind(args)
+            workload = ("full STARK proof (genProof stages 1-5 + FRI + queries, starks.cpp:9-404), %s: 2^%d trace, "
+                        "blowup 2^%d, cm1/cm2/cm3/cm4 = %d/%d/%d/%d, %d constants, %d tmpExp, 2 plookups, post-Z step3, "
+                        "FRI steps %s, %d queries, %d evaluations; trace resident in HBM; one independent proof per GPU"
+                        "; HBM plan: %s"
+                        % ("the zkEVM-shaped instance (fork-9 widths + the five zkEVM-shaped expression programs, "
+                           "zkgpu/zkevm_shaped.py)" if kind == "zkevm" else "the fork-9-width synthetic instance"
+                           if kind else "synthetic config-4 instance", args.log_n, args.blowup_bits, inst.n_cm1,
+                           inst.n_cm2, inst.n_cm3, inst.n_cm4, inst.n_const, inst.n_tmp, inst.fri_steps, args.queries,
+                           len(inst.evmap),
+                           "lean (sections share one arena by lifetime, cm1 / cm3 extended in place; the proof consumes "
+                           "its trace, so each timed proof gets a fresh one from the executor stand-in outside its "
+                           "own barrier + synchronize bracket)" if prepare else "resident"))
             one = (sharded or {}).get("config4") or {}
             parallelism = ("replicas x%d (one independent proof per GPU)" % world if world == 1 or scaling == "weak"
                            else "ONE proof row-sharded x%d (sharded_one_proof.config4: C++ prover, %s exchange of "

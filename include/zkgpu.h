@@ -70,12 +70,24 @@ int zkgpu_gl_extend_pol(uint64_t *out, const uint64_t *in, uint64_t n_ext, uint6
 /* device bytes extend_pol keeps in its grow-only workspaces for ncols
  * columns (column batches; for the host's memory plan, no GPU needed) */
 uint64_t zkgpu_lde_workspace_bytes(uint64_t n, uint64_t n_ext, uint64_t ncols);
+/* at most max_cols columns per extend_pol batch (0: the default, 2^31 words
+ * of n_ext-row scratch): a smaller batch bounds the LDE workspace (and, in the
+ * tests, exercises the column batching at small sizes).  Process-wide. */
+void zkgpu_set_lde_batch_cols(uint64_t max_cols);
 
 /* device-resident, column-major variants */
 int zkgpu_gl_ntt_dev(uint64_t *dst, uint64_t ld_dst, const uint64_t *src, uint64_t ld_src, uint64_t n,
                      uint64_t ncols, int inverse);
 int zkgpu_gl_extend_pol_dev(uint64_t *out, uint64_t ld_out, const uint64_t *in, uint64_t ld_in, uint64_t n_ext,
                             uint64_t n, uint64_t ncols);
+/* extendPol in place (the same transform, starks.cpp:53,215): base holds
+ * ncols n-row columns packed at ld n on entry and the ncols n_ext-row columns
+ * at ld n_ext on return (base must hold ncols * n_ext words).  Column batches
+ * run from the last down, each read whole into the LDE workspace before its
+ * output is stored, so no column is overwritten before it is read; lets a
+ * prover extend a section into the memory its n-domain values occupied
+ * (host/starks.cpp, the lean memory plan). */
+int zkgpu_gl_extend_pol_inplace_dev(uint64_t *base, uint64_t n_ext, uint64_t n, uint64_t ncols);
 /* row-major <-> column-major on device (boundary layout change) */
 int zkgpu_rows_to_cols_dev(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint64_t nrows, uint64_t ncols);
 int zkgpu_cols_to_rows_dev(uint64_t *rows, const uint64_t *cols, uint64_t ld, uint64_t nrows, uint64_t ncols);

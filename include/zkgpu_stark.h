@@ -61,8 +61,29 @@ typedef struct {
 } zkgpu_stark_info;
 
 /* allocate the HBM memory map, build the constant polynomials, their LDE and
- * the constant tree (the reference loads these from files; setup, untimed) */
+ * the constant tree (the reference loads these from files; setup, untimed).
+ * Memory plan ZKGPU_MEM_AUTO (below). */
 int zkgpu_stark_create(void **handle, const zkgpu_stark_info *info);
+
+/* HBM plans of the single-GPU prover (the reference allocates one memory map
+ * for the prover's life and reuses sections as scratch, prover.cpp:94,
+ * starks.cpp:53,105):
+ *   RESIDENT  every section of both domains held for the prover's life: the
+ *             trace survives a proof (prove may run again on it).
+ *   LEAN      one arena whose regions follow the sections' lifetimes within a
+ *             proof: cm1's stage-1 extension is hashed and dropped, the
+ *             n-domain sections die after stage 3, cm3 and (before stage 4)
+ *             cm1 are extended in place over their n-domain values, evmap
+ *             reads the extended rows k << blowup (starks.cpp:308-333).  The
+ *             proof consumes cm1_n: set_cm1 / witness before every prove
+ *             (prove fails loudly otherwise); set_cm1_async is not offered.
+ *             At the fork-9 widths and 2^23 rows: about 260 GB instead of 386.
+ *   AUTO      RESIDENT when its plan fits the device's free HBM, else LEAN.
+ * Proofs are bit-identical under every plan. */
+enum { ZKGPU_MEM_AUTO = 0, ZKGPU_MEM_RESIDENT = 1, ZKGPU_MEM_LEAN = 2 };
+int zkgpu_stark_create_ex(void **handle, const zkgpu_stark_info *info, uint32_t memory_plan);
+/* the plan a single-GPU prover runs under (ZKGPU_MEM_RESIDENT / _LEAN) */
+int zkgpu_stark_memory_mode(void *handle);
 /* synthetic committed trace cm1_n (executor stand-in: PRNG columns + step1) */
 int zkgpu_stark_witness(void *handle);
 /* load cm1_n from a host row-major buffer (n rows x n_cm1), the reference's
@@ -133,12 +154,24 @@ typedef struct {
     uint32_t rank, world; /* world a power of two */
     void *ctx;
     int (*exchange)(void *ctx, const zkgpu_comm_op *ops, uint32_t n_ops);
+    /* optional (may be NULL): this rank has failed -- release the peers.  The
+     * prover calls it when a sharded proof fails on this rank (a local error,
+     * or an exchange it refuses), so that no peer waits for it: every later
+     * exchange of the communicator then fails, on this rank at once and on the
+     * peers at their next exchange (host shared memory) or within the
+     * exchange deadline (RCCL). */
+    int (*abort)(void *ctx);
 } zkgpu_comm;
 
 /* The RCCL implementation (ncclSend / ncclRecv inside ncclGroupStart/End,
  * enqueued on the zkgpu stream; xGMI between the GPUs of a node).  One rank
  * makes the id and hands it to the others (any side channel); every rank then
- * creates its communicator with its own rank.  librccl is opened at run time. */
+ * creates its communicator with its own rank.  librccl is opened at run time.
+ * Each exchange waits for its transfers with a deadline (ZKGPU_COMM_TIMEOUT_S
+ * seconds, default 120) while polling ncclCommGetAsyncError; on an error or
+ * the deadline it calls ncclCommAbort (the transfer kernels exit) and fails,
+ * and so does every later exchange: a rank whose peer failed or stopped
+ * returns an error within the deadline instead of waiting forever. */
 int zkgpu_comm_rccl_unique_id(uint8_t id[128]);
 int zkgpu_comm_rccl_create(zkgpu_comm *comm, const uint8_t id[128], uint32_t world, uint32_t rank);
 void zkgpu_comm_rccl_destroy(zkgpu_comm *comm);
@@ -166,6 +199,9 @@ int zkgpu_stark_create_sharded(void **handle, const zkgpu_stark_info *info, cons
  * ranks.  Host only, no GPU needed; both create calls fail loudly, before
  * allocating, when it exceeds the device's free memory. */
 int zkgpu_stark_memory_plan(const zkgpu_stark_info *info, uint32_t world, uint64_t *bytes_per_gpu);
+/* the same for a single-GPU prover (world 0) under memory plan RESIDENT or
+ * LEAN (ZKGPU_MEM_*; AUTO = RESIDENT here: the choice needs a device) */
+int zkgpu_stark_memory_plan_ex(const zkgpu_stark_info *info, uint32_t memory_plan, uint64_t *bytes);
 
 #ifdef __cplusplus
 }

@@ -8,7 +8,13 @@
 //   2. an error in exchange k + 1 raised by a fast rank while a slow rank is
 //      still reading exchange k's flag (the hook below widens that window):
 //      exchange k must succeed on every rank, k + 1 fail on every rank, and
-//      no rank may hang.
+//      no rank may hang;
+//   3. a failed rank: the last rank aborts the communicator (zkgpu_comm.abort,
+//      what the prover does when its proof fails) instead of exchanging --
+//      every other rank's exchange fails at once; then, on a second
+//      communicator, the last rank stops without exchanging -- every other
+//      rank fails within the exchange deadline (ZKGPU_COMM_TIMEOUT_S = 2 s),
+//      and every exchange after that fails at once.
 // The device copies are host memcpy here (the harness defines the two
 // libzkgpu calls the exchange makes), so the test needs no GPU.
 // Build: g++ -O2 -std=c++17 -pthread -o comm_host_check tests/cpp/comm_host_check.cpp -lrt
@@ -132,6 +138,47 @@ static int run_rank(const char *name, uint32_t W, uint32_t R)
     }
     g_slow_rank = -1;
     host_comm_destroy(&comm);
+    // 3. a failed rank, then a stopped one
+    using clk = std::chrono::steady_clock;
+    auto secs = [](clk::time_point t) { return std::chrono::duration<double>(clk::now() - t).count(); };
+    for (int variant = 0; variant < 2 && !bad; variant++) {
+        char nm[80];
+        snprintf(nm, sizeof nm, "%s_f%d", name, variant);
+        zkgpu_comm c2;
+        if (host_comm_create(&c2, nm, W, R, 1 << 16)) {
+            fprintf(stderr, "rank %u: create %s: %s\n", R, nm, g_err);
+            return 2;
+        }
+        std::vector<uint8_t> x(64, 1), y(64);
+        const uint32_t nx = (R + 1) % W, pv = (R + W - 1) % W;
+        zkgpu_comm_op ops[2] = {{(int32_t)nx, 1, x.data(), 64}, {(int32_t)pv, 0, y.data(), 64}};
+        if (host_exchange(c2.ctx, ops, 2)) {  // a clean exchange first
+            fprintf(stderr, "rank %u variant %d: clean exchange failed: %s\n", R, variant, g_err);
+            bad = 1;
+        }
+        const auto t0 = clk::now();
+        if (R == W - 1) {
+            if (variant == 0) {
+                c2.abort(c2.ctx);
+            } else {
+                std::this_thread::sleep_for(std::chrono::milliseconds(3500));  // stopped: never exchanges
+            }
+        } else {
+            const int rc = host_exchange(c2.ctx, ops, 2);
+            const double el = secs(t0);
+            const double lim = variant == 0 ? 1.5 : 3.0;  // abort: at once; stopped: the 2 s deadline
+            if (!rc || el > lim || (variant == 1 && el < 1.5)) {
+                fprintf(stderr, "rank %u variant %d: exchange rc %d after %.2f s (%s)\n", R, variant, rc, el, g_err);
+                bad = 1;
+            }
+            const auto t1 = clk::now();
+            if (!host_exchange(c2.ctx, ops, 2) || secs(t1) > 0.5) {
+                fprintf(stderr, "rank %u variant %d: the exchange after the failure did not fail at once\n", R, variant);
+                bad = 1;
+            }
+        }
+        host_comm_destroy(&c2);
+    }
     return bad;
 }
 
@@ -141,6 +188,7 @@ int main(int argc, char **argv)
     char name[64];
     snprintf(name, sizeof name, "/zkgpu_cc_%d", (int)getpid());
     setenv("ZKGPU_RUN_ID", name, 1);
+    setenv("ZKGPU_COMM_TIMEOUT_S", "2", 1);
     std::vector<pid_t> kids;
     for (uint32_t r = 0; r < W; r++) {
         const pid_t p = fork();

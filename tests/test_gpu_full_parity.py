@@ -29,22 +29,29 @@ P = 0xFFFFFFFF00000001
 SEC_CONST_2NS, SEC_Q_2NS, SEC_F_2NS = 9, 10, 11
 
 
+@pytest.mark.parametrize("mode", ["auto", "lean"])
 @pytest.mark.parametrize("fixture", ["config4_2p23_proof.json", "zkevm_shaped_2p20_proof.json"])
-def test_full_size_proof_equals_oracle_fixture(zkgpu, fixture):
+def test_full_size_proof_equals_oracle_fixture(zkgpu, fixture, mode):
     """config4_2p23: the headline instance at its benchmarked size;
     zkevm_shaped_2p20: the fork-9 widths with the five zkEVM-shaped programs
     (the sharded_one_proof.fork9_zkevm_shaped workload) at the largest size
-    whose oracle run fits the build container"""
+    whose oracle run fits the build container.  Both under the default plan
+    (resident: they fit) and under the lean one (ZKGPU_MEM_LEAN: sections
+    sharing one arena by lifetime, cm1 / cm3 extended in place, evmap from the
+    extended rows) -- the same proof."""
     import bench
-    from zkgpu.stark import GpuStark
+    import torch
+    from zkgpu.stark import GpuStark, MEM_AUTO, MEM_LEAN
     from golden.make_config4_fixture import summarize
+    torch.cuda.empty_cache()
     fx = json.load(open(os.path.join(ROOT, "tests", "golden", fixture)))
     i = fx["instance"]
     kind = "zkevm" if i.get("kind") == "zkevm" else False
     inst = bench.stark_instance(i["log_n"], i["blowup_bits"], i["ncols"], i["queries"], kind)
     assert [inst.n_cm1, inst.n_cm2, inst.n_cm3, inst.n_cm4] == i["n_cm"] and inst.n_const == i["n_const"]
-    g = GpuStark(inst)
+    g = GpuStark(inst, mode=MEM_LEAN if mode == "lean" else MEM_AUTO)
     try:
+        assert g.memory_mode() == ("lean" if mode == "lean" else "resident")
         g.witness()
         got = summarize(g.prove())
     finally:

@@ -107,11 +107,11 @@ def test_sharded_rejects_bad_world(zkgpu):
         GpuStark(_inst("lookups"), comm=Three())
 
 
-def _worker(rank, world, port, q, name, shm, rows=False):
+def _worker(rank, world, port, q, name, shm, rows=False, env=None):
     import sys
     root_dir = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root_dir, os.path.join(root_dir, "zkevm-prover_amd"), os.path.join(root_dir, "tests")]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **(env or {}))
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -276,3 +276,36 @@ def test_sharded_lookup_value_not_in_table(oracle, world):
                 p.kill()
     for _, proof, _, err in res:
         assert proof is None and err and "Number not included: w=9" in err, err
+
+
+@pytest.mark.parametrize("world,k", [(2, 2), (2, 9), (4, 14), (2, 30)])
+def test_sharded_rank_failure_releases_peers(oracle, world, k):
+    """A rank that fails locally in the middle of a sharded proof (injected
+    before its k-th exchange: setup, the commits, calculateH1H2's five
+    exchanges, the quotient, FRI) aborts the communicator (zkgpu_comm.abort,
+    ShardedStarks::abort_comm): every other rank's next exchange fails at once
+    instead of waiting for it (h1h2_sharded's local errors left the
+    peers in the collective).  No rank may hang: all report within seconds,
+    well inside the 20 s exchange deadline."""
+    import multiprocessing as mp
+    import uuid
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    shm = "/zkgpu_t_%s" % uuid.uuid4().hex[:12]
+    env = {"ZKGPU_TEST_FAIL_EXCHANGE": "%d:%d" % (world - 1, k), "ZKGPU_COMM_TIMEOUT_S": "20"}
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, "lookups", shm, False, env)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=240) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    errs = {r: e for r, proof, _, e in res}
+    assert all(errs[r] for r in range(world)), errs
+    assert "injected failure before exchange %d" % k in errs[world - 1], errs[world - 1]
+    for r in range(world - 1):
+        assert "a rank aborted" in errs[r] or "aborted or timed out" in errs[r], errs[r]

@@ -2,11 +2,13 @@
 Starks::plan; DESIGN.md section 6) at the fork-9 zkEVM widths
 (commit_pols.hpp:1736-1737: 751 / 168 / 408 / 6 committed columns, 234
 constants, 389 tmpExp columns) on the 2^23-row trace of BASELINE configs[4]:
-one MI355X (288 GB) cannot hold it, eight row-sharded ranks can.  Host code
-only; both create calls enforce the same plan against the device's free HBM."""
+one MI355X cannot hold every section of both domains (the resident plan), the
+lean plan (sections sharing one arena by lifetime, ZKGPU_MEM_LEAN) fits it on
+one GPU, eight row-sharded ranks hold it too.  Host code only; both create
+calls enforce the same plan against the device's free HBM."""
 import pytest
 
-HBM = 288e9
+HBM = 309.2e9  # 288 GiB: hipMemGetInfo's total on the MI355X boxes (308.4e9 free after init)
 
 
 @pytest.fixture(scope="module")
@@ -17,7 +19,7 @@ def plan():
     return {w: memory_plan(inst, w) for w in (0, 1, 2, 4, 8)}
 
 
-def test_fork9_needs_eight_gpus(plan):
+def test_fork9_resident_needs_eight_gpus(plan):
     assert plan[8] <= HBM, plan
     assert plan[0] > HBM and plan[1] > HBM, plan
     # the trace itself (n + 2n domains, 1950 + 1561 columns) dominates
@@ -48,3 +50,38 @@ def test_shift_beyond_block_rejected():
     assert memory_plan(inst, 2) > 0
     with pytest.raises(ZkgpuError, match="row shift 11 exceeds"):
         memory_plan(inst, 8)
+
+
+def test_fork9_lean_fits_one_gpu():
+    """the north-star instance (fork-9 widths, zkEVM-shaped programs, 2^23)
+    under the lean plan: <= 280 GB on one GPU, about a
+    third less than the resident plan; at 2^22 as well"""
+    import bench
+    from zkgpu.stark import memory_plan, MEM_LEAN, MEM_RESIDENT
+    for bits in (22, 23):
+        inst = bench.stark_instance(bits, 1, 100, 128, "zkevm")
+        lean, res = memory_plan(inst, 0, MEM_LEAN), memory_plan(inst, 0, MEM_RESIDENT)
+        assert res == memory_plan(inst, 0)
+        assert lean < 0.72 * res, (bits, lean, res)
+        if bits == 23:
+            assert lean <= 280e9 < res, (lean, res)
+            # the 2n-domain committed sections (751 + 168 + 408 + 6 + 234
+            # columns) + the trees bound it from below
+            assert lean > (1567 * 2**24) * 8
+
+
+def test_lean_plan_refused_when_it_cannot_apply():
+    """a quotient program that reads an n-domain section: no lean plan"""
+    import copy
+    import bench
+    from zkgpu import ZkgpuError
+    from zkgpu import synthetic as sy
+    from zkgpu.stark import memory_plan, MEM_LEAN
+    inst = copy.deepcopy(bench.stark_instance(10, 1, 100, 16))
+    p = inst.programs["step42ns"]
+    a = p.o(sy.COL, sy.SEC_CM2_N, 0, 0)
+    p.op(sy.ADD, p.o(sy.TMP1, 0, 0, 0), a, a)
+    with pytest.raises(ZkgpuError, match="step42ns reads an n-domain section"):
+        memory_plan(inst, 0, MEM_LEAN)
+    with pytest.raises(ValueError):
+        memory_plan(inst, 2, MEM_LEAN)

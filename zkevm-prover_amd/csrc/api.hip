@@ -147,9 +147,11 @@ static uint32_t log2u(uint64_t n)
 // scratch.  (Batches of 32 columns
 // at 2^24 rows measured 2-3 % slower than one batch of 100: 51.9 vs 53.5
 // Gelem/s, the same box.)
+static uint64_t g_lde_batch_max = 0;  // zkgpu_set_lde_batch_cols (0: the default)
 static uint64_t lde_batch_cols(uint64_t n_ext, uint64_t ncols)
 {
-    const uint64_t batch = std::max<uint64_t>(1, (1ULL << 31) / (n_ext ? n_ext : 1));
+    uint64_t batch = std::max<uint64_t>(1, (1ULL << 31) / (n_ext ? n_ext : 1));
+    if (g_lde_batch_max && g_lde_batch_max < batch) batch = g_lde_batch_max;
     return batch < ncols ? batch : ncols;
 }
 
@@ -346,12 +348,34 @@ uint64_t zkgpu_lde_workspace_bytes(uint64_t n, uint64_t n_ext, uint64_t ncols)
     return lde_workspace_bytes(n, n_ext, ncols);
 }
 
+void zkgpu_set_lde_batch_cols(uint64_t max_cols) { g_lde_batch_max = max_cols; }
+
 int zkgpu_gl_extend_pol_dev(uint64_t *out, uint64_t ld_out, const uint64_t *in, uint64_t ld_in, uint64_t n_ext,
                             uint64_t n, uint64_t ncols)
 {
     int rc;
     if ((rc = require_init())) return rc;
     return extend_pol_dev(out, ld_out, in, ld_in, n_ext, n, ncols);
+}
+
+int zkgpu_gl_extend_pol_inplace_dev(uint64_t *base, uint64_t n_ext, uint64_t n, uint64_t ncols)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!ncols || !n) return 0;
+    if (!is_pow2(n) || !is_pow2(n_ext) || n_ext < n)
+        return set_error(ZKGPU_ERR_ARG, "extend_pol_inplace: sizes must be powers of two with n_ext >= n");
+    // batch [c0, c1) reads [c0 n, c1 n) and writes [c0 n_ext, c1 n_ext):
+    // the columns below c0, still unread, end at c0 n <= c0 n_ext; within a
+    // batch extend_pol_dev stages the whole input (coefficients in workspace
+    // 0) before the first output store, on one stream
+    const uint64_t batch = lde_batch_cols(n_ext, ncols);
+    for (uint64_t c1 = ncols; c1 > 0;) {
+        const uint64_t c0 = c1 > batch ? c1 - batch : 0;
+        if ((rc = extend_pol_dev(base + c0 * n_ext, n_ext, base + c0 * n, n, n_ext, n, c1 - c0))) return rc;
+        c1 = c0;
+    }
+    return 0;
 }
 
 int zkgpu_rows_to_cols_dev(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint64_t nrows, uint64_t ncols)

@@ -8,21 +8,54 @@
 // receive from a peer takes that peer's k-th send to this rank), and waits
 // again so outboxes can be reused.  Capacity (bytes per rank and exchange) is
 // fixed at creation; a larger exchange fails loudly.
+//
+// No wait is unbounded: the barrier is a counter in the segment polled with a
+// deadline (comm_wait, ZKGPU_COMM_TIMEOUT_S); a rank that gives up there, or
+// aborts (zkgpu_comm.abort: its proof failed), marks the segment broken and
+// every rank's next wait fails -- a failed or stopped rank cannot leave its
+// peers waiting forever.
 #include <fcntl.h>
-#include <pthread.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <string>
 #include <thread>
 
 namespace zkgpu_host {
 
+// seconds a rank waits for its peers in one exchange (ZKGPU_COMM_TIMEOUT_S,
+// default 120: the largest exchange, a fork-9 stage-1 commit at W = 8, moves
+// ~16 GB per rank in ~0.1 s over xGMI; the rest is the ranks' skew)
+static double comm_timeout_s()
+{
+    const char *e = getenv("ZKGPU_COMM_TIMEOUT_S");
+    const double t = e ? atof(e) : 0.0;
+    return t > 0 ? t : 120.0;
+}
+
+// Poll done() until it returns 1 (0: not yet, < 0: failed), with err()
+// checked on the way; returns 0, -1 (failed) or -2 (deadline).  Short sleeps
+// after the first polls keep a waiting rank off its CPU core.
+template <class Done, class Err>
+static int comm_wait(Done done, Err err, double timeout_s)
+{
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    for (uint64_t spin = 0;; spin++) {
+        const int d = done();
+        if (d > 0) return 0;
+        if (d < 0 || err()) return -1;
+        if (std::chrono::duration<double>(clk::now() - t0).count() > timeout_s) return -2;
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(spin > 4096 ? 200 : 20));
+    }
+}
+
 struct HostCommHeader {
-    std::atomic<uint32_t> ready;
+    std::atomic<uint32_t> ready;    // 1: set up; 2: creation failed (a late rank fails too)
     std::atomic<uint32_t> arrived;  // ranks that have mapped the segment (creation)
     uint32_t world;
     uint64_t capacity;
@@ -31,7 +64,10 @@ struct HostCommHeader {
     // (cleared two exchanges ahead, see host_exchange): a rank still reading
     // exchange k's flag never sees a failure a faster rank raised in k + 1
     std::atomic<uint32_t> error[3];
-    pthread_barrier_t barrier;
+    // the barrier: arrivals of the current generation, the generation
+    std::atomic<uint32_t> bar_count, bar_gen;
+    // a rank aborted or a barrier timed out: every later wait fails
+    std::atomic<uint32_t> broken;
 };
 
 // 64-bit tag of this run: ZKGPU_RUN_ID if set, else the launcher's pid
@@ -67,12 +103,33 @@ struct HostCommCtx {
     uint64_t &n_entries(uint32_t r) const { return *(uint64_t *)box(r); }
     HostCommEntry *entries(uint32_t r) const { return (HostCommEntry *)(box(r) + 8); }
     uint8_t *data(uint32_t r) const { return box(r) + 8 + HOST_COMM_MAX_OPS * sizeof(HostCommEntry); }
+    // every rank of the world: the last arrival resets the count and
+    // advances the generation the others poll (with the deadline)
     int wait() const
     {
-        const int rc = pthread_barrier_wait(&hdr()->barrier);
-        return (rc == 0 || rc == PTHREAD_BARRIER_SERIAL_THREAD) ? 0 : fail("host comm: barrier failed");
+        HostCommHeader *h = hdr();
+        if (h->broken.load()) return fail("host comm: a rank aborted or timed out in an earlier exchange");
+        const uint32_t g = h->bar_gen.load(std::memory_order_acquire);
+        if (h->bar_count.fetch_add(1, std::memory_order_acq_rel) + 1 == world) {
+            h->bar_count.store(0, std::memory_order_relaxed);
+            h->bar_gen.fetch_add(1, std::memory_order_release);
+            return 0;
+        }
+        const double limit = comm_timeout_s();
+        const int w = comm_wait([&]() { return h->bar_gen.load(std::memory_order_acquire) != g ? 1 : 0; },
+                                [&]() { return h->broken.load() != 0; }, limit);
+        if (!w) return 0;
+        h->broken.store(1);
+        if (w == -2) return fail("host comm: not every rank reached the exchange within %.0f s (a peer failed or stopped)", limit);
+        return fail("host comm: a rank aborted (its proof failed)");
     }
 };
+
+static int host_abort(void *vctx)
+{
+    ((HostCommCtx *)vctx)->hdr()->broken.store(1);
+    return 0;
+}
 
 // Every rank reaches both barriers whatever happens: a rank that fails
 // raises this exchange's error flag and still waits, so one rank's error is
@@ -177,11 +234,9 @@ static int host_comm_create(zkgpu_comm *comm, const char *name, uint32_t world, 
         }
         c->base = (uint8_t *)m;
         HostCommHeader *h = c->hdr();
-        pthread_barrierattr_t a;
-        pthread_barrierattr_init(&a);
-        pthread_barrierattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
-        pthread_barrier_init(&h->barrier, &a, world);
-        pthread_barrierattr_destroy(&a);
+        h->bar_count.store(0);
+        h->bar_gen.store(0);
+        h->broken.store(0);
         h->world = world;
         h->capacity = capacity;
         h->run = run;
@@ -224,9 +279,13 @@ static int host_comm_create(zkgpu_comm *comm, const char *name, uint32_t world, 
         HostCommHeader *h = c->hdr();
         h->arrived.fetch_add(1);
         bool all = false;
-        for (int t = 0; t < 12000 && !(all = h->arrived.load() >= world); t++)
+        for (int t = 0; t < 12000 && h->ready.load() == 1 && !(all = h->arrived.load() >= world); t++)
             std::this_thread::sleep_for(std::chrono::milliseconds(5));
-        if (!all) {
+        // a rank that gave up marks the segment failed (ready = 2) before it
+        // leaves: a late arrival then fails here too, instead of entering the
+        // first exchange without the others
+        if (!all || h->ready.load() != 1) {
+            h->ready.store(2);
             const uint32_t n = h->arrived.load();
             if (rank == 0) shm_unlink(name);
             munmap(m, c->size);
@@ -239,6 +298,7 @@ static int host_comm_create(zkgpu_comm *comm, const char *name, uint32_t world, 
     comm->world = world;
     comm->ctx = c;
     comm->exchange = host_exchange;
+    comm->abort = host_abort;
     return 0;
 }
 
@@ -250,6 +310,7 @@ static void host_comm_destroy(zkgpu_comm *comm)
     delete c;
     comm->ctx = nullptr;
     comm->exchange = nullptr;
+    comm->abort = nullptr;
 }
 
 }  // namespace zkgpu_host

@@ -5,8 +5,19 @@
 // ncclGroupStart / ncclGroupEnd, enqueued on the zkgpu stream: RCCL matches
 // the sends and receives of a peer pair in order, and later zkgpu work on the
 // stream is ordered after the transfers.
+//
+// Failure: a peer that failed (or never reaches this exchange) leaves this
+// rank's receive kernels spinning.  So each exchange waits for its transfers
+// with a deadline (comm_wait, ZKGPU_COMM_TIMEOUT_S), polling the
+// communicator's asynchronous error; on an error or the deadline it aborts
+// the communicator (ncclCommAbort: the transfer kernels see the abort flag and
+// exit) and fails, and every later exchange fails at once.  A rank whose proof
+// fails locally aborts through zkgpu_comm.abort (ShardedStarks::prove).
 #include <dlfcn.h>
 #include <rccl/rccl.h>
+
+#include <chrono>
+#include <thread>
 
 namespace zkgpu_host {
 
@@ -15,6 +26,8 @@ struct RcclApi {
     decltype(&ncclGetUniqueId) get_unique_id = nullptr;
     decltype(&ncclCommInitRank) comm_init_rank = nullptr;
     decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclCommAbort) comm_abort = nullptr;
+    decltype(&ncclCommGetAsyncError) get_async_error = nullptr;
     decltype(&ncclSend) send = nullptr;
     decltype(&ncclRecv) recv = nullptr;
     decltype(&ncclGroupStart) group_start = nullptr;
@@ -33,6 +46,8 @@ struct RcclApi {
         ZK_SYM(get_unique_id, "ncclGetUniqueId");
         ZK_SYM(comm_init_rank, "ncclCommInitRank");
         ZK_SYM(comm_destroy, "ncclCommDestroy");
+        ZK_SYM(comm_abort, "ncclCommAbort");
+        ZK_SYM(get_async_error, "ncclCommGetAsyncError");
         ZK_SYM(send, "ncclSend");
         ZK_SYM(recv, "ncclRecv");
         ZK_SYM(group_start, "ncclGroupStart");
@@ -46,13 +61,34 @@ struct RcclApi {
 
 static RcclApi g_rccl;
 
+// (comm_timeout_s / comm_wait: comm_host.hpp, included first)
+
 struct RcclCtx {
     ncclComm_t comm = nullptr;
+    bool failed = false;   // an exchange failed or this rank aborted: every later one fails
+    bool aborted = false;  // ncclCommAbort ran (the communicator is gone)
+    hipEvent_t done = nullptr;
 };
 
-static int rccl_exchange(void *ctx, const zkgpu_comm_op *ops, uint32_t n_ops)
+static int rccl_abort(void *vctx)
 {
-    ncclComm_t c = ((RcclCtx *)ctx)->comm;
+    RcclCtx *c = (RcclCtx *)vctx;
+    c->failed = true;
+    if (c->comm && !c->aborted) {
+        (void)g_rccl.comm_abort(c->comm);
+        c->aborted = true;
+        c->comm = nullptr;
+    }
+    return 0;
+}
+
+static int rccl_exchange(void *vctx, const zkgpu_comm_op *ops, uint32_t n_ops)
+{
+    RcclCtx *ctx = (RcclCtx *)vctx;
+    if (ctx->failed)
+        return fail("rccl exchange: the communicator failed earlier (a timed-out or failed exchange, or this rank "
+                    "aborted)");
+    ncclComm_t c = ctx->comm;
     hipStream_t s = (hipStream_t)zkgpu_get_stream();
     ncclResult_t r = g_rccl.group_start();
     if (r != ncclSuccess) return fail("ncclGroupStart: %s", g_rccl.error_string(r));
@@ -64,8 +100,38 @@ static int rccl_exchange(void *ctx, const zkgpu_comm_op *ops, uint32_t n_ops)
         if (r != ncclSuccess && first == ncclSuccess) first = r;
     }
     r = g_rccl.group_end();
-    if (first != ncclSuccess) return fail("ncclSend/ncclRecv: %s", g_rccl.error_string(first));
-    if (r != ncclSuccess) return fail("ncclGroupEnd: %s", g_rccl.error_string(r));
+    if (first != ncclSuccess || r != ncclSuccess) {
+        rccl_abort(ctx);
+        return fail("ncclSend/ncclRecv/ncclGroupEnd: %s", g_rccl.error_string(first != ncclSuccess ? first : r));
+    }
+    if (!n_ops) return 0;
+    if (!ctx->done && hipEventCreateWithFlags(&ctx->done, hipEventDisableTiming) != hipSuccess) {
+        rccl_abort(ctx);
+        return fail("rccl exchange: hipEventCreate failed");
+    }
+    if (hipEventRecord(ctx->done, s) != hipSuccess) {
+        rccl_abort(ctx);
+        return fail("rccl exchange: hipEventRecord failed");
+    }
+    ncclResult_t ae = ncclSuccess;
+    const double limit = comm_timeout_s();
+    const int w = comm_wait(
+        [&]() {
+            const hipError_t q = hipEventQuery(ctx->done);
+            return q == hipSuccess ? 1 : q == hipErrorNotReady ? 0 : -1;
+        },
+        [&]() {
+            return g_rccl.get_async_error(c, &ae) != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress);
+        },
+        limit);
+    if (w) {
+        rccl_abort(ctx);
+        if (w == -2)
+            return fail("rccl exchange of %u operations: not complete after %.0f s (a peer failed or stopped; "
+                        "communicator aborted)", n_ops, limit);
+        return fail("rccl exchange of %u operations failed: %s (communicator aborted)", n_ops,
+                    ae != ncclSuccess ? g_rccl.error_string(ae) : "stream error");
+    }
     return 0;
 }
 

@@ -139,10 +139,11 @@ public:
     int create_sharded(const zkgpu_stark_info *in, const zkgpu_comm *c)
     {
         comm = *c;
-        if (shape(in, c->world, c->rank, true)) return -1;
+        if (shape(in, c->world, c->rank, true)) return abort_comm(-1);
         if (c->world > 1 && !c->exchange) return fail("stark_create_sharded: the communicator has no exchange");
-        if (check_budget() || alloc()) return -1;
-        return build_const();
+        read_fail_hook();
+        if (check_budget() || alloc()) return abort_comm(-1);
+        return abort_comm(build_const());
     }
 
     // n-domain shifts of a program (reads and stores; sets hn) and its stores
@@ -281,6 +282,11 @@ public:
     // multiset segment is all its own rows, calculateH1H2): the host exchange
     // is a barrier per call, so a rank that skipped an empty exchange would
     // pair its next one with the others' current one.
+    //
+    // A rank that cannot take part (it refuses the exchange, or fails before
+    // it) returns an error; prove() / create_sharded() then abort the
+    // communicator (zkgpu_comm.abort), which fails the peers' exchanges
+    // instead of leaving them waiting for this rank.
     int exchange()
     {
         if (W == 1) {
@@ -289,14 +295,19 @@ public:
         }
         max_ops = std::max(max_ops, (uint32_t)ops.size());
         if (ops.size() > 2ULL * (W - 1)) {
-            // still enter the collective exchange, with nothing posted: the
-            // peers' receives from this rank then fail (host exchange: "sent
-            // fewer slices") instead of waiting at its barrier forever
             const size_t n = ops.size();
             ops.clear();
-            (void)comm.exchange(comm.ctx, ops.data(), 0);
             return fail("exchange of %zu operations: more than one send and one receive per peer", n);
         }
+        if (fail_at && n_exch_total + 1 == fail_at) {  // test hook (ZKGPU_TEST_FAIL_EXCHANGE)
+            ops.clear();
+            return fail("injected failure before exchange %llu on rank %u", (unsigned long long)fail_at, R);
+        }
+        n_exch_total++;
+        // the exchange's device interval (stream marks around it; resolved
+        // with the stage timers): bytes / time = the achieved link rate
+        uint32_t m0 = UINT32_MAX;
+        if (n_marks + 3 < ZKGPU_MARKS && !zkgpu_mark(n_marks)) m0 = n_marks++;
         if (comm.exchange(comm.ctx, ops.data(), (uint32_t)ops.size())) {
             const std::string why = last_error_text();
             return fail("zkgpu_comm exchange of %zu operations failed (rank %u of %u): %s", ops.size(), R, W,
@@ -305,11 +316,32 @@ public:
         uint64_t sent = 0;
         for (const zkgpu_comm_op &o : ops)
             if (o.send) sent += o.bytes;
+        if (m0 != UINT32_MAX && !zkgpu_mark(n_marks)) pend_x.push_back({{m0, n_marks++}, sent});
         n_exch++;
         sent_bytes += sent;
         max_sent = std::max(max_sent, sent);
         ops.clear();
         return 0;
+    }
+    // the injected failure of the tests: rank r fails before its k-th
+    // exchange (ZKGPU_TEST_FAIL_EXCHANGE = "r:k"), k counted from creation
+    uint64_t fail_at = 0, n_exch_total = 0;
+    void read_fail_hook()
+    {
+        const char *e = getenv("ZKGPU_TEST_FAIL_EXCHANGE");
+        unsigned r = 0;
+        unsigned long long k = 0;
+        if (e && sscanf(e, "%u:%llu", &r, &k) == 2 && r == R) fail_at = k;
+    }
+    // a failed sharded call on this rank: release the peers
+    int abort_comm(int rc)
+    {
+        if (rc && W > 1 && comm.abort) {
+            const std::string why = last_error_text();
+            (void)comm.abort(comm.ctx);
+            fail("%s (rank %u aborted the communicator)", why.c_str(), R);
+        }
+        return rc;
     }
     void op(uint32_t peer, int send, const void *buf, uint64_t bytes)
     {
@@ -1052,7 +1084,7 @@ public:
 
     int prove(uint64_t *out) override
     {
-        const int rc = prove_sharded(out);
+        const int rc = abort_comm(prove_sharded(out));
         const int rc2 = take_cm1_async(true);  // a queued trace becomes cm1_n (set_cm1_async)
         return rc ? rc : rc2;
     }
@@ -1061,6 +1093,7 @@ public:
     {
         timers.clear();
         pend_t.clear();
+        pend_x.clear();
         n_marks = 0;
         n_exch = sent_bytes = max_sent = 0;
         auto tall = clk::now();
@@ -1157,6 +1190,8 @@ public:
         // and the communicator's world and this proof's exchange volume
         if (W > 1) {
             timers.emplace_back("COUNT_COMM_MAX_OPS", (double)max_ops);
+            timers.emplace_back("COUNT_COMM_EXCHANGE_MS", xchg_ms);  // device time inside the exchanges
+            timers.emplace_back("COUNT_COMM_LARGEST_EXCHANGE_MS", xchg_max_ms);  // of the largest one (bytes sent)
             timers.emplace_back("COUNT_COMM_WORLD", (double)comm.world);
             timers.emplace_back("COUNT_COMM_EXCHANGES", (double)n_exch);
             timers.emplace_back("COUNT_COMM_BYTES_SENT", (double)sent_bytes);

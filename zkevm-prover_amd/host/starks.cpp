@@ -175,6 +175,15 @@ public:
     // memory plan: with `dry` set, dalloc only adds up the bytes (no device)
     bool dry = false;
     uint64_t planned = 0;
+    // ZKGPU_MEM_RESIDENT or ZKGPU_MEM_LEAN (include/zkgpu_stark.h)
+    int mem_mode = ZKGPU_MEM_RESIDENT;
+    bool lean() const { return mem_mode == ZKGPU_MEM_LEAN; }
+    // lean plan: the arena (cm1_n at its start; cm1_2ns over it from stage 4),
+    // cm1's stage-1 extension above cm1_n, and the n-domain columns no stage
+    // writes (zeroed before their stage: the arena's regions are reused)
+    uint64_t *arena = nullptr, *cm1_early = nullptr;
+    std::vector<uint32_t> unwritten[5];
+    bool cm1_consumed = false;
 
     // background hand-off of the next proof's cm1_n (set_cm1_async)
     // (up to two row pieces: a shard's rows wrap around the domain end)
@@ -246,10 +255,98 @@ public:
         return 0;
     }
 
-    int create(const zkgpu_stark_info *in)
+    int create(const zkgpu_stark_info *in, uint32_t mode = ZKGPU_MEM_AUTO)
     {
-        if (load(in) || check_budget() || alloc()) return -1;
+        if (load(in) || choose_mode(mode) || check_budget() || alloc()) return -1;
         return build_const();
+    }
+
+    // AUTO: RESIDENT when its plan fits the free HBM, else LEAN (if the
+    // programs allow it; else RESIDENT, which check_budget then refuses)
+    int choose_mode(uint32_t mode)
+    {
+        if (mode > ZKGPU_MEM_LEAN) return fail("stark_create: unknown memory plan %u", mode);
+        if (mode == ZKGPU_MEM_LEAN) {
+            std::string why;
+            if (!lean_ok(why)) return fail("stark_create: the lean memory plan does not apply: %s", why.c_str());
+            return set_mode(ZKGPU_MEM_LEAN);
+        }
+        mem_mode = ZKGPU_MEM_RESIDENT;
+        if (mode == ZKGPU_MEM_RESIDENT) return 0;
+        uint64_t need = 0, avail = 0, total = 0;
+        if (plan(&need)) return -1;
+        CK(zkgpu_device_memory(&avail, &total));
+        std::string why;
+        if (need > avail && lean_ok(why)) return set_mode(ZKGPU_MEM_LEAN);
+        return 0;
+    }
+    int set_mode(int m)
+    {
+        mem_mode = m;
+        if (m == ZKGPU_MEM_LEAN) find_unwritten();
+        return 0;
+    }
+
+    // The lean plan needs: stage 4/5 programs that read no n-domain section
+    // but the constants (their n-domain regions are gone by then), a witness
+    // program that writes cm1_n only (the other n-domain regions hold cm1's
+    // stage-1 extension then), and a blowup (the in-place extensions)
+    bool lean_ok(std::string &why) const
+    {
+        if (NE < 2 * N) {
+            why = "no blowup";
+            return false;
+        }
+        const Prog *ext[2] = {&step42ns, &step52ns};
+        const char *names[2] = {"step42ns", "step52ns"};
+        for (int k = 0; k < 2; k++)
+            for (const zxp_operand &o : ext[k]->opnd)
+                if ((o.kind == ZXP_COL || o.kind == ZXP_COL3) && o.a < SEC_CONST_N) {
+                    why = std::string(names[k]) + " reads an n-domain section";
+                    return false;
+                }
+        for (const zxp_instr &i : step1.instr) {
+            if (i.dst >= step1.opnd.size()) continue;
+            const zxp_operand &o = step1.opnd[i.dst];
+            if ((o.kind == ZXP_COL || o.kind == ZXP_COL3) && o.a != SEC_CM1_N) {
+                why = "the witness program writes outside cm1_n";
+                return false;
+            }
+        }
+        return true;
+    }
+
+    // n-domain columns of tmpExp / cm2 / cm3 that no stage writes: step2,
+    // calculateH1H2's h1 / h2, step3prev, calculateZ's z, step3
+    void find_unwritten()
+    {
+        const uint32_t widths[5] = {info.n_cm1, info.n_cm2, info.n_cm3, info.n_tmp, info.n_const};
+        std::vector<char> w[5];
+        for (int s = 0; s < 5; s++) w[s].assign(widths[s], 0);
+        for (const Prog *p : {&step2, &step3prev, &step3})
+            for (const zxp_instr &i : p->instr) {
+                if (i.dst >= p->opnd.size()) continue;
+                const zxp_operand &o = p->opnd[i.dst];
+                if ((o.kind != ZXP_COL && o.kind != ZXP_COL3) || o.a > SEC_CONST_N) continue;
+                for (uint32_t c = o.b; c < o.b + (o.kind == ZXP_COL3 ? 3u : 1u) && c < widths[o.a]; c++) w[o.a][c] = 1;
+            }
+        for (uint32_t k = 0; k < info.n_pu; k++)
+            for (uint32_t c = 0; c < pu[5 * k + 4]; c++) {
+                w[SEC_CM2_N][pu[5 * k + 2] + c] = 1;
+                w[SEC_CM2_N][pu[5 * k + 3] + c] = 1;
+            }
+        for (uint32_t z = 0; z < info.n_zctx; z++)
+            for (uint32_t c = 0; c < 3; c++) w[SEC_CM3_N][zctx[3 * z + 2] + c] = 1;
+        for (int s : {(int)SEC_CM2_N, (int)SEC_CM3_N, (int)SEC_TMP_N}) {
+            unwritten[s].clear();
+            for (uint32_t c = 0; c < widths[s]; c++)
+                if (!w[s][c]) unwritten[s].push_back(c);
+        }
+    }
+    int zero_unwritten(uint32_t s)
+    {
+        for (uint32_t c : unwritten[s]) CK(zkgpu_memset_dev(S.sec[s] + (uint64_t)c * N, 0, N * 8));
+        return 0;
     }
 
     // validate the description, keep the programs, bind the device (init =
@@ -329,8 +426,9 @@ public:
     // stage-4/5 and FRI buffers of the whole extended domain
     int alloc_fri()
     {
+        // (lean: evmap reads the quotient pieces' extended rows, no cm4_n)
         if (dalloc(&qq1, 3 * NE) || dalloc(&qq2, (uint64_t)info.n_cm4 * NE) ||
-            dalloc(&cm4_n, (uint64_t)(info.n_cm4 ? info.n_cm4 : 1) * N) || dalloc(&lev, 3 * N) ||
+            dalloc(&cm4_n, lean() ? 1 : (uint64_t)(info.n_cm4 ? info.n_cm4 : 1) * N) || dalloc(&lev, 3 * N) ||
             dalloc(&lpev, 3 * N) || dalloc(&xdiv, 3 * NE) || dalloc(&xdivw, 3 * NE) || dalloc(&fri_pol[0], 3 * NE) ||
             dalloc(&fri_pol[1], 3 * NE))
             return -1;
@@ -344,8 +442,65 @@ public:
         return 0;
     }
 
+    // The lean plan (ZKGPU_MEM_LEAN): the constants, the quotient / FRI
+    // buffers and the trees are held as in the resident plan; the committed
+    // sections of stages 1-3 share ONE arena of (cm1 + cm2 + cm3) extended
+    // columns, laid out by their lifetimes within a proof (words, e = NE / N):
+    //   [0, W1 N)            cm1_n, the proof's input (set_cm1 / witness)
+    //   [W1 N, W1 N + W1 NE) stage 1: cm1_2ns, hashed into tree 1, then dead
+    //   [W1 N, ...)          stages 2-3: tmpExp_n, cm2_n (in (e-1) W1 N
+    //                        words; appended after the arena if larger)
+    //   [W1 NE, +W2 NE)      cm2_2ns from stage 2 on
+    //   [(W1+W2) NE, +W3 NE) cm3_n (bottom, stage 3), then cm3_2ns extended
+    //                        in place over it
+    //   [0, W1 NE)           from stage 4: cm1_2ns, extended in place over
+    //                        cm1_n (whose stage-1 extension was dropped)
+    // The n-domain values die after the stage-3 commit: evmap reads the
+    // extended rows k << blowup with the Lagrange weights of xi / 7, as the
+    // reference does (starks.cpp:308-333).
+    int alloc_lean()
+    {
+        if (alloc_fri()) return -1;
+        memset(&S, 0, sizeof S);
+        const uint64_t W1 = std::max(info.n_cm1, 1u), W2 = std::max(info.n_cm2, 1u), W3 = std::max(info.n_cm3, 1u),
+                       WT = std::max(info.n_tmp, 1u), WC = std::max(info.n_const, 1u);
+        // resident sections: constants (both domains), cm4, q, f
+        if (dalloc(&S.sec[SEC_CONST_N], WC * N) || dalloc(&S.sec[SEC_CONST_2NS], WC * NE) ||
+            dalloc(&S.sec[SEC_CM4_2NS], (uint64_t)std::max(info.n_cm4, 1u) * NE) ||
+            dalloc(&S.sec[SEC_Q_2NS], 3 * NE) || dalloc(&S.sec[SEC_F_2NS], 3 * NE))
+            return -1;
+        uint64_t words = (W1 + W2 + W3) * NE;
+        const uint64_t high = W1 * N, high_words = W1 * NE - W1 * N;
+        uint64_t tmp_off = high;
+        if ((WT + W2) * N > high_words) {
+            tmp_off = words;
+            words += (WT + W2) * N;
+        }
+        words = std::max(words, high + W1 * NE);  // cm1's stage-1 extension
+        if (dalloc(&arena, words)) return -1;
+        S.sec[SEC_CM1_N] = arena;
+        S.sec[SEC_TMP_N] = arena + tmp_off;
+        S.sec[SEC_CM2_N] = arena + tmp_off + WT * N;
+        S.sec[SEC_CM2_2NS] = arena + W1 * NE;
+        S.sec[SEC_CM3_2NS] = arena + (W1 + W2) * NE;
+        S.sec[SEC_CM3_N] = S.sec[SEC_CM3_2NS];
+        cm1_early = arena + high;
+        S.sec[SEC_CM1_2NS] = cm1_early;
+        const uint32_t widths[SEC_COUNT] = {info.n_cm1, info.n_cm2,  info.n_cm3, info.n_tmp, info.n_const, info.n_cm1,
+                                            info.n_cm2, info.n_cm3, info.n_cm4, info.n_const, 3,           3};
+        for (int s = 0; s < SEC_COUNT; s++) {
+            S.ld[s] = s <= SEC_CONST_N ? N : NE;
+            S.ncols[s] = widths[s];
+        }
+        uint64_t tn = zkgpu_gl_merkle_num_elements(NE);
+        for (int t = 0; t < 4; t++)
+            if (dalloc(&nodes[t], tn)) return -1;
+        return dalloc(&const_nodes, tn);
+    }
+
     virtual int alloc()
     {
+        if (lean()) return alloc_lean();
         if (alloc_n() || alloc_fri()) return -1;
         const zkgpu_stark_info *in = &info;
         const uint32_t widths_e[7] = {in->n_cm1, in->n_cm2, in->n_cm3, in->n_cm4, in->n_const, 3, 3};
@@ -407,6 +562,7 @@ public:
         uint64_t ev0[3] = {0, 0, 0};
         if (run(step1, false, ch, ev0, 0)) return -1;
         CK(zkgpu_synchronize());
+        cm1_consumed = false;
         return 0;
     }
 
@@ -417,12 +573,14 @@ public:
         if (take_cm1_async(false)) return -1;  // a pending background load is superseded
         if (zkgpu_load_rows_dev(S.sec[SEC_CM1_N], N, rows, N, info.n_cm1, 0, 0))
             return fail("set_cm1: %s", zkgpu_last_error());
+        cm1_consumed = false;
         return 0;
     }
 
     // cm1_n back as the executor's row-major layout (n rows x n_cm1)
     virtual int get_cm1(uint64_t *rows)
     {
+        if (lean() && cm1_consumed) return fail("get_cm1: the last proof consumed the trace (lean memory plan)");
         void *tmp = nullptr;
         const uint64_t bytes = (uint64_t)info.n_cm1 * N * 8;
         CK(zkgpu_dev_malloc(&tmp, bytes ? bytes : 8));
@@ -435,6 +593,9 @@ public:
 
     virtual int set_cm1_async(const uint64_t *rows)
     {
+        if (lean())
+            return fail("set_cm1_async: not offered under the lean memory plan (the proof extends cm1_n in place; "
+                        "the next trace's buffer would not fit beside it); use set_cm1 between proofs");
         if (take_cm1_async(false)) return -1;
         if (cm1_next_alloc(N, 1)) return -1;
         if (zkgpu_load_rows_async(cm1_next, N, rows, N, info.n_cm1, 0, cm1_xfer[0], xfer_bytes, &cm1_ticket[0]))
@@ -539,6 +700,10 @@ public:
         timers.emplace_back(name, std::chrono::duration<double, std::milli>(clk::now() - t0).count());
         return 0;
     }
+    // exchanges of a sharded proof: (marks, bytes sent) -> the total device
+    // time inside them and that of the largest one
+    std::vector<std::pair<std::pair<uint32_t, uint32_t>, uint64_t>> pend_x;
+    double xchg_ms = 0, xchg_max_ms = 0;
     int flush_timers()
     {
         for (const auto &p : pend_t) {
@@ -547,16 +712,34 @@ public:
             timers[p.first].second = ms;
         }
         pend_t.clear();
+        xchg_ms = xchg_max_ms = 0;
+        uint64_t big = 0;
+        for (const auto &x : pend_x) {
+            double ms = 0;
+            CK(zkgpu_mark_elapsed(x.first.first, x.first.second, &ms));
+            xchg_ms += ms;
+            if (x.second >= big) {
+                big = x.second;
+                xchg_max_ms = ms;
+            }
+        }
+        pend_x.clear();
         n_marks = 0;
         t0_mark = UINT32_MAX;
         return 0;
     }
 
+    // extendPol of an n-domain section into its extended one, then its tree;
+    // in place (lean plan: the section's n-domain values sit at the start of
+    // its extended region) when the two pointers are equal
     int commit(int t, uint32_t sec_n, uint32_t sec_e, uint32_t ncols, Transcript &tr, uint64_t root[4],
                const char *lde_name, const char *tree_name)
     {
         tstart();
-        CK(zkgpu_gl_extend_pol_dev(S.sec[sec_e], NE, S.sec[sec_n], N, NE, N, ncols));
+        if (S.sec[sec_e] == S.sec[sec_n])
+            CK(zkgpu_gl_extend_pol_inplace_dev(S.sec[sec_e], NE, N, ncols));
+        else
+            CK(zkgpu_gl_extend_pol_dev(S.sec[sec_e], NE, S.sec[sec_n], N, NE, N, ncols));
         if (tstop(lde_name)) return -1;
         tstart();
         CK(zkgpu_gl_merkletree_dev(nodes[t], S.sec[sec_e], NE, ncols, NE));
@@ -570,6 +753,9 @@ public:
     // meanwhile) becomes cm1_n when it returns
     virtual int prove(uint64_t *out)
     {
+        if (lean() && cm1_consumed)
+            return fail("stark_prove: the previous proof consumed the trace (lean memory plan: cm1_n is extended in "
+                        "place); load the next one with set_cm1 or witness first");
         const int rc = prove_body(out);
         const int rc2 = take_cm1_async(true);
         return rc ? rc : rc2;
@@ -579,6 +765,7 @@ public:
     {
         timers.clear();
         pend_t.clear();
+        pend_x.clear();
         n_marks = 0;
         auto tall = clk::now();
         Transcript tr;
@@ -588,7 +775,12 @@ public:
         uint64_t roots[4][4];
         std::vector<uint64_t> evals(3 * info.n_ev);
         // STAGE 1 (starks.cpp:49-63)
+        if (lean()) S.sec[SEC_CM1_2NS] = cm1_early;  // hashed, then dropped (extended again at stage 4)
         if (commit(0, SEC_CM1_N, SEC_CM1_2NS, info.n_cm1, tr, roots[0], "STARK_STEP_1_LDE", "STARK_STEP_1_MERKLETREE"))
+            return -1;
+        // lean: the regions of tmpExp_n / cm2_n / cm3_n held other sections;
+        // the columns no stage writes read 0, as under the resident plan
+        if (lean() && (zero_unwritten(SEC_TMP_N) || zero_unwritten(SEC_CM2_N) || zero_unwritten(SEC_CM3_N)))
             return -1;
         // STAGE 2 (:65-144)
         tr.get_field(ch + 0);
@@ -622,6 +814,14 @@ public:
             return -1;
         // STAGE 4 (:226-296)
         tr.get_field(ch + 12);
+        if (lean()) {
+            // cm1_2ns again, over cm1_n (tmpExp_n / cm2_n above it are dead)
+            tstart();
+            cm1_consumed = true;
+            CK(zkgpu_gl_extend_pol_inplace_dev(arena, NE, N, info.n_cm1));
+            S.sec[SEC_CM1_2NS] = arena;
+            if (tstop("STARK_STEP_4_CM1_LDE")) return -1;
+        }
         tstart();
         if (run(step42ns, true, ch, evals.data(), 0)) return -1;
         if (tstop("STARK_STEP_4_CALCULATE_EXPS_2NS")) return -1;
@@ -644,7 +844,14 @@ public:
         // polynomial of degree < N is the same, the field sums are exact, and
         // contiguous n-domain columns read half the lines of the strided
         // extension rows.
-        if (lagrange_xi(xi, 0, N)) return -1;
+        if (lean()) {
+            // the extended rows k << eb are the points 7 w_N^k: the weights of
+            // xi / 7 (starks.cpp:316-322)
+            const uint64_t i7 = inv(7), xs[3] = {mul(xi[0], i7), mul(xi[1], i7), mul(xi[2], i7)};
+            if (lagrange_xi(xs, 0, N)) return -1;
+        } else if (lagrange_xi(xi, 0, N)) {
+            return -1;
+        }
         if (tstop("STARK_STEP_5_LEv_LpEv")) return -1;
         tstart();
         if (evmap_rows(0, N, evals.data())) return -1;
@@ -728,6 +935,7 @@ public:
         uint64_t shift_in = pw(inv(7), N);
         CK(zkgpu_qsplit_dev(qq2, NE, qq1, NE, N, info.q_deg, shift_in));
         CK(zkgpu_gl_ntt_dev(cm4, NE, qq2, NE, NE, info.n_cm4, 0));
+        if (lean()) return 0;  // evmap reads the pieces' extended rows
         // the quotient pieces on the n-domain too (for evmap below): qq2 holds
         // coset-scaled coefficients c_k 7^k (k < N, the rest zero); plain
         // coefficients c_k = qq2_k 7^-k, then NTT_N -> q_p(w_N^j)
@@ -756,12 +964,17 @@ public:
         std::vector<uint64_t> lds(info.n_ev);
         std::vector<uint32_t> dims(info.n_ev), primes(info.n_ev);
         for (uint32_t e = 0; e < info.n_ev; e++) {
-            cols[e] = ncol(ev[4 * e], ev[4 * e + 1], k0, lds[e]);
+            if (lean()) {  // the extended rows k << eb (the n-domain values are gone)
+                lds[e] = NE;
+                cols[e] = S.sec[ev[4 * e]] + (uint64_t)ev[4 * e + 1] * NE + (k0 << eb);
+            } else {
+                cols[e] = ncol(ev[4 * e], ev[4 * e + 1], k0, lds[e]);
+            }
             dims[e] = ev[4 * e + 2];
             primes[e] = ev[4 * e + 3];
         }
         CK(zkgpu_evmap_dev(evals_out, cols.data(), lds.data(), dims.data(), primes.data(), info.n_ev, lev + k0,
-                           lpev + k0, N, nrows, 0));
+                           lpev + k0, N, nrows, lean() ? eb : 0));
         return 0;
     }
 
@@ -913,10 +1126,10 @@ extern "C" {
 
 const char *zkgpu_stark_last_error(void) { return zkgpu_host::g_err; }
 
-int zkgpu_stark_create(void **handle, const zkgpu_stark_info *info)
+int zkgpu_stark_create_ex(void **handle, const zkgpu_stark_info *info, uint32_t memory_plan)
 {
     Starks *s = new Starks();
-    if (s->create(info)) {
+    if (s->create(info, memory_plan)) {
         delete s;
         *handle = nullptr;
         return -1;
@@ -924,6 +1137,13 @@ int zkgpu_stark_create(void **handle, const zkgpu_stark_info *info)
     *handle = s;
     return 0;
 }
+
+int zkgpu_stark_create(void **handle, const zkgpu_stark_info *info)
+{
+    return zkgpu_stark_create_ex(handle, info, ZKGPU_MEM_AUTO);
+}
+
+int zkgpu_stark_memory_mode(void *h) { return ((Starks *)h)->mem_mode; }
 
 int zkgpu_stark_witness(void *h) { return ((Starks *)h)->witness(); }
 int zkgpu_stark_set_cm1(void *h, const uint64_t *rows) { return ((Starks *)h)->set_cm1(rows); }
@@ -1023,6 +1243,21 @@ int zkgpu_stark_memory_plan(const zkgpu_stark_info *info, uint32_t world, uint64
     return s.plan(bytes_per_gpu);
 }
 
+int zkgpu_stark_memory_plan_ex(const zkgpu_stark_info *info, uint32_t memory_plan, uint64_t *bytes)
+{
+    if (!info || !bytes) return zkgpu_host::fail("stark_memory_plan_ex: null argument");
+    *bytes = 0;
+    if (memory_plan > ZKGPU_MEM_LEAN) return zkgpu_host::fail("stark_memory_plan_ex: unknown plan %u", memory_plan);
+    Starks s;
+    if (s.load(info, false)) return -1;
+    if (memory_plan == ZKGPU_MEM_LEAN) {
+        std::string why;
+        if (!s.lean_ok(why)) return zkgpu_host::fail("stark_memory_plan_ex: the lean plan does not apply: %s", why.c_str());
+        s.set_mode(ZKGPU_MEM_LEAN);
+    }
+    return s.plan(bytes);
+}
+
 int zkgpu_comm_rccl_unique_id(uint8_t id[128])
 {
     using zkgpu_host::g_rccl;
@@ -1053,6 +1288,7 @@ int zkgpu_comm_rccl_create(zkgpu_comm *comm, const uint8_t id[128], uint32_t wor
     comm->world = world;
     comm->ctx = ctx;
     comm->exchange = zkgpu_host::rccl_exchange;
+    comm->abort = zkgpu_host::rccl_abort;
     return 0;
 }
 
@@ -1067,10 +1303,12 @@ void zkgpu_comm_rccl_destroy(zkgpu_comm *comm)
 {
     if (!comm || !comm->ctx) return;
     auto *ctx = (zkgpu_host::RcclCtx *)comm->ctx;
-    if (ctx->comm && zkgpu_host::g_rccl.comm_destroy) zkgpu_host::g_rccl.comm_destroy(ctx->comm);
+    if (ctx->comm && !ctx->aborted && zkgpu_host::g_rccl.comm_destroy) zkgpu_host::g_rccl.comm_destroy(ctx->comm);
+    if (ctx->done) (void)hipEventDestroy(ctx->done);
     delete ctx;
     comm->ctx = nullptr;
     comm->exchange = nullptr;
+    comm->abort = nullptr;
 }
 
 }  // extern "C"

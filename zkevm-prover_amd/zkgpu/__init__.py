@@ -47,6 +47,8 @@ _SIGS = {
     "zkgpu_gl_extend_pol": (ctypes.c_int, [vp, vp, u64, u64, u64]),
     "zkgpu_gl_ntt_dev": (ctypes.c_int, [vp, u64, vp, u64, u64, u64, ctypes.c_int]),
     "zkgpu_gl_extend_pol_dev": (ctypes.c_int, [vp, u64, vp, u64, u64, u64, u64]),
+    "zkgpu_gl_extend_pol_inplace_dev": (ctypes.c_int, [vp, u64, u64, u64]),
+    "zkgpu_set_lde_batch_cols": (None, [u64]),
     "zkgpu_rows_to_cols_dev": (ctypes.c_int, [vp, u64, vp, u64, u64]),
     "zkgpu_cols_to_rows_dev": (ctypes.c_int, [vp, vp, u64, u64, u64]),
     "zkgpu_gl_poseidon_full": (ctypes.c_int, [vp, vp]),
@@ -340,6 +342,17 @@ def ntt_dev(dst, ld_dst, src, ld_src, n, ncols, inverse=False):
 def extend_pol_dev(out, ld_out, src, ld_in, n_ext, n, ncols):
     _check(lib().zkgpu_gl_extend_pol_dev(_addr(out), ld_out, _addr(src), ld_in, n_ext, n, ncols),
            "zkgpu_gl_extend_pol_dev")
+
+
+def extend_pol_inplace_dev(base, n_ext, n, ncols):
+    """extendPol in place: base holds ncols n-row columns (ld n) on entry and
+    their n_ext-row extensions (ld n_ext) on return"""
+    _check(lib().zkgpu_gl_extend_pol_inplace_dev(_addr(base), n_ext, n, ncols), "zkgpu_gl_extend_pol_inplace_dev")
+
+
+def set_lde_batch_cols(max_cols):
+    """at most max_cols columns per extend_pol batch (0: the default)"""
+    lib().zkgpu_set_lde_batch_cols(max_cols)
 
 
 def rows_to_cols_dev(cols, ld, rows, nrows, ncols):

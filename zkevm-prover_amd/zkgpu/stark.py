@@ -45,12 +45,13 @@ class CommOp(ctypes.Structure):
 
 
 EXCHANGE = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(CommOp), ctypes.c_uint32)
+ABORT = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
 
 
 class Comm(ctypes.Structure):
-    """zkgpu_comm (include/zkgpu_stark.h)"""
+    """zkgpu_comm (include/zkgpu_stark.h); abort may stay NULL"""
     _fields_ = [("rank", ctypes.c_uint32), ("world", ctypes.c_uint32), ("ctx", ctypes.c_void_p),
-                ("exchange", EXCHANGE)]
+                ("exchange", EXCHANGE), ("abort", ABORT)]
 
 
 _slib = None
@@ -66,6 +67,8 @@ def slib():
         vp, u64 = ctypes.c_void_p, ctypes.c_uint64
         for name, res, args in [
             ("zkgpu_stark_create", ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(_Info)]),
+            ("zkgpu_stark_create_ex", ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(_Info), ctypes.c_uint32]),
+            ("zkgpu_stark_memory_mode", ctypes.c_int, [vp]),
             ("zkgpu_stark_witness", ctypes.c_int, [vp]),
             ("zkgpu_stark_set_cm1", ctypes.c_int, [vp, vp]),
             ("zkgpu_stark_set_cm1_async", ctypes.c_int, [vp, vp]),
@@ -81,6 +84,8 @@ def slib():
                                                           ctypes.POINTER(Comm)]),
             ("zkgpu_stark_memory_plan", ctypes.c_int, [ctypes.POINTER(_Info), ctypes.c_uint32,
                                                        ctypes.POINTER(u64)]),
+            ("zkgpu_stark_memory_plan_ex", ctypes.c_int, [ctypes.POINTER(_Info), ctypes.c_uint32,
+                                                          ctypes.POINTER(u64)]),
             ("zkgpu_comm_rccl_unique_id", ctypes.c_int, [vp]),
             ("zkgpu_comm_rccl_create", ctypes.c_int, [ctypes.POINTER(Comm), vp, ctypes.c_uint32, ctypes.c_uint32]),
             ("zkgpu_comm_rccl_destroy", None, [ctypes.POINTER(Comm)]),
@@ -263,18 +268,34 @@ def make_info(inst, keep):
     return info
 
 
-def memory_plan(inst, world=0):
+# single-GPU memory plans (include/zkgpu_stark.h ZKGPU_MEM_*)
+MEM_AUTO, MEM_RESIDENT, MEM_LEAN = 0, 1, 2
+MEM_NAMES = {MEM_RESIDENT: "resident", MEM_LEAN: "lean"}
+
+
+def memory_plan(inst, world=0, mode=None):
     """HBM bytes per GPU of a prover of this instance (zkgpu_stark_memory_plan:
-    world 0 = one GPU, W = row-sharded over W ranks); no GPU needed."""
+    world 0 = one GPU, W = row-sharded over W ranks; mode MEM_RESIDENT /
+    MEM_LEAN for one GPU, zkgpu_stark_memory_plan_ex); no GPU needed."""
     keep = []
     info = make_info(inst, keep)
     out = ctypes.c_uint64(0)
+    if mode is not None:
+        if world:
+            raise ValueError("memory plans other than the sharded prover's apply to one GPU (world 0)")
+        _check(slib().zkgpu_stark_memory_plan_ex(ctypes.byref(info), mode, ctypes.byref(out)),
+               "zkgpu_stark_memory_plan_ex")
+        return out.value
     _check(slib().zkgpu_stark_memory_plan(ctypes.byref(info), world, ctypes.byref(out)), "zkgpu_stark_memory_plan")
     return out.value
 
 
 class GpuStark:
-    def __init__(self, inst, comm=None):
+    """mode: single-GPU memory plan (MEM_AUTO: resident when it fits the free
+    HBM, else lean; under MEM_LEAN a proof consumes its trace, so witness()
+    or set_cm1() comes before every prove)"""
+
+    def __init__(self, inst, comm=None, mode=MEM_AUTO):
         self.inst = inst
         self._keep = []
         info = make_info(inst, self._keep)
@@ -282,13 +303,20 @@ class GpuStark:
         self.h = ctypes.c_void_p()
         self.comm = comm
         if comm is None:
-            _check(slib().zkgpu_stark_create(ctypes.byref(self.h), ctypes.byref(info)), "zkgpu_stark_create")
+            _check(slib().zkgpu_stark_create_ex(ctypes.byref(self.h), ctypes.byref(info), mode),
+                   "zkgpu_stark_create_ex")
         else:  # row-sharded over comm's ranks (host/sharded_starks.hpp)
             _check(slib().zkgpu_stark_create_sharded(ctypes.byref(self.h), ctypes.byref(info), ctypes.byref(comm.c)),
                    "zkgpu_stark_create_sharded")
 
     def witness(self):
         _check(slib().zkgpu_stark_witness(self.h), "zkgpu_stark_witness")
+
+    def memory_mode(self):
+        """"resident" / "lean" (single-GPU prover), "sharded" """
+        if self.comm is not None:
+            return "sharded"
+        return MEM_NAMES[slib().zkgpu_stark_memory_mode(self.h)]
 
     def set_cm1(self, rows):
         rows = np.ascontiguousarray(rows, np.uint64)
