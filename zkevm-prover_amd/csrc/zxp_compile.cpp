@@ -481,14 +481,11 @@ struct Compiler {
                 const int dim = std::max(A.dim, B.dim);
                 if (to_col) {
                     const int sd = (D.kind == ZXP_COL || dim == 1) ? 1 : 3;
-                    const uint32_t t = new_ssa(dim);
-                    instr.push_back(zxp_instr{I.op, t, ra, rb});
+                    const uint32_t t = opaque_op(I.op, ra, rb, dim);
                     store_col(D, t, sd);
                 } else {
                     const int sd = (D.kind == ZXP_TMP1 || dim == 1) ? 1 : 3;
-                    const uint32_t t = new_ssa(sd);
-                    instr.push_back(zxp_instr{I.op, t, ra, rb});
-                    store_temp(D, identity(t, sd));
+                    store_temp(D, identity(opaque_op(I.op, ra, rb, sd), sd));
                 }
                 continue;
             }
@@ -520,6 +517,28 @@ struct Compiler {
             store_temp(D, std::move(R));
         }
         return 0;
+    }
+
+    // A row-varying product (or sum with a special value) of two realised
+    // operands into an SSA temporary of dimension dim -- or the temporary that
+    // already holds the same operation on the same operands (value numbering:
+    // operands are SSA temporaries, or columns / specials read before any
+    // store to them -- a column read after a store in the row is the stored
+    // SSA value, store_col's forwarding -- so equal operand indices are equal
+    // values).  The reference's step3 / step42ns bytecode recompute ~1,300
+    // such products each (tools/real_programs_compile.py), which the kernel
+    // compiler cannot merge across the kernels' opaque code blocks.
+    std::unordered_map<OKey, uint32_t, OKeyHash> vn;
+    uint32_t opaque_op(uint32_t opc, uint32_t ra, uint32_t rb, int dim)
+    {
+        if ((opc == ZXP_MUL || opc == ZXP_ADD) && rb < ra) std::swap(ra, rb);  // commutative
+        const OKey key{{opc, ra, rb, (uint32_t)dim}};
+        auto it = vn.find(key);
+        if (it != vn.end()) return it->second;
+        const uint32_t t = new_ssa(dim);
+        instr.push_back(zxp_instr{opc, t, ra, rb});
+        vn.emplace(key, t);
+        return t;
     }
 
     // realise operand k's value; for temps, the state entry is updated (in
