@@ -776,15 +776,20 @@ def sharded_children(args, world, rank, local, dist, torch):
     Returns rank 0's summary."""
     # fork-9 widths at 2^23 rows: on one GPU the single-GPU prover under the
     # lean HBM plan (271 GB; the row-sharded prover at W = 1 would hold every
-    # section: 419 GB); from W = 4 the row-sharded prover (217 GB per rank at
-    # W = 4); at W = 2 it needs 369 GB per rank, so 2^22 rows there
-    small = ["--log-n", "22"] if world == 2 and args.log_n > 22 else []
+    # section: 419 GB); from W = 2 the row-sharded prover (W = 2: 313 GB per
+    # rank with the default LDE batches, 294 GB with the 32-column batches
+    # create_sharded then picks; W = 4: 195 GB; W = 8: 132 GB).  If a W = 2
+    # run at 2^23 fails, it runs again at 2^22 (and says so).
     single = world == 1  # the fork-9 runs through `--workload stark` (one GPU, AUTO plan -> lean)
-    runs = [("config4", [], False), ("fork9", ["--fork9"] + small, single),
-            ("fork9_zkevm_shaped", ["--zkevm-shaped"] + small, single)]
+    runs = [("config4", [], False), ("fork9", ["--fork9"], single), ("fork9_zkevm_shaped", ["--zkevm-shaped"], single)]
     out = {}
     for name, extra, one_gpu in runs:
         ok, rec = _sharded_child(args, world, rank, local, dist, torch, extra, "rccl", one_gpu)
+        if not ok and name != "config4" and world == 2 and args.log_n > 22:
+            ok, rec2 = _sharded_child(args, world, rank, local, dist, torch, extra + ["--log-n", "22"], "rccl", one_gpu)
+            if rank == 0:
+                rec = dict(rec2, run_at_2p23=rec) if ok else {"error": "2^23 and 2^22 runs failed", "run_at_2p23": rec,
+                                                              "run_at_2p22": rec2}
         if rank == 0:
             out[name] = rec
         if ok:

@@ -30,7 +30,20 @@ def test_plan_falls_with_world(plan):
     assert plan[1] > plan[2] > plan[4] > plan[8]
     # every trace section is divided by W; the replicated parts (q / f / FRI,
     # 2n x 3 each) stay
-    assert plan[4] / plan[8] > 1.5
+    assert plan[4] / plan[8] > 1.4
+
+
+def test_fork9_two_ranks_fit_with_small_lde_batches(plan):
+    """W = 2 at 2^23: the per-rank plan with the default LDE batches (128
+    columns at 2^24 rows) exceeds the free HBM; with the 32-column batches
+    create_sharded falls back to (fit_lde_batch) it fits"""
+    import zkgpu
+    N, NE = 1 << 23, 1 << 24
+    ms = (751 + 1) // 2  # the largest column share at W = 2
+    L = zkgpu.lib()
+    ws_default, ws_32 = L.zkgpu_lde_workspace_bytes(N, NE, ms), L.zkgpu_lde_workspace_bytes(N, NE, 32)
+    assert ws_default - ws_32 > 15e9
+    assert plan[2] > 308e9 > plan[2] - ws_default + ws_32, (plan[2], ws_default, ws_32)
 
 
 def test_config4_fits_one_gpu():

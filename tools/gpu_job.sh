@@ -3,7 +3,12 @@
 # stops at the first fault / abort / segfault / timeout (exit >= 124 or
 # signal), but continues past an ordinary test failure (exit 1).
 # Usage: tools/gpu_job.sh <step>...
-#   steps: tests large smoke bench instbench bwbench parser step42ns prof pmc cpufull merkle zkevm sharded
+#   steps: tests large smoke bench benchq instbench bwbench parser step42ns prof trace1 pmc cpufull merkle
+#          zkevm northstar profns sharded
+#   parametrised (replace the round-by-round one-off scripts):
+#     pytest:<file>[,<file>...]   those test files (-x -v, 300 s per test)
+#     benchargs:<tag>             python bench.py $BENCH_ARGS -> gpurun_out/bench_<tag>.json
+#     ab:<tag>                    tools/ab_lib.sh <tag> $AB_ARGS (this tree's lib vs lib_ab)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOTDIR=$(pwd)
@@ -106,6 +111,38 @@ for step in "$@"; do
             --no-lde --no-handoff --no-s42 --no-sharded > gpurun_out/bench_zkevm.json 2> gpurun_out/bench_zkevm.err
         ok_or_stop $? "bench zkevm-shaped 2^22"
         cat gpurun_out/bench_zkevm.json
+        ;;
+    pytest:*)
+        files=$(echo "${step#pytest:}" | tr ',' ' ')
+        timeout -k 10 1100 $PYT $files > gpurun_out/pytest_files.log 2>&1
+        ok_or_stop $? "pytest $files"
+        tail -5 gpurun_out/pytest_files.log
+        ;;
+    benchargs:*)
+        tag=${step#benchargs:}
+        timeout -k 10 900 python -u bench.py ${BENCH_ARGS:-} > "gpurun_out/bench_$tag.json" 2> "gpurun_out/bench_$tag.err"
+        ok_or_stop $? "bench $tag (${BENCH_ARGS:-})"
+        tail -c 1500 "gpurun_out/bench_$tag.json"
+        ;;
+    ab:*)
+        bash tools/ab_lib.sh "${step#ab:}" ${AB_ARGS:-}
+        ok_or_stop $? "A/B ${step#ab:}"
+        ;;
+    northstar)
+        # the north-star instance: fork-9 widths + zkEVM-shaped programs, 2^23 rows, one GPU (lean HBM plan)
+        timeout -k 10 400 python -u bench.py --workload stark --zkevm-shaped --log-n 23 --steps 3 --warmup 1 --no-cpu \
+            --no-lde --no-handoff --no-s42 --no-sharded > gpurun_out/bench_northstar.json 2> gpurun_out/bench_northstar.err
+        ok_or_stop $? "bench north star 2^23"
+        tail -c 600 gpurun_out/bench_northstar.json
+        ;;
+    profns)
+        cd /tmp
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOTDIR/gpurun_out/prof_ns" -o run --output-format csv -- \
+            python3 "$ROOTDIR/bench.py" --workload stark --zkevm-shaped --log-n 23 --steps 2 --warmup 1 --no-cpu --no-lde \
+            --no-handoff --no-s42 --no-sharded > "$ROOTDIR/gpurun_out/prof_ns.json" 2> "$ROOTDIR/gpurun_out/prof_ns.err"
+        rc=$?
+        cd "$ROOTDIR"
+        ok_or_stop $rc "rocprofv3 kernel-trace (north star)"
         ;;
     sharded)
         timeout -k 10 600 $PYT tests/test_gpu_sharded_cpp.py tests/test_gpu_zkevm_shaped.py > gpurun_out/pytest_sharded.log 2>&1

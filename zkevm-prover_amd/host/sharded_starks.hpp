@@ -73,6 +73,8 @@ public:
     // slices for a peer are gathered into its region of pack_s (stride_s
     // words per peer), a peer's message lands in its region of pack_r
     uint64_t *pack_s = nullptr, *pack_r = nullptr;
+    // peer d's send region (the rank's own never is one: W - 1 regions)
+    uint64_t *psend(uint32_t d) const { return pack_s + (uint64_t)(d < R ? d : d - 1) * stride_s; }
     uint64_t stride_s = 0, stride_r = 0;
     uint32_t max_ops = 0;  // largest exchange so far (operations posted by this rank)
     // this proof's exchanges: count, bytes this rank sent, the largest one's
@@ -142,8 +144,26 @@ public:
         if (shape(in, c->world, c->rank, true)) return abort_comm(-1);
         if (c->world > 1 && !c->exchange) return fail("stark_create_sharded: the communicator has no exchange");
         read_fail_hook();
-        if (check_budget() || alloc()) return abort_comm(-1);
+        if (fit_lde_batch() || check_budget() || alloc()) return abort_comm(-1);
         return abort_comm(build_const());
+    }
+
+    // LDE column batches of 32 / 64 columns when the default (2^31 words of
+    // scratch: 128 columns at 2^24 rows, 25.8 GB of workspaces) would not fit
+    // beside the rank's sections (fork-9 widths at 2^23 over 2 ranks); the
+    // smaller batches cost 2-3 % of LDE rate.  Process-wide
+    // (zkgpu_set_lde_batch_cols), set only when needed.
+    int fit_lde_batch()
+    {
+        uint64_t avail = 0, total = 0, need = 0;
+        CK(zkgpu_device_memory(&avail, &total));
+        for (uint64_t cap : {(uint64_t)0, (uint64_t)64, (uint64_t)32}) {
+            lde_batch_cap = cap;
+            if (plan(&need)) return -1;
+            if (need <= avail) break;
+        }
+        if (lde_batch_cap) zkgpu_set_lde_batch_cols(lde_batch_cap);
+        return 0;
     }
 
     // n-domain shifts of a program (reads and stores; sets hn) and its stores
@@ -238,7 +258,7 @@ public:
             const uint64_t piece = 3ULL * info.q_deg * (B + nb);
             stride_s = std::max<uint64_t>({ms * BH, 3 * B, piece, 6 * nb});
             stride_r = std::max<uint64_t>({3 * B, piece, 6 * nb});
-            if (dalloc(&pack_s, W * stride_s) || dalloc(&pack_r, W * stride_r)) return -1;
+            if (dalloc(&pack_s, (W - 1) * stride_s) || dalloc(&pack_r, W * stride_r)) return -1;
         }
         if (info.n_pu && W == 1 && dalloc(&puw, 12 * N)) return -1;
         if (info.n_pu && W > 1) {
@@ -268,7 +288,33 @@ public:
 
     // the constants' whole copy while they are set up and committed (set_const:
     // plus the row-major staging of the host's rows)
-    uint64_t setup_bytes() const override { return 2ULL * (info.n_const ? info.n_const : 1) * N * 8; }
+    // the constants' whole copy lives in coln and set_const's row-major
+    // staging in ext when they are large enough (both are free during setup:
+    // the constant commit extends from the whole copy into ext after the
+    // staging is done), else in transient allocations
+    uint64_t const_words() const { return (uint64_t)(info.n_const ? info.n_const : 1) * N; }
+    uint64_t ext_words() const
+    {
+        return W > 1 ? std::max<uint64_t>((uint64_t)max_share() * NE, (uint64_t)W * max_share() * ldn) : 0;
+    }
+    uint64_t coln_words() const { return W > 1 ? (uint64_t)max_share() * N : 0; }
+    uint64_t setup_bytes() const override
+    {
+        return 8 * ((coln_words() >= const_words() ? 0 : const_words()) + (ext_words() >= const_words() ? 0 : const_words()));
+    }
+    // a setup buffer of `words`: `have` (of `cap` words) when it fits, else a
+    // transient allocation (*owned set)
+    int setup_buffer(uint64_t **p, uint64_t *have, uint64_t cap, uint64_t words, void **owned)
+    {
+        *owned = nullptr;
+        if (have && cap >= words) {
+            *p = have;
+            return 0;
+        }
+        CK(zkgpu_dev_malloc(owned, words * 8));
+        *p = (uint64_t *)*owned;
+        return 0;
+    }
     uint64_t lde_cols_max() const override { return max_share(); }
     uint64_t prog_rows_max() const override { return std::max(B, nb); }
 
@@ -410,8 +456,8 @@ public:
         for (uint32_t d = 0; d < W; d++) {
             const std::vector<uint32_t> js = q_owned(d);
             if (d == R || js.empty()) continue;
-            CK(zkgpu_copy_rows_dev(pack_s + d * stride_s, B, 0, nullptr, qb, B, 0, 0, js.data(), (uint32_t)js.size(), B));
-            op(d, 1, pack_s + d * stride_s, js.size() * B * 8);
+            CK(zkgpu_copy_rows_dev(psend(d), B, 0, nullptr, qb, B, 0, 0, js.data(), (uint32_t)js.size(), B));
+            op(d, 1, psend(d), js.size() * B * 8);
         }
         if (!mine.empty()) {
             for (uint32_t s = 0; s < W; s++)
@@ -440,7 +486,7 @@ public:
         const uint32_t np = (uint32_t)my_pieces.size();
         for (uint32_t d = 0; d < W && np; d++) {
             if (d == R) continue;
-            uint64_t *m = pack_s + d * stride_s;
+            uint64_t *m = psend(d);
             CK(zkgpu_copy_rows_dev(m, B, 0, nullptr, cm4, NE, (uint64_t)d * B, 0, my_pieces.data(), np, B));
             CK(zkgpu_copy_rows_dev(m + (uint64_t)np * B, nb, 0, nullptr, cm4_n, N, (uint64_t)d * nb, 0, my_pieces.data(),
                                    np, nb));
@@ -629,34 +675,35 @@ public:
     int build_const() override
     {
         void *w = nullptr;
-        CK(zkgpu_dev_malloc(&w, (uint64_t)(info.n_const ? info.n_const : 1) * N * 8));
-        uint64_t *whole = (uint64_t *)w;
+        uint64_t *whole = nullptr;
+        if (setup_buffer(&whole, coln, coln_words(), const_words(), &w)) return -1;
         const zkgpu_sections blocks = S;
         S.sec[SEC_CONST_N] = whole;  // Starks::build_const's fill on the whole domain ...
         S.ld[SEC_CONST_N] = N;
         int rc = fill_const();
         S = blocks;
         if (!rc) rc = const_from_whole(whole);  // ... then the commit and the cut
-        zkgpu_dev_free(w);
+        if (w) zkgpu_dev_free(w);
         if (!rc) init_publics();
         return rc;
     }
 
     int set_const(const uint64_t *rows) override
     {
-        void *w = nullptr, *tmp = nullptr;
-        CK(zkgpu_dev_malloc(&w, (uint64_t)(info.n_const ? info.n_const : 1) * N * 8));
-        int rc = zkgpu_dev_malloc(&tmp, (uint64_t)(info.n_const ? info.n_const : 1) * N * 8);
+        void *w = nullptr, *t = nullptr;
+        uint64_t *whole = nullptr, *tmp = nullptr;
+        if (setup_buffer(&whole, coln, coln_words(), const_words(), &w)) return -1;
+        int rc = setup_buffer(&tmp, ext, ext_words(), const_words(), &t);
         if (!rc) rc = zkgpu_memcpy_h2d(tmp, rows, (uint64_t)info.n_const * N * 8);
-        if (!rc) rc = zkgpu_rows_to_cols_dev((uint64_t *)w, N, (const uint64_t *)tmp, N, info.n_const);
+        if (!rc) rc = zkgpu_rows_to_cols_dev(whole, N, tmp, N, info.n_const);
         if (!rc) rc = zkgpu_synchronize();
-        if (tmp) zkgpu_dev_free(tmp);
+        if (t) zkgpu_dev_free(t);
         if (rc) {
-            zkgpu_dev_free(w);
+            if (w) zkgpu_dev_free(w);
             return fail("set_const: %s", zkgpu_last_error());
         }
-        rc = const_from_whole((uint64_t *)w);
-        zkgpu_dev_free(w);
+        rc = const_from_whole(whole);
+        if (w) zkgpu_dev_free(w);
         return rc;
     }
 
@@ -683,14 +730,16 @@ public:
     // the executor's row-major buffer: the rank takes rows [r0, r0 + ldn) mod N
     int set_cm1(const uint64_t *rows) override
     {
-        void *tmp = nullptr;
+        void *t = nullptr;
+        uint64_t *tmp = nullptr;
         const uint64_t w = info.n_cm1, first = std::min(ldn, N - r0());
-        CK(zkgpu_dev_malloc(&tmp, w * ldn * 8));
+        // the row-major staging in ext (free between proofs) when it fits
+        if (setup_buffer(&tmp, ext, ext_words(), std::max<uint64_t>(1, w * ldn), &t)) return -1;
         int rc = zkgpu_memcpy_h2d(tmp, rows + r0() * w, first * w * 8);
-        if (!rc && ldn > first) rc = zkgpu_memcpy_h2d((uint64_t *)tmp + first * w, rows, (ldn - first) * w * 8);
-        if (!rc) rc = zkgpu_rows_to_cols_dev(S.sec[SEC_CM1_N], ldn, (const uint64_t *)tmp, ldn, info.n_cm1);
+        if (!rc && ldn > first) rc = zkgpu_memcpy_h2d(tmp + first * w, rows, (ldn - first) * w * 8);
+        if (!rc) rc = zkgpu_rows_to_cols_dev(S.sec[SEC_CM1_N], ldn, tmp, ldn, info.n_cm1);
         if (!rc) rc = zkgpu_synchronize();
-        zkgpu_dev_free(tmp);
+        if (t) zkgpu_dev_free(t);
         if (rc) return fail("set_cm1: %s", zkgpu_last_error());
         return 0;
     }
@@ -736,9 +785,9 @@ public:
         while ((1ULL << log_ne) < NE) log_ne++;
         for (uint32_t d = 0; d < W; d++) {
             if (d == R || hi == lo) continue;
-            CK(zkgpu_copy_rows_dev(pack_s + d * stride_s, BH, 0, nullptr, ext, NE, (uint64_t)d * B, log_ne, nullptr,
+            CK(zkgpu_copy_rows_dev(psend(d), BH, 0, nullptr, ext, NE, (uint64_t)d * B, log_ne, nullptr,
                                    hi - lo, B + H));
-            op(d, 1, pack_s + d * stride_s, (uint64_t)(hi - lo) * BH * 8);
+            op(d, 1, psend(d), (uint64_t)(hi - lo) * BH * 8);
         }
         for (uint32_t s = 0; s < W; s++) {
             uint32_t slo, shi;
@@ -797,7 +846,7 @@ public:
         // one message per peer, column-major bl x 3 kw (column 3 kc + c: chunk
         // kc, component c); the rank's own lands straight in gath
         for (uint32_t d = 0; d < W; d++) {
-            uint64_t *m = d == R ? gath + (uint64_t)R * msg : pack_s + d * stride_s;
+            uint64_t *m = d == R ? gath + (uint64_t)R * msg : psend(d);
             for (uint64_t kc = 0; kc < kw; kc++)
                 CK(zkgpu_copy_rows_dev(m + kc * 3 * bl, bl, 0, nullptr, f + kc * w + (uint64_t)d * bl, B, 0, 0, nullptr,
                                        3, bl));
@@ -1008,8 +1057,8 @@ public:
                 CK(zkgpu_h1h2_shard_place(h1, ldn, h2, ldn, hs_seg + (a - O), sld, a, b - a, r0(), d));
                 continue;
             }
-            CK(zkgpu_copy_rows_dev(pack_s + e * stride_s, b - a, 0, nullptr, hs_seg, sld, a - O, 0, nullptr, d, b - a));
-            op(e, 1, pack_s + e * stride_s, (b - a) * d * 8);
+            CK(zkgpu_copy_rows_dev(psend(e), b - a, 0, nullptr, hs_seg, sld, a - O, 0, nullptr, d, b - a));
+            op(e, 1, psend(e), (b - a) * d * 8);
         }
         std::vector<std::pair<uint64_t, uint64_t>> got(W, {0, 0});
         for (uint32_t s = 0; s < W; s++) {

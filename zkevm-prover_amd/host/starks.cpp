@@ -225,6 +225,9 @@ public:
         return std::max({info.n_cm1, info.n_cm2, info.n_cm3, info.n_const, 1u});
     }
     virtual uint64_t prog_rows_max() const { return NE; }
+    // at most this many columns per LDE batch (0: the library's default);
+    // the sharded prover lowers it when its plan would not fit otherwise
+    uint64_t lde_batch_cap = 0;
     int plan(uint64_t *bytes)
     {
         dry = true;
@@ -233,7 +236,8 @@ public:
         dry = false;
         if (rc) return -1;
         const uint64_t ntt_ws = std::max<uint64_t>(3, info.n_cm4) * NE * 8;  // ntt_dev scratch (workspace slot 1)
-        const uint64_t lde_ws = zkgpu_lde_workspace_bytes(N, NE, lde_cols_max());
+        const uint64_t lde_ws = zkgpu_lde_workspace_bytes(
+            N, NE, lde_batch_cap ? std::min<uint64_t>(lde_cols_max(), lde_batch_cap) : lde_cols_max());
         const uint64_t prog_ws = 64ULL * prog_rows_max() * 8;  // <= 64 carried columns between program segments
         const uint64_t h1h2_ws = info.n_pu ? 32ULL * N : 0;    // 2N-slot table + counts + scan
         *bytes = planned + setup_bytes() + std::max(lde_ws, ntt_ws + zkgpu_lde_workspace_bytes(N, NE, 0)) + prog_ws +
