@@ -1206,6 +1206,19 @@ def main():
             res["quotient_zkevm_shaped"] = quotient
         if sharded is not None:
             res["sharded_one_proof"] = sharded
+            ns = sharded.get("fork9_zkevm_shaped") or {}
+            if ns.get("value"):
+                # the north-star instance (BASELINE.json north_star: the 2^23-row
+                # zkEVM trace), surfaced beside the config-4 headline
+                res["north_star"] = {
+                    "value": ns["value"], "unit": ns["unit"], "n_gpus": ns["n_gpus"], "log_n": ns.get("log_n"),
+                    "instance": "fork-9 widths (751/168/408/6 committed, 234 constants) + the five zkEVM-shaped "
+                                "expression programs (zkgpu/zkevm_shaped.py)",
+                    "prover": ns.get("prover"),
+                    "hbm_plan": "lean (one GPU)" if world == 1 else "row-sharded",
+                    "verified_by": "tests/test_gpu_verify_full.py (verifier replay of the GPU's 2^23 proof: transcript, "
+                                   "every Merkle path, every FRI fold, the FRI polynomial at the query rows)",
+                    "source": "sharded_one_proof.fork9_zkevm_shaped"}
         if replicas is not None:
             res["replicas"] = replicas
             one = (sharded or {}).get("config4") or {}

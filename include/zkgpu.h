@@ -119,6 +119,12 @@ uint64_t zkgpu_gl_merkle_num_elements(uint64_t nrows);
 int zkgpu_gl_merkletree(uint64_t *nodes, const uint64_t *src, uint64_t ncols, uint64_t nrows);
 /* device-resident: src column-major (ld), nodes on device */
 int zkgpu_gl_merkletree_dev(uint64_t *nodes, const uint64_t *src, uint64_t ld, uint64_t ncols, uint64_t nrows);
+/* the same tree over a section held in two regions: columns [0, split) at
+ * src + c*ld, columns [split, ncols) at src2 + (c - split)*ld (split a
+ * multiple of 8: the linear hash absorbs 8 columns at a time).  The lean
+ * memory plan's stage-1 commit (host/starks.cpp). */
+int zkgpu_gl_merkletree2_dev(uint64_t *nodes, const uint64_t *src, const uint64_t *src2, uint64_t ld, uint64_t split,
+                             uint64_t ncols, uint64_t nrows);
 /* device-resident, row-major source (FRI trees: friProve.cpp:117-121) */
 int zkgpu_gl_merkletree_rows_dev(uint64_t *nodes, const uint64_t *src, uint64_t ncols, uint64_t nrows);
 /* ---- constant tree (tools/starkpil/bctree) -----------------------------

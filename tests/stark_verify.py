@@ -23,11 +23,14 @@ description (its step52ns program and evaluation map) and the verkey:
     zkgpu/synthetic.py): the zkEVM-shaped instance's step52ns is a program
     with the reference's opcode histogram, not its FRI polynomial
     (zkgpu/zkevm_shaped.py), so its f is not of low degree (low_degree=False).
-Not checked: the constraint identity C(xi) Z_H(xi)^-1 = sum_p xi^(pN) q_p(xi),
-which needs the verifier's evaluation of step42ns at an extension-field point
-(the oracle interpreter evaluates on base-field domain points only) and, for
-the zkEVM-shaped instance, a trace that satisfies its constraints (it does
-not: the quotient there is not a low-degree polynomial).
+  * the constraint identity at xi (starks.cpp:222-241; the verifier's check
+    of the pil2/pilcom verifier circuits): step42ns run over F_p^3 at the
+    single point xi with every column operand read from the proof's evals
+    (row shift 0 -> the eval at xi, the next row -> at w xi, evMap's prime),
+    Z_H^-1 -> (xi^N - 1)^-1, equals q(xi) = sum_p xi^(pN) q_p(xi) from the
+    quotient pieces' evals.  Also only for the synthetic config-4 instance:
+    it is a valid AIR (its trace satisfies its constraints); the zkEVM-shaped
+    trace does not satisfy its stand-in constraints.
 """
 import ctypes
 
@@ -88,6 +91,90 @@ def final_degree_ok(oc, inst, proof):
     return bool(np.all(coef[lim:] == 0)), int(np.count_nonzero(np.any(coef[lim:] != 0, axis=1)))
 
 
+def _f3_mul(a, b):
+    c0 = a[0] * b[0]
+    c1 = a[0] * b[1] + a[1] * b[0]
+    c2 = a[0] * b[2] + a[1] * b[1] + a[2] * b[0]
+    c3 = a[1] * b[2] + a[2] * b[1]
+    c4 = a[2] * b[2]
+    return ((c0 + c3) % P, (c1 + c3 + c4) % P, (c2 + c4) % P)  # x^3 = x + 1
+
+
+def _f3_pow(a, e):
+    r = (1, 0, 0)
+    while e:
+        if e & 1:
+            r = _f3_mul(r, a)
+        a = _f3_mul(a, a)
+        e >>= 1
+    return r
+
+
+def _f3_inv(a):
+    return _f3_pow(a, P ** 3 - 2)
+
+
+def quotient_identity(inst, proof, ch, publics):
+    """(C(xi) Z_H(xi)^-1, q(xi)) from the proof's evals (module doc): step42ns
+    interpreted over F_p^3 (ops and operands of include/zkgpu_zxp.h)"""
+    from zkgpu import synthetic as sy
+    evals = [tuple(int(v) % P for v in e) for e in proof["evals"]]
+    chal = {k: tuple(int(v) for v in ch[k]) for k in ch}
+    xi = chal[7]
+    n = 1 << inst.n_bits
+    xin = _f3_pow(xi, n)
+    zi = _f3_inv(((xin[0] - 1) % P, xin[1], xin[2]))
+    nxt = 1 << inst.blowup_bits
+    prog = inst.programs["step42ns"]
+    regs, out = {}, {}
+
+    def val(i):
+        kind, a, b, c = prog.opnd[i]
+        if kind in (sy.TMP1, sy.TMP3):
+            return regs[i]
+        if kind in (sy.COL, sy.COL3):
+            if c not in (0, nxt):
+                raise AssertionError("step42ns reads column (%d, %d) at row shift %d" % (a, b, c))
+            return evals[inst.ev_index[(a, b, 0 if c == 0 else 1)]]
+        if kind == sy.LIT:
+            return ((a | (b << 32)) % P, 0, 0)
+        if kind == sy.CHAL:
+            return chal[a]
+        if kind == sy.PUB:
+            return (int(publics[a]) % P, 0, 0)
+        if kind == sy.X:
+            return xi
+        if kind == sy.EVAL:
+            return evals[a]
+        if kind == sy.ZI:
+            return zi
+        raise AssertionError("step42ns operand kind %d at xi" % kind)
+
+    for op, dst, a, b in prog.instr:
+        x = val(a)
+        if op == sy.COPY:
+            r = x
+        else:
+            y = val(b)
+            if op == sy.ADD:
+                r = tuple((u + v) % P for u, v in zip(x, y))
+            elif op == sy.SUB:
+                r = tuple((u - v) % P for u, v in zip(x, y))
+            else:
+                r = _f3_mul(x, y)
+        if prog.opnd[dst][0] in (sy.TMP1, sy.TMP3):
+            regs[dst] = r
+        else:
+            out[prog.opnd[dst][1:]] = r
+    cz = out[(sy.SEC_Q_2NS, 0, 0)]
+    q, xp = (0, 0, 0), (1, 0, 0)
+    for piece in range(inst.q_deg):
+        qp = _f3_mul(xp, evals[inst.ev_index[(sy.SEC_CM4_2NS, 3 * piece, 0)]])
+        q = tuple((u + v) % P for u, v in zip(q, qp))
+        xp = _f3_mul(xp, xin)
+    return cz, q
+
+
 def verify(inst, proof, verkey, publics, low_degree=True):
     """All checks of the module doc on a zkin-layout proof (canonical strings
     or ints; the final-degree check only with low_degree).  Returns the
@@ -107,6 +194,8 @@ def verify(inst, proof, verkey, publics, low_degree=True):
                 bad["fri_pol"] += 1
     if low_degree:
         bad["final_degree"] = final_degree_ok(oc, inst, proof)[1]
+        cz, q = quotient_identity(inst, proof, ch, pub)
+        bad["quotient_at_xi"] = int(cz != q)
     bad["queries"] = len(ys)
     return bad
 

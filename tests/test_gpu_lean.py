@@ -53,15 +53,20 @@ def oracle_proofs(oracle):
 
 
 @pytest.mark.parametrize("kind", [False, "zkevm"], ids=["config4", "zkevm_shaped"])
-@pytest.mark.parametrize("batch", [0, 7], ids=["batch_default", "batch7"])
-def test_lean_proof_equals_oracle(zkgpu, oracle_proofs, kind, batch):
+@pytest.mark.parametrize("batch,keep", [(0, None), (7, "0"), (7, "45"), (0, "100000")],
+                         ids=["batch_default-keep_auto", "batch7-keep0", "batch7-keep_part", "keep_all"])
+def test_lean_proof_equals_oracle(zkgpu, oracle_proofs, monkeypatch, kind, batch, keep):
     """config-4 and the zkEVM-shaped instance at 2^10 under the lean plan
     (with the LDE batches forced to 7 columns: the in-place extensions of cm1
-    (100 / 751 columns) and cm3 run in many batches) == the oracle's proof;
-    and the trace is consumed: a second prove without a new trace fails,
-    witness() then prove() gives the same proof again"""
+    (100 / 751 columns) and cm3 run in many batches; cm1's extended columns
+    kept from stage 1: none -- all extended again at stage 4 --, some -- a
+    two-region stage-1 tree --, all, or as many as the HBM holds) == the
+    oracle's proof; and the trace is consumed: a second prove without a new
+    trace fails, witness() then prove() gives the same proof again"""
     from zkgpu import ZkgpuError
     from zkgpu.stark import GpuStark, MEM_LEAN
+    if keep is not None:
+        monkeypatch.setenv("ZKGPU_LEAN_KEEP_COLS", keep)
     zkgpu.set_lde_batch_cols(batch)
     g = GpuStark(_inst(kind), mode=MEM_LEAN)
     try:
@@ -129,3 +134,22 @@ def test_lean_refused_when_the_quotient_reads_the_n_domain(zkgpu):
     p.op(sy.ADD, p.o(sy.TMP1, 0, 0, 0), a, a)
     with pytest.raises(ZkgpuError, match="lean memory plan does not apply"):
         GpuStark(inst, mode=MEM_LEAN)
+
+
+@pytest.mark.parametrize("ncols,split", [(100, 64), (751, 536), (13, 8), (9, 0)])
+def test_merkletree_two_regions(zkgpu, ncols, split):
+    """zkgpu_gl_merkletree2_dev (columns [0, split) in one region, the rest in
+    another) == zkgpu_gl_merkletree_dev of the section in one piece"""
+    import torch
+    n = 1 << 10
+    g = torch.Generator(device="cuda")
+    g.manual_seed(ncols)
+    src = torch.randint(0, 2**63 - 1, (ncols, n), dtype=torch.int64, device="cuda", generator=g)
+    a = src[:split].contiguous() if split else torch.zeros((1, n), dtype=torch.int64, device="cuda")
+    b = src[split:].contiguous()
+    ref = torch.empty(zkgpu.merkle_num_elements(n), dtype=torch.int64, device="cuda")
+    got = torch.empty_like(ref)
+    zkgpu.merkletree_dev(ref, src, n, ncols, n)
+    zkgpu.merkletree2_dev(got, a, b, n, split, ncols, n)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)

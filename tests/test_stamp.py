@@ -30,7 +30,8 @@ def test_stamp_depends_on_sources_and_env(tmp_path, monkeypatch):
             src += open(os.path.join(stamp.PKG, d, fn), errors="replace").read()
     read = set(re.findall(r'getenv\("(ZKGPU_\w+)"\)', src))
     not_kernel = {"ZKGPU_ZXP_JIT", "ZKGPU_JIT_CACHE", "ZKGPU_JIT_LOG", "ZKGPU_ZXP_JIT_THREADS", "ZKGPU_ZXP_JIT_ONLY",
-                  "ZKGPU_ZXP_JIT_DUMP", "ZKGPU_RUN_ID"}
+                  "ZKGPU_ZXP_JIT_DUMP", "ZKGPU_RUN_ID", "ZKGPU_COMM_TIMEOUT_S", "ZKGPU_LEAN_KEEP_COLS",
+                  "ZKGPU_SYNC_STAGES", "ZKGPU_TEST_FAIL_EXCHANGE"}
     listed = {k for v in stamp.ENV.values() for k in v}
     assert read <= listed | not_kernel, read - listed - not_kernel
     # the interpreter/compiled switch is not a kernel setting

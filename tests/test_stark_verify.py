@@ -52,3 +52,24 @@ def test_final_polynomial_degree(proved):
     p = json.loads(json.dumps(proof))
     p["finalPol"][3][0] = _bump(p["finalPol"][3][0])
     assert not sv.final_degree_ok(oc, inst, p)[0]
+
+
+def test_quotient_identity_at_xi(proved):
+    """config-4 is a valid AIR: C(xi) Z_H(xi)^-1 == sum_p xi^(pN) q_p(xi) from
+    the evals; a changed eval of a constrained column or of a quotient piece
+    breaks it"""
+    inst, proof, vk, pub, low = proved
+    if not low:
+        pytest.skip("the zkEVM-shaped trace does not satisfy its stand-in constraints (stark_verify doc)")
+    from oracle import oracle as oc
+    from zkgpu import synthetic as sy
+    steps = list(inst.fri_steps)
+    _, _, ch = sv.gr.verify_fri(oc, proof, [int(v) for v in vk], [int(v) for v in pub], steps, inst.n_queries)
+    cz, q = sv.quotient_identity(inst, proof, ch, pub)
+    assert cz == q and any(q)
+    for i in (inst.ev_index[(sy.SEC_CM1_2NS, 2, 0)], inst.ev_index[(sy.SEC_CM4_2NS, 3, 0)]):
+        p = json.loads(json.dumps(proof))
+        p["evals"][i][1] = _bump(p["evals"][i][1])
+        cz, q = sv.quotient_identity(inst, p, ch, pub)
+        assert cz != q
+        assert sv.failures(sv.verify(inst, p, vk, pub)).get("quotient_at_xi")

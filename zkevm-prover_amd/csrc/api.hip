@@ -555,6 +555,20 @@ int zkgpu_gl_merkletree_dev(uint64_t *nodes, const uint64_t *src, uint64_t ld, u
     return merkle_levels(nodes, nrows, g_ctx.stream);
 }
 
+int zkgpu_gl_merkletree2_dev(uint64_t *nodes, const uint64_t *src, const uint64_t *src2, uint64_t ld, uint64_t split,
+                             uint64_t ncols, uint64_t nrows)
+{
+    int rc;
+    if ((rc = require_init())) return rc;
+    if (!nrows) return 0;
+    if (!is_pow2(nrows)) return set_error(ZKGPU_ERR_ARG, "merkletree2: nrows must be a power of two");
+    if (split > ncols || (split < ncols && split % 8))
+        return set_error(ZKGPU_ERR_ARG, "merkletree2: split %llu must be a multiple of 8 up to ncols",
+                         (unsigned long long)split);
+    if ((rc = merkle_leaves_cols(nodes, src, ncols, nrows, ld, g_ctx.stream, src2, split))) return rc;
+    return merkle_levels(nodes, nrows, g_ctx.stream);
+}
+
 int zkgpu_gl_merkletree_rows_dev(uint64_t *nodes, const uint64_t *src, uint64_t ncols, uint64_t nrows)
 {
     int rc;
@@ -988,12 +1002,13 @@ static void zxp_alloc_slots(const zxp_instr *in, uint32_t n_instr, std::vector<z
 // zhInv tables (<= 64 words) on the device, one per (log omega, extend
 // bits), uploaded once: the compiled expression kernels read them and need
 // no per-call upload (and no stream sync for a pageable source)
+// (keyed by device too: zkgpu_init may switch devices)
 static const uint64_t *zh_table(uint32_t log_omega, uint32_t eb, const uint64_t *zhv, size_t n)
 {
     static std::mutex mu;
-    static std::map<std::pair<uint32_t, uint32_t>, uint64_t *> tabs;
+    static std::map<std::pair<int, std::pair<uint32_t, uint32_t>>, uint64_t *> tabs;
     std::lock_guard<std::mutex> lk(mu);
-    const auto key = std::make_pair(log_omega, eb);
+    const auto key = std::make_pair(g_ctx.device, std::make_pair(log_omega, eb));
     auto it = tabs.find(key);
     if (it != tabs.end()) return it->second;
     uint64_t *d = nullptr;
@@ -1844,13 +1859,23 @@ int zkgpu_prof_kernels(char *buf, uint64_t buflen)
     buf[n] = 0;
     return 0;
 }
-// stream marks for the host prover's stage timers (no synchronisation)
+// stream marks for the host prover's stage timers (no synchronisation);
+// events belong to a device: a zkgpu_init on another device drops them
 static hipEvent_t g_marks[ZKGPU_MARKS];
+static int g_marks_dev = -1;
 int zkgpu_mark(uint32_t slot)
 {
     int rc;
     if ((rc = require_init())) return rc;
     if (slot >= ZKGPU_MARKS) return set_error(ZKGPU_ERR_ARG, "mark: slot %u >= %d", slot, ZKGPU_MARKS);
+    if (g_marks_dev != g_ctx.device) {
+        for (hipEvent_t &e : g_marks)
+            if (e) {
+                (void)hipEventDestroy(e);
+                e = nullptr;
+            }
+        g_marks_dev = g_ctx.device;
+    }
     if (!g_marks[slot] && (rc = check_hip(hipEventCreate(&g_marks[slot]), "mark event"))) return rc;
     return check_hip(hipEventRecord(g_marks[slot], g_ctx.stream), "mark record");
 }

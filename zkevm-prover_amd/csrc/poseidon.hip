@@ -31,9 +31,14 @@ __global__ void k_poseidon_batch(uint64_t *out, const uint64_t *in, uint64_t n, 
     for (int k = 0; k < w; k++) out[i * w + k] = gl_canon(st[k]);
 }
 
-// leaf digests from a column-major source (column c at src + c*ld)
-__global__ void __launch_bounds__(256) k_leaves_cols(uint64_t *digests, const uint64_t *__restrict__ src,
-                                                    uint64_t ncols, uint64_t nrows, uint64_t ld)
+// leaf digests from a column-major source (column c at src + c*ld); SPLIT:
+// columns from `split` on (a multiple of 8, so no absorption chunk straddles
+// it) at src2 + (c - split)*ld -- one section held in two regions (the lean
+// plan's stage-1 commit, host/starks.cpp)
+template <bool SPLIT>
+__device__ __forceinline__ void leaves_cols(uint64_t *digests, const uint64_t *__restrict__ src, uint64_t ncols,
+                                            uint64_t nrows, uint64_t ld, const uint64_t *__restrict__ src2,
+                                            uint64_t split)
 {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nrows) return;
@@ -50,14 +55,26 @@ __global__ void __launch_bounds__(256) k_leaves_cols(uint64_t *digests, const ui
 #pragma unroll
                 for (int k = 0; k < 4; k++) st[8 + k] = st[k];
             }
+            const uint64_t *b = (!SPLIT || c0 < split) ? src + c0 * ld : src2 + (c0 - split) * ld;
 #pragma unroll
-            for (int k = 0; k < 8; k++) st[k] = (uint64_t)k < nk ? src[(c0 + k) * ld + i] : 0;
+            for (int k = 0; k < 8; k++) st[k] = (uint64_t)k < nk ? b[k * ld + i] : 0;
             poseidon_perm(st);
         }
     }
     uint64_t *d = digests + 4 * i;
 #pragma unroll
     for (int k = 0; k < 4; k++) d[k] = ncols <= 4 ? st[k] : gl_canon(st[k]);
+}
+__global__ void __launch_bounds__(256) k_leaves_cols(uint64_t *digests, const uint64_t *__restrict__ src,
+                                                    uint64_t ncols, uint64_t nrows, uint64_t ld)
+{
+    leaves_cols<false>(digests, src, ncols, nrows, ld, nullptr, ncols);
+}
+__global__ void __launch_bounds__(256) k_leaves_cols2(uint64_t *digests, const uint64_t *__restrict__ src,
+                                                     uint64_t ncols, uint64_t nrows, uint64_t ld,
+                                                     const uint64_t *__restrict__ src2, uint64_t split)
+{
+    leaves_cols<true>(digests, src, ncols, nrows, ld, src2, split);
 }
 
 // leaf digests from a row-major source (row i at src + i*ncols)
@@ -293,11 +310,16 @@ int poseidon_batch(uint64_t *out, const uint64_t *in, uint64_t n, int full, hipS
 }
 
 int merkle_leaves_cols(uint64_t *digests, const uint64_t *src, uint64_t ncols, uint64_t nrows, uint64_t ld,
-                       hipStream_t s)
+                       hipStream_t s, const uint64_t *src2, uint64_t split)
 {
     if (!nrows) return 0;
     prof_begin(s);
-    hipLaunchKernelGGL(k_leaves_cols, dim3(blocks_for(nrows, 256)), dim3(256), 0, s, digests, src, ncols, nrows, ld);
+    if (src2 && split < ncols && ncols > 4)
+        hipLaunchKernelGGL(k_leaves_cols2, dim3(blocks_for(nrows, 256)), dim3(256), 0, s, digests, src, ncols, nrows,
+                           ld, src2, split);
+    else
+        hipLaunchKernelGGL(k_leaves_cols, dim3(blocks_for(nrows, 256)), dim3(256), 0, s, digests, src, ncols, nrows,
+                           ld);
     prof_end("k_leaves_cols", 8.0 * (double)nrows * (double)ncols + 32.0 * (double)nrows, s);
     return check_launch("k_leaves_cols");
 }

@@ -72,7 +72,7 @@ int lde3_columns(Ctx &c, uint64_t *out, uint64_t ld_out, const uint64_t *in, uin
 // ---- poseidon.hip
 int poseidon_batch(uint64_t *out, const uint64_t *in, uint64_t n, int full, hipStream_t s);
 int merkle_leaves_cols(uint64_t *digests, const uint64_t *src, uint64_t ncols, uint64_t nrows, uint64_t ld,
-                       hipStream_t s);
+                       hipStream_t s, const uint64_t *src2 = nullptr, uint64_t split = 0);
 int merkle_leaves_rows(uint64_t *digests, const uint64_t *src, uint64_t ncols, uint64_t nrows, hipStream_t s);
 int merkle_levels(uint64_t *nodes, uint64_t nrows, hipStream_t s);
 int merkle_open_cols(uint64_t *vals, uint64_t *sibs, const uint64_t *nodes, const uint64_t *src, uint64_t ncols,

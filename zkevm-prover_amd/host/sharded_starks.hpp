@@ -831,6 +831,10 @@ public:
     // output (1/kk of f) is then all-gathered and the later, smaller layers run
     // as before.  Replaces the all-gather of f (3 NE words to every rank) and
     // the fold of the whole 2^steps[0] domain on every rank.
+    // Invariant: when this holds, fri_pol[0] is never filled (f stays in the
+    // rank's row blocks, S.sec[SEC_F_2NS]); the FRI loop passes a null pol to
+    // fri_transpose_layer(0, ...), whose override below reads the blocks.
+    bool fri_pol0_filled() const override { return !fri_first_sharded(); }
     bool fri_first_sharded() const
     {
         if (W == 1 || fri_steps.size() < 2) return false;
@@ -841,6 +845,7 @@ public:
     int fri_transpose_layer(size_t si, uint64_t *aux, const uint64_t *pol, uint64_t degree, uint32_t nb) override
     {
         if (si != 0 || !fri_first_sharded()) return Starks::fri_transpose_layer(si, aux, pol, degree, nb);
+        (void)pol;  // null here (fri_pol0_filled)
         const uint64_t w = 1ULL << nb, kk = NE / w, kw = kk / W, bl = w / W, msg = 3 * kw * bl;
         const uint64_t *f = S.sec[SEC_F_2NS];  // the rank's f rows: 3 columns, ld B
         // one message per peer, column-major bl x 3 kw (column 3 kc + c: chunk

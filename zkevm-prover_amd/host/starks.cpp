@@ -184,6 +184,12 @@ public:
     uint64_t *arena = nullptr, *cm1_early = nullptr;
     std::vector<uint32_t> unwritten[5];
     bool cm1_consumed = false;
+    // lean plan: cm1's last keep_cols extended columns, kept from stage 1 in
+    // their own region (what the HBM left over by the plan holds) and copied
+    // into place at stage 4 instead of being extended again; (n_cm1 -
+    // keep_cols) is a multiple of 8 (the linear hash's chunks)
+    uint64_t keep_cols = 0;
+    uint64_t *keep = nullptr;
 
     // background hand-off of the next proof's cm1_n (set_cm1_async)
     // (up to two row pieces: a shard's rows wrap around the domain end)
@@ -284,10 +290,34 @@ public:
         if (need > avail && lean_ok(why)) return set_mode(ZKGPU_MEM_LEAN);
         return 0;
     }
-    int set_mode(int m)
+    int set_mode(int m, bool device = true)
     {
         mem_mode = m;
-        if (m == ZKGPU_MEM_LEAN) find_unwritten();
+        if (m != ZKGPU_MEM_LEAN) return 0;
+        find_unwritten();
+        return device ? choose_keep() : 0;
+    }
+    // how many of cm1's extended columns the lean plan keeps from stage 1:
+    // as many as the free HBM left by the plan holds (4 GB or 2 % of the
+    // device spare), ZKGPU_LEAN_KEEP_COLS overriding (tests)
+    int choose_keep()
+    {
+        const uint64_t W1 = info.n_cm1;
+        keep_cols = 0;
+        uint64_t want = W1;
+        const char *e = getenv("ZKGPU_LEAN_KEEP_COLS");
+        if (e) {
+            want = std::min<uint64_t>(W1, strtoull(e, nullptr, 10));
+        } else {
+            uint64_t need = 0, avail = 0, total = 0;
+            if (plan(&need)) return -1;
+            CK(zkgpu_device_memory(&avail, &total));
+            const uint64_t spare = std::max<uint64_t>(4000000000ULL, total / 50);
+            want = avail > need + spare ? std::min<uint64_t>(W1, (avail - need - spare) / (NE * 8)) : 0;
+        }
+        const uint64_t split = W1 - want;
+        keep_cols = W1 - std::min<uint64_t>(W1, (split + 7) / 8 * 8);  // (W1 - keep) a multiple of 8
+        if (W1 <= 4) keep_cols = want == W1 ? W1 : 0;
         return 0;
     }
 
@@ -480,8 +510,9 @@ public:
             tmp_off = words;
             words += (WT + W2) * N;
         }
-        words = std::max(words, high + W1 * NE);  // cm1's stage-1 extension
+        words = std::max(words, high + (W1 - keep_cols) * NE);  // cm1's stage-1 extension (not kept)
         if (dalloc(&arena, words)) return -1;
+        if (keep_cols && dalloc(&keep, keep_cols * NE)) return -1;
         S.sec[SEC_CM1_N] = arena;
         S.sec[SEC_TMP_N] = arena + tmp_off;
         S.sec[SEC_CM2_N] = arena + tmp_off + WT * N;
@@ -693,8 +724,16 @@ public:
         t0_mark = UINT32_MAX;
         if (n_marks + 1 < ZKGPU_MARKS && !zkgpu_mark(n_marks)) t0_mark = n_marks++;
     }
+    // ZKGPU_SYNC_STAGES=1 (debugging): a device synchronisation at every
+    // stage end, so an asynchronous kernel fault is reported by the stage
+    // that launched it rather than at the proof's end (flush_timers)
+    bool sync_stages = [] {
+        const char *e = getenv("ZKGPU_SYNC_STAGES");
+        return e && atoi(e) != 0;
+    }();
     int tstop(const char *name)
     {
+        if (sync_stages && zkgpu_synchronize()) return fail("%s: %s", name, zkgpu_last_error());
         if (t0_mark != UINT32_MAX && n_marks < ZKGPU_MARKS && !zkgpu_mark(n_marks)) {
             pend_t.push_back({timers.size(), {t0_mark, n_marks++}});
             timers.emplace_back(name, 0.0);
@@ -753,6 +792,30 @@ public:
         return 0;
     }
 
+    // lean plan, stage 1: cm1's extension into the scratch above cm1_n
+    // (columns [0, split), hashed and dropped) and into `keep` (the rest,
+    // kept for stage 4), one tree over both regions
+    int commit_cm1_lean(Transcript &tr, uint64_t root[4])
+    {
+        const uint64_t W1 = info.n_cm1, split = W1 - keep_cols;
+        S.sec[SEC_CM1_2NS] = cm1_early;
+        tstart();
+        if (split) CK(zkgpu_gl_extend_pol_dev(cm1_early, NE, arena, N, NE, N, split));
+        if (keep_cols) CK(zkgpu_gl_extend_pol_dev(keep, NE, arena + split * N, N, NE, N, keep_cols));
+        if (tstop("STARK_STEP_1_LDE")) return -1;
+        tstart();
+        if (!keep_cols)
+            CK(zkgpu_gl_merkletree_dev(nodes[0], cm1_early, NE, W1, NE));
+        else if (!split)
+            CK(zkgpu_gl_merkletree_dev(nodes[0], keep, NE, W1, NE));
+        else
+            CK(zkgpu_gl_merkletree2_dev(nodes[0], cm1_early, keep, NE, split, W1, NE));
+        CK(zkgpu_memcpy_d2h(root, nodes[0] + zkgpu_gl_merkle_num_elements(NE) - 4, 32));
+        if (tstop("STARK_STEP_1_MERKLETREE")) return -1;
+        tr.put(root, 4);
+        return 0;
+    }
+
     // the proof of the current cm1_n; a trace queued by set_cm1_async (loaded
     // meanwhile) becomes cm1_n when it returns
     virtual int prove(uint64_t *out)
@@ -779,9 +842,12 @@ public:
         uint64_t roots[4][4];
         std::vector<uint64_t> evals(3 * info.n_ev);
         // STAGE 1 (starks.cpp:49-63)
-        if (lean()) S.sec[SEC_CM1_2NS] = cm1_early;  // hashed, then dropped (extended again at stage 4)
-        if (commit(0, SEC_CM1_N, SEC_CM1_2NS, info.n_cm1, tr, roots[0], "STARK_STEP_1_LDE", "STARK_STEP_1_MERKLETREE"))
+        if (lean()) {
+            if (commit_cm1_lean(tr, roots[0])) return -1;
+        } else if (commit(0, SEC_CM1_N, SEC_CM1_2NS, info.n_cm1, tr, roots[0], "STARK_STEP_1_LDE",
+                          "STARK_STEP_1_MERKLETREE")) {
             return -1;
+        }
         // lean: the regions of tmpExp_n / cm2_n / cm3_n held other sections;
         // the columns no stage writes read 0, as under the resident plan
         if (lean() && (zero_unwritten(SEC_TMP_N) || zero_unwritten(SEC_CM2_N) || zero_unwritten(SEC_CM3_N)))
@@ -819,10 +885,13 @@ public:
         // STAGE 4 (:226-296)
         tr.get_field(ch + 12);
         if (lean()) {
-            // cm1_2ns again, over cm1_n (tmpExp_n / cm2_n above it are dead)
+            // cm1_2ns again, over cm1_n (tmpExp_n / cm2_n above it are dead):
+            // the columns not kept extended in place, the kept ones copied
             tstart();
             cm1_consumed = true;
-            CK(zkgpu_gl_extend_pol_inplace_dev(arena, NE, N, info.n_cm1));
+            const uint64_t split = info.n_cm1 - keep_cols;
+            if (split) CK(zkgpu_gl_extend_pol_inplace_dev(arena, NE, N, split));
+            if (keep_cols) CK(zkgpu_memcpy_d2d(arena + split * NE, keep, keep_cols * NE * 8));
             S.sec[SEC_CM1_2NS] = arena;
             if (tstop("STARK_STEP_4_CM1_LDE")) return -1;
         }
@@ -1010,7 +1079,10 @@ public:
                 uint32_t nb = fri_steps[si + 1];
                 uint64_t ngroups = 1ULL << nb;
                 uint64_t width = (3ULL << fri_steps[si]) / ngroups;
-                if (fri_transpose_layer(si, fri_aux[si + 1], fri_pol[cur], 1ULL << fri_steps[si], nb)) return -1;
+                // (layer 0 of a prover that keeps f in row blocks: no whole
+                // fri_pol[0] exists, the override reads the blocks)
+                const uint64_t *pol = si == 0 && !fri_pol0_filled() ? nullptr : fri_pol[cur];
+                if (fri_transpose_layer(si, fri_aux[si + 1], pol, 1ULL << fri_steps[si], nb)) return -1;
                 if (fri_commit(si + 1, ngroups, width, &fri_roots[4 * (si + 1)])) return -1;
                 tr.put(&fri_roots[4 * (si + 1)], 4);
             } else {
@@ -1059,6 +1131,9 @@ public:
         CK(zkgpu_fri_fold_dev(dst, src, pol_bits, out_bits, sx, shift_inv));
         return 0;
     }
+    // whether fri_pol[0] holds the whole FRI polynomial when the FRI loop
+    // starts (the row-sharded prover keeps it in row blocks instead)
+    virtual bool fri_pol0_filled() const { return true; }
     // layer si + 1's tree rows: getTransposed of the 2^pol_bits-element
     // polynomial of step si into 2^nb groups (friProve.cpp:111-121)
     virtual int fri_transpose_layer(size_t si, uint64_t *aux, const uint64_t *pol, uint64_t degree, uint32_t nb)
@@ -1257,7 +1332,7 @@ int zkgpu_stark_memory_plan_ex(const zkgpu_stark_info *info, uint32_t memory_pla
     if (memory_plan == ZKGPU_MEM_LEAN) {
         std::string why;
         if (!s.lean_ok(why)) return zkgpu_host::fail("stark_memory_plan_ex: the lean plan does not apply: %s", why.c_str());
-        s.set_mode(ZKGPU_MEM_LEAN);
+        s.set_mode(ZKGPU_MEM_LEAN, false);  // (no device: no kept columns)
     }
     return s.plan(bytes);
 }

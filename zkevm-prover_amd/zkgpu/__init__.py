@@ -49,6 +49,7 @@ _SIGS = {
     "zkgpu_gl_extend_pol_dev": (ctypes.c_int, [vp, u64, vp, u64, u64, u64, u64]),
     "zkgpu_gl_extend_pol_inplace_dev": (ctypes.c_int, [vp, u64, u64, u64]),
     "zkgpu_set_lde_batch_cols": (None, [u64]),
+    "zkgpu_gl_merkletree2_dev": (ctypes.c_int, [vp, vp, vp, u64, u64, u64, u64]),
     "zkgpu_rows_to_cols_dev": (ctypes.c_int, [vp, u64, vp, u64, u64]),
     "zkgpu_cols_to_rows_dev": (ctypes.c_int, [vp, vp, u64, u64, u64]),
     "zkgpu_gl_poseidon_full": (ctypes.c_int, [vp, vp]),
@@ -369,6 +370,12 @@ def poseidon_batch_dev(out, src, n, full=True):
 
 def merkletree_dev(nodes, src, ld, ncols, nrows):
     _check(lib().zkgpu_gl_merkletree_dev(_addr(nodes), _addr(src), ld, ncols, nrows), "zkgpu_gl_merkletree_dev")
+
+
+def merkletree2_dev(nodes, src, src2, ld, split, ncols, nrows):
+    """tree of a section in two regions: columns [0, split) at src, the rest at src2"""
+    _check(lib().zkgpu_gl_merkletree2_dev(_addr(nodes), _addr(src), _addr(src2), ld, split, ncols, nrows),
+           "zkgpu_gl_merkletree2_dev")
 
 
 def merkletree_rows_dev(nodes, src, ncols, nrows):
