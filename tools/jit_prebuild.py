@@ -19,7 +19,7 @@ are compiled too, one process per program: their kernels are what the
 driver's bench runs, and the fork-9 ones take minutes of hiprtc that a rank
 must not spend inside its timed child.
 
-Usage: tools/jit_prebuild.py [--check] [--prune] [--quarter-only | --full-only] [-j N]
+Usage: tools/jit_prebuild.py [--check] [--prune] [--quarter-only | --full-only | --only SPEC,...] [-j N]
        (--check: report cache hits only; --prune: delete the cache entries
        this run neither found nor compiled -- a hit refreshes the entry's mtime)
 """
@@ -91,7 +91,9 @@ def main():
     jobs = int(sys.argv[sys.argv.index("-j") + 1]) if "-j" in sys.argv else min(16, os.cpu_count() or 1)
     scales = SCALES[:1] if "--quarter-only" in sys.argv else SCALES[1:] if "--full-only" in sys.argv else SCALES
     work = [("shaped:step42ns:%g" % sc, "step42ns-shaped (seed 1, scale %g)" % sc) for sc in scales]
-    if "--quarter-only" not in sys.argv:
+    if "--only" in sys.argv:  # e.g. --only shaped:step42ns:1 (A/B variants under an env switch)
+        work = [(sp, sp) for sp in sys.argv[sys.argv.index("--only") + 1].split(",")]
+    elif "--quarter-only" not in sys.argv:
         work += [("shaped:%s:1" % o, "%s-shaped (seed 1, scale 1)" % o) for o in OTHERS]
         if "--full-only" not in sys.argv:
             work += [("stark:%s:%s" % (i, p), "STARK %s %s" % (i, p)) for i, _ in STARKS for p in STARK_PROGS

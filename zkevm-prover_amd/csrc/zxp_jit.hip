@@ -524,6 +524,114 @@ static std::string expand_rows(const std::string &text, uint32_t rows)
     return out;
 }
 
+// Segment kernels (round 6, VERDICT r5 "next" 4):
+// 3 waves per SIMD, up to 22 LDS cache slots per lane (LDS budget 160 KB /
+// waves per workgroup) and the software prefetch below (16 loads per code
+// block).  zkEVM-shaped quotient at 2^24 rows: 49.9 -> 53.1 Mrow/s, HBM
+// traffic 1.70 -> 1.30 TB per pass (r06_seg_ab.json).  A/B switch:
+// ZKGPU_ZXP_SEG_AB="waves,slots,prefetch" (4,12,0 = the round-5 segments).
+struct SegAb {
+    uint32_t waves = 0, slots = 0, prefetch = 0;
+};
+static const SegAb &seg_ab()
+{
+    static const SegAb c = [] {
+        SegAb v;
+        if (const char *e = getenv("ZKGPU_ZXP_SEG_AB")) {
+            if (sscanf(e, "%u,%u,%u", &v.waves, &v.slots, &v.prefetch) != 3 || v.waves > 8) v = SegAb();
+        }
+        return v;
+    }();
+    return c;
+}
+
+// Software prefetch across code blocks (the SEG_AB experiment): the first
+// `pf` global column reads of every code block are issued at the start of the
+// block before it, into per-row registers (zpf<k>`), and read from there --
+// a column load then has a whole code block (~1 KB of source) to arrive
+// instead of the compiler's in-block scheduling window.  Loads stay
+// in flight across __syncthreads (it waits for LDS only).  Columns the kernel
+// stores to are never prefetched; a cached read (CS) keeps its slot store.
+// Returns the number of prefetch registers.
+static uint32_t prefetch_blocks(std::string &body, uint32_t pf)
+{
+    static const std::string head = "if (zk_one()) {\n";
+    std::vector<size_t> starts;
+    for (size_t q = body.find(head); q != std::string::npos; q = body.find(head, q + head.size()))
+        starts.push_back(q + head.size());
+    if (starts.size() < 2 || !pf) return 0;
+    auto ident = [](char c) {
+        return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_';
+    };
+    auto num = [&](size_t &q, int64_t &v) {
+        const char *b = body.c_str() + q;
+        char *e;
+        v = strtoll(b, &e, 10);
+        if (e == b) return false;
+        q += (size_t)(e - b);
+        return true;
+    };
+    std::set<int64_t> stored;
+    for (size_t q = body.find("ZK_ST"); q != std::string::npos; q = body.find("ZK_ST", q + 5)) {
+        size_t t = q + (body.compare(q, 7, "ZK_STS(") == 0 ? 7 : body.compare(q, 6, "ZK_ST(") == 0 ? 6 : 0);
+        int64_t j;
+        if (t > q && num(t, j)) stored.insert(j);
+    }
+    struct Edit {
+        size_t pos, len;
+        std::string text;
+    };
+    std::vector<Edit> edits;  // replacements and insertions, by position
+    uint32_t n = 0;
+    for (size_t b = 1; b < starts.size(); b++) {
+        const size_t lo = starts[b], hi = b + 1 < starts.size() ? starts[b + 1] - head.size() : body.size();
+        std::string loads;
+        uint32_t taken = 0;
+        for (size_t q = lo; q < hi && taken < pf; q++) {
+            if (body[q] != 'C' || ident(body[q - 1])) continue;
+            const bool cs = body.compare(q, 3, "CS(") == 0;
+            if (!cs && body.compare(q, 2, "C(") != 0) continue;
+            size_t t = q + (cs ? 3 : 2);
+            int64_t j, sh, slot = 0;
+            if (!num(t, j) || body[t] != ',') continue;
+            t++;
+            if (!num(t, sh) || body.compare(t, 3, ",i`") != 0) continue;
+            t += 3;
+            if (cs) {
+                if (body[t] != ',') continue;
+                t++;
+                if (!num(t, slot) || body.compare(t, 3, ",~)") != 0) continue;
+                t += 3;
+            } else {
+                if (body[t] != ')') continue;
+                t++;
+            }
+            if (stored.count(j)) continue;
+            std::string var = "zpf";
+            app_num(var, n);
+            var += '`';
+            loads += var + " = C(";
+            loads += std::to_string(j) + "," + std::to_string(sh) + ",i`);\n";
+            edits.push_back({q, t - q, cs ? "CSV(" + var + "," + std::to_string(slot) + ",~)" : var});
+            n++;
+            taken++;
+        }
+        if (!loads.empty()) edits.push_back({starts[b - 1], 0, loads});
+    }
+    std::stable_sort(edits.begin(), edits.end(), [](const Edit &x, const Edit &y) { return x.pos < y.pos; });
+    std::string out;
+    out.reserve(body.size() + n * 40);
+    size_t at = 0;
+    for (const Edit &e : edits) {
+        out.append(body, at, e.pos - at);
+        out += e.text;
+        at = e.pos + e.len;
+    }
+    out.append(body, at, std::string::npos);
+    body.swap(out);
+    return n;
+}
+
 // Compiler-managed LDS column cache for block-split programs.  A large
 // program's kernel is HBM-bound on re-reads: it loads a column again at every
 // use, and a re-read hits the 4 MB L2 of an XCD only within ~16 columns (512
@@ -1558,21 +1666,27 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     // 32-bit column offsets from scalar bases (64-bit addresses, the round-3
     // form: 44.6 against 46.3 Mrow/s on the zkEVM-sized quotient)
     src += "#define ZKJIT_SADDR 1\n";
+    uint32_t n_prefetch = 0;
     {
         // LDS column cache (lds_column_cache): block-split programs, 12
         // slots per lane and row (LDS: 2 KB per slot, row and workgroup; 16
         // slots measured +2 % on one box, -5 % on another)
-        constexpr int lslots = 12, lgap = 0;
+        const SegAb &ab = seg_ab();
+        const bool seg = split && in.force_split;  // a segment (zxp_segment)
+        const uint32_t seg_w = in.waves_per_eu ? in.waves_per_eu : 4;
+        const int lslots = seg ? (ab.waves ? (int)ab.slots : 22) : 12, lgap = 0;
         // LDS budget of one workgroup (64 KB): the limb double buffer (kbuf)
         // or the whole limb table, then as many cache slots as still fit
         // (none: the uncached source)
         const size_t lds_limbs = kchunk ? 2 * JIT_KCHUNK * 4 : (jit_kl_lds(kl.size()) ? kl.size() * 4 : 0);
         const size_t slot_bytes = (size_t)rows * 256 * 8;
-        const size_t lds_budget = 64 * 1024;
+        const size_t lds_budget = seg ? 160 * 1024 / seg_w : 64 * 1024;
         const int fit = lds_limbs >= lds_budget ? 0 : (int)((lds_budget - lds_limbs) / slot_bytes);
         const int slots = std::min(lslots, fit);
         const bool lc = split && slots > 0 && lds_column_cache(body, slots, lgap) > 0;
         appendf(src, "#define ZKJIT_LCACHE %d\n", lc ? slots : 0);
+        n_prefetch = seg ? prefetch_blocks(body, ab.waves ? ab.prefetch : 16) : 0;
+        if (n_prefetch) src += "#define CSV(v, s, r) zk_cs(zkc_ + ((s) * ZKJIT_ROWS + (r)) * 256, (v))\n";
     }
     src += k_kernel_head;
     // per-row text carries a ` (-> _r) and ~ (-> r) on its line; expand()
@@ -1597,6 +1711,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         }
     }
     for (uint32_t r = 0; r < wcell.size(); r++) appendf(decl, "uint64_t w%u` = 0;\n", r);
+    for (uint32_t r = 0; r < n_prefetch; r++) appendf(decl, "uint64_t zpf%u`;\n", r);
     if (uses_x)
         appendf(decl, "const uint64_t ex_` = i` << (%u - p.logomega);\n"
                      "const uint64_t xv` = gl_mul(p.x_start, gl_mul(gload(p.tw_lo + (ex_` & %lluULL)), gload(p.tw_hi + (ex_` >> %u))));\n",
@@ -1983,17 +2098,14 @@ int build_kernels(const ZxpJitIn &in, std::vector<JitKernel> &ks, const std::fun
         J.n_opnd = (uint32_t)seg[j].opnd.size();
         J.terms = seg[j].term.data();
         J.force_split = 1;
-        // occupancy target of a segment (seg_waves, 4 waves per SIMD = 128
-        // VGPRs): zkEVM-sized quotient at 2^24 rows 0.57 s with the compiler's
-        // choice (~250 VGPRs), 0.55 s at 4 waves
+        // occupancy target of a segment (seg_waves): 3 waves per SIMD (168
+        // VGPRs) since round 6, with the larger LDS cache and the prefetch
+        // (seg_ab above; round 5: 4 waves, 12 slots, spills <= 348 bytes).
         // A segment whose code spills more than spill_max bytes per lane
         // (300) at that target is compiled again one wave
         // lower (down to 2): the reference's step3 segments spill 324-452
-        // bytes at 4 waves, none at 2.  Small spills stay: on the synthetic
-        // quotient (<= 272 bytes) 4 waves with spills ran 0.54 s, the
-        // spill-free lower targets 0.58 s -- it is HBM-bound, occupancy buys
-        // bandwidth.
-        constexpr uint32_t seg_waves = 4;
+        // bytes at 4 waves, none at 2.
+        const uint32_t seg_waves = seg_ab().waves ? seg_ab().waves : 3;
         constexpr uint64_t spill_max = 300;
         const bool fixed = J.waves_per_eu != 0;
         J.scratch = scr;

@@ -31,7 +31,7 @@ ENV = {
     # the compiler's fusion / term cap change the compiled programs (ZKGPU_ZXP_JIT,
     # interpreter vs compiled, is not one: the profiled workloads pick the
     # compiled kernels themselves, bench.py --s42-jit)
-    "zxp": ["ZKGPU_ZXP_FUSE", "ZKGPU_ZXP_MAX_TERMS"],
+    "zxp": ["ZKGPU_ZXP_FUSE", "ZKGPU_ZXP_MAX_TERMS", "ZKGPU_ZXP_SEG_AB"],
 }
 
 
