@@ -190,6 +190,7 @@ public:
     // keep_cols) is a multiple of 8 (the linear hash's chunks)
     uint64_t keep_cols = 0;
     uint64_t *keep = nullptr;
+    bool lowered_lde_batch = false;  // choose_keep set the process-wide LDE batch (restored at destruction)
 
     // background hand-off of the next proof's cm1_n (set_cm1_async)
     // (up to two row pieces: a shard's rows wrap around the domain end)
@@ -200,6 +201,7 @@ public:
 
     virtual ~Starks()
     {
+        if (lowered_lde_batch) zkgpu_set_lde_batch_cols(0);
         for (void *t : cm1_ticket) (void)zkgpu_load_wait(t);
         for (void *p : allocs) zkgpu_dev_free(p);
     }
@@ -299,7 +301,13 @@ public:
     }
     // how many of cm1's extended columns the lean plan keeps from stage 1:
     // as many as the free HBM left by the plan holds (4 GB or 2 % of the
-    // device spare), ZKGPU_LEAN_KEEP_COLS overriding (tests)
+    // device spare), ZKGPU_LEAN_KEEP_COLS overriding (tests).  When not all
+    // fit, LDE batches of 32 columns instead of the default 128 at 2^24 rows
+    // free 19 GB of workspace for ~144 more kept columns: the LDE rate drops
+    // ~1.2 % (tools/lde_batch_ab.py, profiles/r06_lde_batch_ab.json), the
+    // stage-4 re-extension loses a fifth of its columns.  The batch is a
+    // process-wide setting (zkgpu_set_lde_batch_cols), restored to the
+    // default when this prover is destroyed.
     int choose_keep()
     {
         const uint64_t W1 = info.n_cm1;
@@ -309,11 +317,26 @@ public:
         if (e) {
             want = std::min<uint64_t>(W1, strtoull(e, nullptr, 10));
         } else {
-            uint64_t need = 0, avail = 0, total = 0;
-            if (plan(&need)) return -1;
+            uint64_t avail = 0, total = 0;
             CK(zkgpu_device_memory(&avail, &total));
             const uint64_t spare = std::max<uint64_t>(4000000000ULL, total / 50);
-            want = avail > need + spare ? std::min<uint64_t>(W1, (avail - need - spare) / (NE * 8)) : 0;
+            auto fits = [&](uint64_t cap, uint64_t &cols) {
+                uint64_t need = 0;
+                lde_batch_cap = cap;
+                if (plan(&need)) return -1;
+                cols = avail > need + spare ? std::min<uint64_t>(W1, (avail - need - spare) / (NE * 8)) : 0;
+                return 0;
+            };
+            if (fits(0, want)) return -1;
+            uint64_t want32 = 0;
+            if (want < W1 && fits(32, want32)) return -1;
+            if (want < W1 && want32 > want) {
+                want = want32;
+                zkgpu_set_lde_batch_cols(32);
+                lowered_lde_batch = true;
+            } else {
+                lde_batch_cap = 0;
+            }
         }
         const uint64_t split = W1 - want;
         keep_cols = W1 - std::min<uint64_t>(W1, (split + 7) / 8 * 8);  // (W1 - keep) a multiple of 8
