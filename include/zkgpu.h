@@ -86,7 +86,8 @@ int zkgpu_gl_extend_pol_dev(uint64_t *out, uint64_t ld_out, const uint64_t *in, 
  * run from the last down, each read whole into the LDE workspace before its
  * output is stored, so no column is overwritten before it is read; lets a
  * prover extend a section into the memory its n-domain values occupied
- * (host/starks.cpp, the lean memory plan). */
+ * (host/starks.cpp, the lean memory plan).  Same values as extendPol
+ * (starks.cpp:53,134,215) out of place. */
 int zkgpu_gl_extend_pol_inplace_dev(uint64_t *base, uint64_t n_ext, uint64_t n, uint64_t ncols);
 /* row-major <-> column-major on device (boundary layout change) */
 int zkgpu_rows_to_cols_dev(uint64_t *cols, uint64_t ld, const uint64_t *rows, uint64_t nrows, uint64_t ncols);
@@ -122,7 +123,8 @@ int zkgpu_gl_merkletree_dev(uint64_t *nodes, const uint64_t *src, uint64_t ld, u
 /* the same tree over a section held in two regions: columns [0, split) at
  * src + c*ld, columns [split, ncols) at src2 + (c - split)*ld (split a
  * multiple of 8: the linear hash absorbs 8 columns at a time).  The lean
- * memory plan's stage-1 commit (host/starks.cpp). */
+ * memory plan's stage-1 commit (host/starks.cpp); same nodes as the
+ * reference's merkelize of the whole section (merkleTreeGL.cpp:37-44). */
 int zkgpu_gl_merkletree2_dev(uint64_t *nodes, const uint64_t *src, const uint64_t *src2, uint64_t ld, uint64_t split,
                              uint64_t ncols, uint64_t nrows);
 /* device-resident, row-major source (FRI trees: friProve.cpp:117-121) */
