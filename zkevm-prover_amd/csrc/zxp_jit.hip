@@ -525,20 +525,22 @@ static std::string expand_rows(const std::string &text, uint32_t rows)
 }
 
 // Segment kernels (round 6, VERDICT r5 "next" 4):
-// 3 waves per SIMD, up to 22 LDS cache slots per lane (LDS budget 160 KB /
-// waves per workgroup) and the software prefetch below (16 loads per code
-// block).  zkEVM-shaped quotient at 2^24 rows: 49.9 -> 53.1 Mrow/s, HBM
-// traffic 1.70 -> 1.30 TB per pass (r06_seg_ab.json).  A/B switch:
-// ZKGPU_ZXP_SEG_AB="waves,slots,prefetch" (4,12,0 = the round-5 segments).
+// 512-byte code blocks, up to 16 LDS cache slots per lane (LDS budget
+// 160 KB / waves per workgroup, 4 waves per SIMD) and the software prefetch
+// below (16 loads, one block ahead).  zkEVM-shaped quotient at 2^24 rows:
+// 49.9 -> 56.1 Mrow/s (r06_seg_ab.json).  A/B switch:
+// ZKGPU_ZXP_SEG_AB="waves,slots,prefetch[,block bytes[,blocks ahead]]"
+// (4,12,0,1024,1 = the round-5 segments).
 struct SegAb {
-    uint32_t waves = 0, slots = 0, prefetch = 0;
+    uint32_t waves = 0, slots = 0, prefetch = 0, block = 0, dist = 0;  // block / dist: 0 = the default
 };
 static const SegAb &seg_ab()
 {
     static const SegAb c = [] {
         SegAb v;
         if (const char *e = getenv("ZKGPU_ZXP_SEG_AB")) {
-            if (sscanf(e, "%u,%u,%u", &v.waves, &v.slots, &v.prefetch) != 3 || v.waves > 8) v = SegAb();
+            if (sscanf(e, "%u,%u,%u,%u,%u", &v.waves, &v.slots, &v.prefetch, &v.block, &v.dist) < 3 || v.waves > 8)
+                v = SegAb();
         }
         return v;
     }();
@@ -553,7 +555,7 @@ static const SegAb &seg_ab()
 // in flight across __syncthreads (it waits for LDS only).  Columns the kernel
 // stores to are never prefetched; a cached read (CS) keeps its slot store.
 // Returns the number of prefetch registers.
-static uint32_t prefetch_blocks(std::string &body, uint32_t pf)
+static uint32_t prefetch_blocks(std::string &body, uint32_t pf, uint32_t dist = 1)
 {
     static const std::string head = "if (zk_one()) {\n";
     std::vector<size_t> starts;
@@ -616,7 +618,7 @@ static uint32_t prefetch_blocks(std::string &body, uint32_t pf)
             n++;
             taken++;
         }
-        if (!loads.empty()) edits.push_back({starts[b - 1], 0, loads});
+        if (!loads.empty()) edits.push_back({starts[b >= dist ? b - dist : 0], 0, loads});
     }
     std::stable_sort(edits.begin(), edits.end(), [](const Edit &x, const Edit &y) { return x.pos < y.pos; });
     std::string out;
@@ -1335,7 +1337,9 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
     // step42ns-shaped program at 2^24 rows, 256 / 512 / 1024 / 4096 bytes ->
     // 184 / 246 / 246 / 512+spills VGPRs, 453 / 359 / 303 / 394 ms, hiprtc
     // 63 / 56 / 80 / 116 s.
-    constexpr size_t block = 1024;  // source bytes per block
+    // source bytes per block (segments: 512, round 6 -- paired with the
+    // prefetch: without it the 512-byte segments ran 8 % slower)
+    const size_t block = in.force_split ? (seg_ab().block ? seg_ab().block : 512) : 1024;
     // Limb chunks in LDS: a split program whose limb
     // table is too large for LDS reads it from global memory, one wave-uniform
     // 16 + 8-byte vector load pair per term, each taking the texture
@@ -1674,7 +1678,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         const SegAb &ab = seg_ab();
         const bool seg = split && in.force_split;  // a segment (zxp_segment)
         const uint32_t seg_w = in.waves_per_eu ? in.waves_per_eu : 4;
-        const int lslots = seg ? (ab.waves ? (int)ab.slots : 22) : 12, lgap = 0;
+        const int lslots = seg ? (ab.waves ? (int)ab.slots : 16) : 12, lgap = 0;
         // LDS budget of one workgroup (64 KB): the limb double buffer (kbuf)
         // or the whole limb table, then as many cache slots as still fit
         // (none: the uncached source)
@@ -1685,7 +1689,7 @@ int zxp_jit_build_source(const ZxpJitIn &in, std::string &src, std::vector<const
         const int slots = std::min(lslots, fit);
         const bool lc = split && slots > 0 && lds_column_cache(body, slots, lgap) > 0;
         appendf(src, "#define ZKJIT_LCACHE %d\n", lc ? slots : 0);
-        n_prefetch = seg ? prefetch_blocks(body, ab.waves ? ab.prefetch : 16) : 0;
+        n_prefetch = seg ? prefetch_blocks(body, ab.waves ? ab.prefetch : 16, ab.dist ? ab.dist : 1) : 0;
         if (n_prefetch) src += "#define CSV(v, s, r) zk_cs(zkc_ + ((s) * ZKJIT_ROWS + (r)) * 256, (v))\n";
     }
     src += k_kernel_head;
@@ -2098,14 +2102,14 @@ int build_kernels(const ZxpJitIn &in, std::vector<JitKernel> &ks, const std::fun
         J.n_opnd = (uint32_t)seg[j].opnd.size();
         J.terms = seg[j].term.data();
         J.force_split = 1;
-        // occupancy target of a segment (seg_waves): 3 waves per SIMD (168
-        // VGPRs) since round 6, with the larger LDS cache and the prefetch
-        // (seg_ab above; round 5: 4 waves, 12 slots, spills <= 348 bytes).
+        // occupancy target of a segment (seg_waves): 4 waves per SIMD (128
+        // VGPRs; the 512-byte blocks keep fewer values live than the round-5
+        // 1024-byte ones, which spilled up to 348 bytes with the prefetch).
         // A segment whose code spills more than spill_max bytes per lane
         // (300) at that target is compiled again one wave
         // lower (down to 2): the reference's step3 segments spill 324-452
         // bytes at 4 waves, none at 2.
-        const uint32_t seg_waves = seg_ab().waves ? seg_ab().waves : 3;
+        const uint32_t seg_waves = seg_ab().waves ? seg_ab().waves : 4;
         constexpr uint64_t spill_max = 300;
         const bool fixed = J.waves_per_eu != 0;
         J.scratch = scr;
