@@ -1014,6 +1014,7 @@ def main():
     res = {"metric": METRIC}
     gs = inst = None
     prepare = None
+    lean = False
     sharded = None
     lde = roof = handoff = quotient = None
     if args.workload == "lde":
@@ -1071,9 +1072,17 @@ def main():
         else:
             value, unit, hib = n * C * world * args.steps / elapsed / 1e9, "Gelem/s", True
         stages = gs.timers() if gs is not None else None
+        lean = prepare is not None
+        if lean:
+            # a lean prover holds what the HBM had to spare (its kept columns):
+            # release it (and the bound witness method holding it) before the
+            # LDE line allocates
+            gs = prepare = step = None
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
         if args.workload == "stark" and not args.no_lde:
             lde, roof = lde_measure(args, dev, torch, world, dist)
-        if args.workload == "stark" and world == 1 and not args.no_handoff and prepare is None:
+        if args.workload == "stark" and world == 1 and not args.no_handoff and not lean:
             handoff = handoff_measure(n, inst.n_cm1, dev, torch, zkgpu, value)
             handoff["pipelined"] = handoff_pipelined(gs, value)
         if args.workload == "stark" and world == 1 and args.log_n == 23 and not args.no_s42:
@@ -1146,7 +1155,7 @@ def main():
                            len(inst.evmap),
                            "lean (sections share one arena by lifetime, cm1 / cm3 extended in place; the proof consumes "
                            "its trace, so each timed proof gets a fresh one from the executor stand-in outside its "
-                           "own barrier + synchronize bracket)" if prepare else "resident"))
+                           "own barrier + synchronize bracket)" if lean else "resident"))
             one = (sharded or {}).get("config4") or {}
             parallelism = ("replicas x%d (one independent proof per GPU)" % world if world == 1 or scaling == "weak"
                            else "ONE proof row-sharded x%d (sharded_one_proof.config4: C++ prover, %s exchange of "
